@@ -1,0 +1,259 @@
+// rh_abi.hip -- the extern "C" boundary of librafthip.so (declared in include/rafthip.h).
+//
+// Host-side responsibilities only: argument validation, the per-context device copy of
+// the design descriptors, kernel configuration and error translation.  No numerics here.
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rh_device.h"
+
+#include "rh_kernels.hip"   // single translation unit: kernels + their host launchers
+
+struct rh_ctx {
+  int device = 0;
+  rh::DevDesign* d_designs = nullptr;   // device copy of the descriptor array
+  rh::DevDesign* h_designs = nullptr;   // pinned staging
+  int cap = 0;
+  hipEvent_t staged = nullptr;          // last copy out of h_designs
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define RH_HIP(call)                                                                     \
+  do {                                                                                   \
+    hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess) return fail(RH_EHIP, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int kThreads = 256;
+constexpr int kMaxNodes = 1024;
+
+int check_design(const rh_design& d, bool need_tables) {
+  if (d.nw < 2 || d.nw > 2048) return fail(RH_EINVAL, "nw=%d outside [2, 2048]", d.nw);
+  if (d.nn < 0 || d.nn > kMaxNodes) return fail(RH_EINVAL, "nn=%d outside [0, %d]", d.nn, kMaxNodes);
+  if (!d.w || !d.k || (d.nn > 0 && !d.node)) return fail(RH_EINVAL, "design: null w/k/node table");
+  if (!d.M || !d.B || !d.C) return fail(RH_EINVAL, "design: null M/B/C");
+  if (need_tables && (!d.uhat || !d.finer || d.nhead < 1))
+    return fail(RH_EINVAL, "design: wave tables missing (call rh_wave_tables first)");
+  if (!(d.dw > 0)) return fail(RH_EINVAL, "design: dw must be > 0");
+  return RH_OK;
+}
+
+int stage_designs(rh_ctx* ctx, const rh_design* designs, int n, hipStream_t s) {
+  if (n > ctx->cap) {
+    if (ctx->staged) RH_HIP(hipEventSynchronize(ctx->staged));
+    if (ctx->d_designs) RH_HIP(hipFree(ctx->d_designs));
+    if (ctx->h_designs) RH_HIP(hipHostFree(ctx->h_designs));
+    int cap = n < 64 ? 64 : n;
+    RH_HIP(hipMalloc(&ctx->d_designs, sizeof(rh::DevDesign) * cap));
+    RH_HIP(hipHostMalloc(&ctx->h_designs, sizeof(rh::DevDesign) * cap, hipHostMallocDefault));
+    ctx->cap = cap;
+  }
+  if (ctx->staged) RH_HIP(hipEventSynchronize(ctx->staged));  // previous copy has left the staging buffer
+  for (int i = 0; i < n; ++i) ctx->h_designs[i].d = designs[i];
+  RH_HIP(hipMemcpyAsync(ctx->d_designs, ctx->h_designs, sizeof(rh::DevDesign) * n, hipMemcpyHostToDevice, s));
+  RH_HIP(hipEventRecord(ctx->staged, s));
+  return RH_OK;
+}
+
+int nb_for(int nw) {
+  if (nw <= 256) return 1;
+  if (nw <= 512) return 2;
+  if (nw <= 1024) return 4;
+  return 8;
+}
+}  // namespace
+
+extern "C" {
+
+const char* rh_last_error(void) { return g_err.c_str(); }
+
+int rh_version(void) { return 1; }
+
+int rh_ctx_create(int device, rh_ctx** out) {
+  if (!out) return fail(RH_EINVAL, "rh_ctx_create: null out");
+  int n = 0;
+  RH_HIP(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(RH_EINVAL, "device %d not present (%d visible)", device, n);
+  RH_HIP(hipSetDevice(device));
+  rh_ctx* c = new rh_ctx;
+  c->device = device;
+  hipError_t e = hipEventCreateWithFlags(&c->staged, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(RH_EHIP, "hipEventCreate: %s", hipGetErrorString(e));
+  }
+  *out = c;
+  return RH_OK;
+}
+
+int rh_ctx_destroy(rh_ctx* ctx) {
+  if (!ctx) return RH_OK;
+  if (ctx->staged) {
+    (void)hipEventSynchronize(ctx->staged);
+    (void)hipEventDestroy(ctx->staged);
+  }
+  if (ctx->d_designs) (void)hipFree(ctx->d_designs);
+  if (ctx->h_designs) (void)hipHostFree(ctx->h_designs);
+  delete ctx;
+  return RH_OK;
+}
+
+int rh_wave_tables(rh_ctx* ctx, const rh_design* d, const double* beta, rh_c128* uhat, rh_c128* finer,
+                   rh_stream stream) {
+  if (!ctx || !d || !beta || !uhat || !finer) return fail(RH_EINVAL, "rh_wave_tables: null argument");
+  if (int r = check_design(*d, false)) return r;
+  if (d->nhead < 1) return fail(RH_EINVAL, "rh_wave_tables: nhead must be >= 1");
+  RH_HIP(hipSetDevice(ctx->device));
+  dim3 grid((d->nw + 127) / 128, d->nhead);
+  hipLaunchKernelGGL(rh::k_wave_tables, grid, dim3(128), 0, (hipStream_t)stream, *d, beta, uhat, finer);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
+int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_cases* cases,
+                   const rh_solve_out* out, rh_stream stream) {
+  if (!ctx || !designs || !cases || !out) return fail(RH_EINVAL, "rh_solve_cases: null argument");
+  if (ndesign < 1) return fail(RH_EINVAL, "rh_solve_cases: ndesign=%d", ndesign);
+  if (cases->ncase < 0) return fail(RH_EINVAL, "rh_solve_cases: ncase=%d", cases->ncase);
+  if (cases->ncase == 0) return RH_OK;
+  if (!cases->design || !cases->head || !cases->spectrum || !cases->Hs || !cases->Tp || !cases->gamma)
+    return fail(RH_EINVAL, "rh_solve_cases: null case array");
+  if (!out->Xi || !out->Xi_last || !out->iters || !out->status)
+    return fail(RH_EINVAL, "rh_solve_cases: Xi, Xi_last, iters and status outputs are required");
+  if (cases->nIter < 0) return fail(RH_EINVAL, "rh_solve_cases: nIter=%d", cases->nIter);
+  const int nw = designs[0].nw;
+  int nnmax = 0;
+  for (int i = 0; i < ndesign; ++i) {
+    if (int r = check_design(designs[i], true)) return r;
+    if (designs[i].nw != nw) return fail(RH_EINVAL, "rh_solve_cases: all designs must share nw");
+    if (designs[i].nn > nnmax) nnmax = designs[i].nn;
+  }
+  if (out->Bmat && ndesign > 1) {
+    for (int i = 0; i < ndesign; ++i)
+      if (designs[i].nn != nnmax) return fail(RH_EINVAL, "rh_solve_cases: Bmat output needs equal nn across designs");
+  }
+  RH_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
+  rh::CaseArgs a;
+  a.designs = ctx->d_designs;
+  a.c = *cases;
+  a.o = *out;
+  const size_t smem = sizeof(double) * (size_t)((kThreads / 64) * nnmax * 3 + nnmax * 9 + 36 + (kThreads / 64) * 6 + 108);
+  dim3 grid(cases->ncase), block(kThreads);
+  switch (nb_for(nw)) {
+    case 1: hipLaunchKernelGGL(rh::k_solve_cases<1>, grid, block, smem, s, a); break;
+    case 2: hipLaunchKernelGGL(rh::k_solve_cases<2>, grid, block, smem, s, a); break;
+    case 4: hipLaunchKernelGGL(rh::k_solve_cases<4>, grid, block, smem, s, a); break;
+    default: hipLaunchKernelGGL(rh::k_solve_cases<8>, grid, block, smem, s, a); break;
+  }
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
+int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int ncase, const int* design_idx,
+                        const int* head, const double* zeta, const double* B_drag, const double* Bmat, rh_c128* Xi,
+                        rh_stream stream) {
+  if (!ctx || !designs || !design_idx || !head || !zeta || !B_drag || !Bmat || !Xi)
+    return fail(RH_EINVAL, "rh_heading_response: null argument");
+  if (ncase <= 0) return ncase == 0 ? RH_OK : fail(RH_EINVAL, "ncase=%d", ncase);
+  const int nw = designs[0].nw;
+  int nnmax = 0;
+  for (int i = 0; i < ndesign; ++i) {
+    if (int r = check_design(designs[i], true)) return r;
+    if (designs[i].nw != nw) return fail(RH_EINVAL, "rh_heading_response: all designs must share nw");
+    if (designs[i].nn > nnmax) nnmax = designs[i].nn;
+  }
+  RH_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
+  rh::HeadArgs a{ctx->d_designs, ncase, design_idx, head, zeta, B_drag, Bmat, Xi};
+  const size_t smem = sizeof(double) * (size_t)(nnmax * 9 + 36 + 108);
+  dim3 grid((nw + kThreads - 1) / kThreads, ncase);
+  hipLaunchKernelGGL(rh::k_heading_resp, grid, dim3(kThreads), smem, s, a);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
+int rh_linearize(rh_ctx* ctx, const rh_design* d, int head, const rh_c128* Xi, const double* zeta, double* B_drag,
+                 double* Bmat, rh_c128* F_drag, rh_stream stream) {
+  if (!ctx || !d || !Xi || !zeta || !B_drag || !Bmat) return fail(RH_EINVAL, "rh_linearize: null argument");
+  if (int r = check_design(*d, true)) return r;
+  if (head < 0 || head >= d->nhead) return fail(RH_EINVAL, "rh_linearize: head %d out of range", head);
+  RH_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (d->nn > 0) hipLaunchKernelGGL(rh::k_lin_sums, dim3(d->nn), dim3(kThreads), 0, s, *d, head, Xi, zeta, Bmat);
+  RH_HIP(hipGetLastError());
+  hipLaunchKernelGGL(rh::k_lin_bdrag, dim3(1), dim3(64), 0, s, *d, (const double*)Bmat, B_drag);
+  RH_HIP(hipGetLastError());
+  if (F_drag) return rh_drag_excitation(ctx, d, head, zeta, Bmat, F_drag, stream);
+  return RH_OK;
+}
+
+int rh_drag_excitation(rh_ctx* ctx, const rh_design* d, int head, const double* zeta, const double* Bmat,
+                       rh_c128* F_drag, rh_stream stream) {
+  if (!ctx || !d || !zeta || !Bmat || !F_drag) return fail(RH_EINVAL, "rh_drag_excitation: null argument");
+  if (int r = check_design(*d, true)) return r;
+  if (head < 0 || head >= d->nhead) return fail(RH_EINVAL, "rh_drag_excitation: head %d out of range", head);
+  RH_HIP(hipSetDevice(ctx->device));
+  const size_t smem = sizeof(double) * (size_t)(d->nn * 9 + 2);
+  hipLaunchKernelGGL(rh::k_drag_exc, dim3((d->nw + kThreads - 1) / kThreads), dim3(kThreads), smem,
+                     (hipStream_t)stream, *d, head, zeta, Bmat, F_drag);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
+int rh_sea_state(rh_ctx* ctx, int ncase, int nw, const double* w, double dw, const int* spectrum, const double* Hs,
+                 const double* Tp, const double* gamma, double* S, double* zeta, rh_stream stream) {
+  if (!ctx || !w || !spectrum || !Hs || !Tp || !gamma || !zeta) return fail(RH_EINVAL, "rh_sea_state: null argument");
+  if (ncase < 0 || nw <= 0 || !(dw > 0)) return fail(RH_EINVAL, "rh_sea_state: bad sizes");
+  if (ncase == 0) return RH_OK;
+  RH_HIP(hipSetDevice(ctx->device));
+  dim3 grid((nw + 255) / 256, ncase);
+  hipLaunchKernelGGL(rh::k_sea_state, grid, dim3(256), 0, (hipStream_t)stream, nw, w, dw, spectrum, Hs, Tp, gamma, S,
+                     zeta);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
+int rh_motion_stats(rh_ctx* ctx, int ncase, int nrow, int nw, double dw, const rh_c128* Xi, double* psd, double* std_,
+                    rh_stream stream) {
+  if (!ctx || !Xi) return fail(RH_EINVAL, "rh_motion_stats: null argument");
+  if (ncase <= 0 || nrow <= 0 || nw <= 0 || !(dw > 0)) return fail(RH_EINVAL, "rh_motion_stats: bad sizes");
+  RH_HIP(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(rh::k_motion_stats, dim3(ncase), dim3(kThreads), 0, (hipStream_t)stream, nrow, nw, dw, Xi, psd,
+                     std_);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
+int rh_system_solve(rh_ctx* ctx, int nf, int nw, const rh_c128* Z, const double* K, const rh_c128* F, rh_c128* Xi,
+                    rh_stream stream) {
+  if (!ctx || !Z || !F || !Xi) return fail(RH_EINVAL, "rh_system_solve: null argument");
+  if (nw <= 0) return fail(RH_EINVAL, "rh_system_solve: nw=%d", nw);
+  if (nf < 1 || nf > 2) return fail(RH_EINVAL, "rh_system_solve: nf=%d (supported: 1, 2)", nf);
+  RH_HIP(hipSetDevice(ctx->device));
+  const int N = 6 * nf;
+  const size_t smem = sizeof(double) * 2 * (size_t)(N * N + N) * rh::kSysThreads;
+  dim3 grid((nw + rh::kSysThreads - 1) / rh::kSysThreads);
+  hipLaunchKernelGGL(rh::k_system_solve, grid, dim3(rh::kSysThreads), smem, (hipStream_t)stream, N, nw, Z, K, F, Xi);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+// rh_device.h -- device-side building blocks for librafthip (gfx950, FP64 VALU).
+//
+// Complex FP64 arithmetic in the order NumPy uses it, the register-resident partially
+// pivoted LU solve that replaces LAPACK zgesv (numpy.linalg.solve, raft/raft_model.py:947)
+// and wavefront reductions for 64-lane waves.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "../../include/rafthip.h"
+
+namespace rh {
+
+struct cd {
+  double r, i;
+};
+
+__device__ __forceinline__ cd mk(double r, double i) { return cd{r, i}; }
+__device__ __forceinline__ cd ld(const rh_c128* p) {
+  const double2 v = *reinterpret_cast<const double2*>(p);
+  return cd{v.x, v.y};
+}
+__device__ __forceinline__ void st(rh_c128* p, cd v) {
+  *reinterpret_cast<double2*>(p) = make_double2(v.r, v.i);
+}
+__device__ __forceinline__ cd add(cd a, cd b) { return cd{a.r + b.r, a.i + b.i}; }
+__device__ __forceinline__ cd sub(cd a, cd b) { return cd{a.r - b.r, a.i - b.i}; }
+__device__ __forceinline__ cd mul(cd a, cd b) { return cd{a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r}; }
+__device__ __forceinline__ cd scl(cd a, double s) { return cd{a.r * s, a.i * s}; }
+// i*w*a  (NumPy: (1j*w)*a = (0,w)*(ar,ai))
+__device__ __forceinline__ cd iw(double w, cd a) { return cd{-w * a.i, w * a.r}; }
+__device__ __forceinline__ double abs2(cd a) { return a.r * a.r + a.i * a.i; }
+__device__ __forceinline__ double cabs(cd a) { return hypot(a.r, a.i); }
+__device__ __forceinline__ double cabs1(cd a) { return fabs(a.r) + fabs(a.i); }  // LAPACK dcabs1
+
+// Smith's complex division (as LAPACK zladiv / C99), a / b.
+__device__ __forceinline__ cd cdiv(cd a, cd b) {
+  if (fabs(b.i) <= fabs(b.r)) {
+    const double e = b.i / b.r, f = b.r + b.i * e;
+    return cd{(a.r + a.i * e) / f, (a.i - a.r * e) / f};
+  }
+  const double e = b.r / b.i, f = b.i + b.r * e;
+  return cd{(a.r * e + a.i) / f, (a.i * e - a.r) / f};
+}
+
+// In-register Gaussian elimination with partial pivoting (max |re|+|im|, first maximum
+// wins as in izamax) on an N x N complex system; A and x are overwritten, x = A^-1 x.
+// Returns false on an exactly zero pivot (LAPACK: info > 0 -> LinAlgError("Singular matrix")).
+template <int N>
+__device__ __forceinline__ bool lu_solve(cd (&A)[N][N], cd (&x)[N]) {
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    int p = k;
+    double best = cabs1(A[k][k]);
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) {
+      const double v = cabs1(A[i][k]);
+      if (v > best) { best = v; p = i; }
+    }
+    ok = ok && (best != 0.0);
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) {
+      const bool sw = (p == i);
+#pragma unroll
+      for (int j = k; j < N; ++j) {
+        const cd a = A[k][j], b = A[i][j];
+        A[k][j] = sw ? b : a;
+        A[i][j] = sw ? a : b;
+      }
+      const cd a = x[k], b = x[i];
+      x[k] = sw ? b : a;
+      x[i] = sw ? a : b;
+    }
+    const cd piv = A[k][k];
+    const cd rinv = cdiv(mk(1.0, 0.0), best != 0.0 ? piv : mk(1.0, 0.0));
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) {
+      const cd l = mul(A[i][k], rinv);
+#pragma unroll
+      for (int j = k + 1; j < N; ++j) A[i][j] = sub(A[i][j], mul(l, A[k][j]));
+      x[i] = sub(x[i], mul(l, x[k]));
+    }
+  }
+#pragma unroll
+  for (int k = N - 1; k >= 0; --k) {
+    cd s = x[k];
+#pragma unroll
+    for (int j = k + 1; j < N; ++j) s = sub(s, mul(A[k][j], x[j]));
+    x[k] = cdiv(s, A[k][k]);
+  }
+  return ok;
+}
+
+// full 64-lane butterfly sum (every lane ends with the total)
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// blockIdx -> work item such that blocks dispatched to the same XCD (b % 8 under the
+// observed round-robin placement) get a CONTIGUOUS range of items; bijective for any G.
+// Placement only affects speed (L2 locality of the per-design/heading tables), never results.
+__device__ __forceinline__ int xcd_remap(int b, int G) {
+  const int x = b & 7, q = G >> 3, r = G & 7;
+  return x * q + (x < r ? x : r) + (b >> 3);
+}
+
+}  // namespace rh

@@ -1,0 +1,707 @@
+// rh_kernels.hip -- gfx950 kernels of RAFT's frequency-domain response solve.
+//
+// Hot path:
+//   k_wave_tables  : unit-amplitude Airy kinematics per (heading, node, bin) and the
+//                    strip-theory inertial excitation sum over nodes
+//                    (raft/raft_fowt.py:1098-1124, raft/helpers.py:105-154).
+//   k_solve_cases  : one workgroup per sea-state case; the whole Borgman drag fixed point
+//                    (raft/raft_model.py:918-1000) runs inside the workgroup:
+//                      A  RMS of node relative velocity over all bins (raft/raft_fowt.py:1185-1220)
+//                      B  per-node Bmat and B_drag = sum translateMatrix3to6DOF (:1223-1250)
+//                      C  per-bin drag excitation + Z assembly + pivoted LU (raft/raft_model.py:937-947)
+//                      D  convergence test / 0.2-0.8 relaxation (:961-991)
+//                    then the motion statistics of saveTurbineOutputs (raft/raft_fowt.py:1831-1875).
+//   k_heading_resp : extra sea states with the linearisation frozen (raft/raft_model.py:1049-1065).
+//
+// Work layout: lane = frequency bin (NB bins per thread, 256 threads per case), node loop
+// innermost with node parameters wave-uniform (scalar loads), the per-node bin reductions
+// done with 64-lane butterflies and a fixed-order cross-wave sum (deterministic).
+#include "rh_device.h"
+
+namespace rh {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr double kSqrt8Pi = 1.5957691216057308;   // np.sqrt(8/np.pi)
+constexpr double kRad2Deg = 57.29577951308232;    // raft/helpers.py:25-26
+
+struct DevDesign {
+  rh_design d;
+};
+
+__device__ __forceinline__ double nf(const double* node, int nn, int f, int n) { return node[f * nn + n]; }
+
+// Spectral density S(w) for one bin (raft/helpers.py:606-663, raft/raft_fowt.py:1000-1014)
+__device__ double sea_spectrum(int spec, double Hs, double Tp, double gam, double w) {
+  double S;
+  if (spec == RH_SPEC_UNIT) {
+    S = 1.0;
+  } else if (spec == RH_SPEC_CONSTANT) {
+    S = Hs;
+  } else if (spec == RH_SPEC_NONE) {
+    S = 0.0;
+  } else {
+    double G = gam;
+    if (!(G != 0.0)) {                      // `if not Gamma:` (0 -> IEC automatic)
+      const double t = Tp / sqrt(Hs);
+      if (t <= 3.6) G = 5.0;
+      else if (t >= 5.0) G = 1.0;
+      else G = exp(5.75 - 1.15 * t);
+    }
+    const double f = 0.5 / M_PI * w;
+    const double fp4 = pow(Tp * f, -4.0);
+    const double C = 1.0 - (0.287 * log(G));
+    const double sig = (f <= 1.0 / Tp) ? 0.07 : 0.09;
+    const double a = (f * Tp - 1.0) / sig;
+    const double Alpha = exp(-0.5 * (a * a));
+    S = 0.5 / M_PI * C * 0.3125 * Hs * Hs * fp4 / f * exp(-1.25 * fp4) * pow(G, Alpha);
+  }
+  return S;
+}
+
+// wave amplitude zeta = sqrt(2 S dw) (raft/raft_fowt.py:1003-1009)
+__device__ __forceinline__ double sea_amplitude(int spec, double Hs, double Tp, double gam, double w, double dw) {
+  return sqrt(2.0 * sea_spectrum(spec, Hs, Tp, gam, w) * dw);
+}
+
+__global__ __launch_bounds__(256) void k_sea_state(int nw, const double* __restrict__ w, double dw,
+                                                    const int* __restrict__ spec, const double* __restrict__ Hs,
+                                                    const double* __restrict__ Tp, const double* __restrict__ gam,
+                                                    double* __restrict__ S, double* __restrict__ zeta) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x, ic = blockIdx.y;
+  if (b >= nw) return;
+  const double s = sea_spectrum(spec[ic], Hs[ic], Tp[ic], gam[ic], w[b]);
+  if (S) S[(size_t)ic * nw + b] = s;
+  zeta[(size_t)ic * nw + b] = sqrt(2.0 * s * dw);
+}
+
+// ----------------------------------------------------------------------------------------
+// k_wave_tables: thread per (heading, bin); loop over nodes.
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void k_wave_tables(rh_design d, const double* __restrict__ beta,
+                                                      rh_c128* __restrict__ uhat, rh_c128* __restrict__ finer) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int h = blockIdx.y;
+  const int nw = d.nw, nn = d.nn;
+  if (b >= nw) return;
+  const double w = d.w[b], k = d.k[b], hd = d.depth;
+  const double be = beta[h];
+  const double cb = cos(be), sb = sin(be);
+  cd F[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
+  const double* node = d.node;
+  for (int n = 0; n < nn; ++n) {
+    const double x = nf(node, nn, RH_NF_RX, n), y = nf(node, nn, RH_NF_RY, n), z = nf(node, nn, RH_NF_RZ, n);
+    const double th = k * (cb * x + sb * y);
+    const cd e = mk(cos(th), -sin(th));      // exp(-1j*th)
+    double s_sh, c_sh, c_ch;
+    if (k * hd > 89.4) {                     // deep-water switch (raft/helpers.py:133-136)
+      const double ez = exp(k * z);
+      s_sh = ez;
+      c_sh = ez;
+      c_ch = ez + exp(-k * (z + 2.0 * hd));
+    } else {
+      const double skh = sinh(k * hd);
+      s_sh = sinh(k * (z + hd)) / skh;
+      c_sh = cosh(k * (z + hd)) / skh;
+      c_ch = cosh(k * (z + hd)) / cosh(k * hd);
+    }
+    const cd we = scl(e, w);
+    const cd u0 = scl(scl(we, c_sh), cb);
+    const cd u1 = scl(scl(we, c_sh), sb);
+    const cd u2 = scl(iw(w, e), s_sh);
+    rh_c128* U = uhat + ((size_t)(h * nn + n) * 3) * nw + b;
+    st(U, u0);
+    st(U + nw, u1);
+    st(U + 2 * nw, u2);
+    // inertial excitation: Imat ud + pDyn a_i q, ud = i w u  (raft/raft_fowt.py:1113-1124)
+    const cd ud[3] = {iw(w, u0), iw(w, u1), iw(w, u2)};
+    const cd pd = scl(scl(e, d.pdyn_rho_g), c_ch);
+    const double ai = nf(node, nn, RH_NF_AI, n);
+    const double q[3] = {nf(node, nn, RH_NF_QX, n), nf(node, nn, RH_NF_QY, n), nf(node, nn, RH_NF_QZ, n)};
+    const cd pa = scl(pd, ai);
+    cd f[3];
+    if (nf(node, nn, RH_NF_MCF, n) != 0.0) {
+      const rh_c128* I = d.imat_mcf + (size_t)n * 9 * nw + b;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        cd s = mul(ld(I + (3 * r + 0) * nw), ud[0]);
+        s = add(s, mul(ld(I + (3 * r + 1) * nw), ud[1]));
+        s = add(s, mul(ld(I + (3 * r + 2) * nw), ud[2]));
+        f[r] = add(s, scl(pa, q[r]));
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        cd s = scl(ud[0], nf(node, nn, RH_NF_I00 + 3 * r + 0, n));
+        s = add(s, scl(ud[1], nf(node, nn, RH_NF_I00 + 3 * r + 1, n)));
+        s = add(s, scl(ud[2], nf(node, nn, RH_NF_I00 + 3 * r + 2, n)));
+        f[r] = add(s, scl(pa, q[r]));
+      }
+    }
+    const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
+    F[0] = add(F[0], f[0]);
+    F[1] = add(F[1], f[1]);
+    F[2] = add(F[2], f[2]);
+    F[3] = add(F[3], sub(scl(f[2], ry), scl(f[1], rz)));
+    F[4] = add(F[4], sub(scl(f[0], rz), scl(f[2], rx)));
+    F[5] = add(F[5], sub(scl(f[1], rx), scl(f[0], ry)));
+  }
+  rh_c128* Fo = finer + (size_t)h * 6 * nw + b;
+#pragma unroll
+  for (int c = 0; c < 6; ++c) st(Fo + c * nw, F[c]);
+}
+
+// ----------------------------------------------------------------------------------------
+// shared pieces of the case solve
+// ----------------------------------------------------------------------------------------
+
+// Node drag matrix from the three bin-summed squared relative-velocity magnitudes
+// (raft/raft_fowt.py:1213-1248).  sums = {sum|vrel_q|^2, sum|vrel_p or p1|^2, sum|vrel_p2|^2}.
+__device__ __forceinline__ void node_bmat(const double* node, int nn, int n, double rho, const double* sums,
+                                          double* bm) {
+  const bool circ = nf(node, nn, RH_NF_CIRC, n) != 0.0;
+  const double vq = sqrt(0.5 * sums[0]);
+  const double vp1 = sqrt(0.5 * sums[1]);
+  const double vp2 = circ ? vp1 : sqrt(0.5 * sums[2]);
+  const double Bq = kSqrt8Pi * vq * 0.5 * rho * nf(node, nn, RH_NF_AQ, n) * nf(node, nn, RH_NF_CDQ, n);
+  const double Bp1 = kSqrt8Pi * vp1 * 0.5 * rho * nf(node, nn, RH_NF_AP1, n) * nf(node, nn, RH_NF_CDP1, n);
+  const double Bp2 = kSqrt8Pi * vp2 * 0.5 * rho * nf(node, nn, RH_NF_AP2, n) * nf(node, nn, RH_NF_CDP2, n);
+  const double Be = kSqrt8Pi * vq * 0.5 * rho * nf(node, nn, RH_NF_AEND, n) * nf(node, nn, RH_NF_CDEND, n);
+  const double q[3] = {nf(node, nn, RH_NF_QX, n), nf(node, nn, RH_NF_QY, n), nf(node, nn, RH_NF_QZ, n)};
+  const double p1[3] = {nf(node, nn, RH_NF_P1X, n), nf(node, nn, RH_NF_P1Y, n), nf(node, nn, RH_NF_P1Z, n)};
+  const double p2[3] = {nf(node, nn, RH_NF_P2X, n), nf(node, nn, RH_NF_P2Y, n), nf(node, nn, RH_NF_P2Z, n)};
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      bm[3 * i + j] = (Bq * (q[i] * q[j]) + Bp1 * (p1[i] * p1[j]) + Bp2 * (p2[i] * p2[j])) + Be * (q[i] * q[j]);
+}
+
+// Entry (i,j) of translateMatrix3to6DOF(Bm, r) (raft/helpers.py:455-478).
+__device__ __forceinline__ double t3to6(const double* Bm, double rx, double ry, double rz, int i, int j) {
+  const double H[3][3] = {{0, rz, -ry}, {-rz, 0, rx}, {ry, -rx, 0}};
+  auto BH = [&](int a, int c) { return Bm[3 * a + 0] * H[0][c] + Bm[3 * a + 1] * H[1][c] + Bm[3 * a + 2] * H[2][c]; };
+  if (i < 3 && j < 3) return Bm[3 * i + j];
+  if (i < 3) return BH(i, j - 3);
+  if (j < 3) return BH(j, i - 3);
+  const int a = i - 3, c = j - 3;   // (H Bm H^T)[a][c] = sum_k H[a][k] (Bm H^T)[k][c] = sum_k H[a][k] BH? -> (H (Bm H^T))
+  double s = 0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double HB = H[a][0] * Bm[0 * 3 + k] + H[a][1] * Bm[1 * 3 + k] + H[a][2] * Bm[2 * 3 + k];  // (H Bm)[a][k]
+    s += HB * H[c][k];                                                                          // * H^T[k][c]
+  }
+  return s;
+}
+
+// Drag excitation of one bin before the zeta factor: sum_n [Bm_n uhat_n; r_n x Bm_n uhat_n]
+__device__ __forceinline__ void drag_exc_bin(const double* node, int nn, const double* bm_lds,
+                                             const rh_c128* __restrict__ Uh, int nw, int b, cd (&F)[6]) {
+#pragma unroll
+  for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
+  for (int n = 0; n < nn; ++n) {
+    const rh_c128* U = Uh + (size_t)n * 3 * nw + b;
+    const cd u0 = ld(U), u1 = ld(U + nw), u2 = ld(U + 2 * nw);
+    const double* Bm = bm_lds + 9 * n;
+    cd f[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) f[r] = add(add(scl(u0, Bm[3 * r]), scl(u1, Bm[3 * r + 1])), scl(u2, Bm[3 * r + 2]));
+    const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
+    F[0] = add(F[0], f[0]);
+    F[1] = add(F[1], f[1]);
+    F[2] = add(F[2], f[2]);
+    F[3] = add(F[3], sub(scl(f[2], ry), scl(f[1], rz)));
+    F[4] = add(F[4], sub(scl(f[0], rz), scl(f[2], rx)));
+    F[5] = add(F[5], sub(scl(f[1], rx), scl(f[0], ry)));
+  }
+}
+
+// Z(w) = -w^2 M + i w (B + B_drag) + C (raft/raft_model.py:944).
+// mbc: LDS image {M[36], B_lin[36], C[36]} of a frequency-independent design (wave-uniform
+// broadcast reads); per-bin M/B (BEM added mass / radiation damping) come from global memory.
+__device__ __forceinline__ void assemble_z(const rh_design& d, const double* mbc, int b, double w, const double* bd,
+                                           cd (&Z)[6][6]) {
+  const double w2 = -(w * w);
+  if (d.mb_per_bin) {
+    const double* M = d.M + (size_t)b * 36;
+    const double* B = d.B + (size_t)b * 36;
+#pragma unroll
+    for (int e = 0; e < 36; ++e) Z[e / 6][e % 6] = mk(w2 * M[e] + mbc[72 + e], w * (B[e] + bd[e]));
+  } else {
+#pragma unroll
+    for (int e = 0; e < 36; ++e) Z[e / 6][e % 6] = mk(w2 * mbc[e] + mbc[72 + e], w * (mbc[36 + e] + bd[e]));
+  }
+}
+
+// LDS image of M_lin, B_lin, C_lin (frequency-independent parts); call with >= 36 threads.
+__device__ __forceinline__ void load_mbc(const rh_design& d, double* mbc, int tid) {
+  if (tid < 36) {
+    mbc[tid] = d.mb_per_bin ? 0.0 : d.M[tid];
+    mbc[36 + tid] = d.mb_per_bin ? 0.0 : d.B[tid];
+    mbc[72 + tid] = d.C[tid];
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// k_solve_cases
+// ----------------------------------------------------------------------------------------
+struct CaseArgs {
+  const DevDesign* designs;
+  rh_cases c;
+  rh_solve_out o;
+};
+
+template <int NB>
+__global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ncase = a.c.ncase;
+  const int slot = xcd_remap(blockIdx.x, ncase);
+  const int ic = a.c.order ? a.c.order[slot] : slot;
+  const rh_design& d = a.designs[a.c.design[ic]].d;
+  const int nw = d.nw, nn = d.nn;
+  const double* node = d.node;
+  const int head = a.c.head[ic];
+  const rh_c128* Uh = d.uhat + (size_t)head * nn * 3 * nw;
+  const rh_c128* Fe = d.finer + (size_t)head * 6 * nw;
+
+  double* red = smem;                     // [kWaves][nn][3]
+  double* bm = red + kWaves * nn * 3;     // [nn][9]
+  double* bd = bm + nn * 9;               // [36]
+  double* sred = bd + 36;                 // [kWaves][6]
+  double* mbc = sred + kWaves * 6;        // [108] M, B_lin, C
+  load_mbc(d, mbc, tid);
+
+  const int spec = a.c.spectrum[ic];
+  const double Hs = a.c.Hs[ic], Tp = a.c.Tp[ic], gam = a.c.gamma[ic];
+  double zt[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int b = tid + kThreads * j;
+    zt[j] = (b < nw) ? sea_amplitude(spec, Hs, Tp, gam, d.w[b], d.dw) : 0.0;
+    if (b < nw && a.o.zeta) a.o.zeta[(size_t)ic * nw + b] = zt[j];
+  }
+  rh_c128* Xo = a.o.Xi + (size_t)ic * 6 * nw;
+  rh_c128* XL = a.o.Xi_last + (size_t)ic * 6 * nw;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int b = tid + kThreads * j;
+    if (b < nw)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) st(XL + c * nw + b, mk(a.c.XiStart, 0.0));
+  }
+
+  const int nloop = a.c.nIter + 1;
+  const double tol = a.c.tol;
+  int status = RH_CASE_NOT_CONVERGED, iters = nloop;
+  for (int it = 0; it < nloop; ++it) {
+    // ---------------- A: per-node sums of squared relative-velocity components ----------
+    cd xl[NB][6];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int b = tid + kThreads * j;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) xl[j][c] = (b < nw) ? ld(XL + c * nw + b) : mk(0, 0);
+    }
+    for (int n = 0; n < nn; ++n) {
+      const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
+      const double q0 = nf(node, nn, RH_NF_QX, n), q1 = nf(node, nn, RH_NF_QY, n), q2 = nf(node, nn, RH_NF_QZ, n);
+      const bool circ = nf(node, nn, RH_NF_CIRC, n) != 0.0;
+      double s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int b = tid + kThreads * j;
+        if (b < nw) {
+          const double w = d.w[b];
+          const rh_c128* U = Uh + (size_t)n * 3 * nw + b;
+          const cd u0 = scl(ld(U), zt[j]), u1 = scl(ld(U + nw), zt[j]), u2 = scl(ld(U + 2 * nw), zt[j]);
+          const cd* X = xl[j];
+          // getKinematics: dr = Xi[:3] + th x r ; v = i w dr  (raft/helpers.py:95-97)
+          const cd dr0 = add(X[0], add(scl(X[5], -ry), scl(X[4], rz)));
+          const cd dr1 = add(X[1], sub(scl(X[5], rx), scl(X[3], rz)));
+          const cd dr2 = add(X[2], add(scl(X[4], -rx), scl(X[3], ry)));
+          const cd v0 = sub(u0, iw(w, dr0)), v1 = sub(u1, iw(w, dr1)), v2 = sub(u2, iw(w, dr2));
+          const cd sq = add(add(scl(v0, q0), scl(v1, q1)), scl(v2, q2));
+          const cd vq0 = scl(sq, q0), vq1 = scl(sq, q1), vq2 = scl(sq, q2);
+          s0 += abs2(vq0) + abs2(vq1) + abs2(vq2);
+          if (circ) {
+            s1 += abs2(sub(v0, vq0)) + abs2(sub(v1, vq1)) + abs2(sub(v2, vq2));
+          } else {
+            const double a0 = nf(node, nn, RH_NF_P1X, n), a1 = nf(node, nn, RH_NF_P1Y, n), a2 = nf(node, nn, RH_NF_P1Z, n);
+            const double b0 = nf(node, nn, RH_NF_P2X, n), b1 = nf(node, nn, RH_NF_P2Y, n), b2 = nf(node, nn, RH_NF_P2Z, n);
+            const cd s_1 = add(add(scl(v0, a0), scl(v1, a1)), scl(v2, a2));
+            const cd s_2 = add(add(scl(v0, b0), scl(v1, b1)), scl(v2, b2));
+            s1 += abs2(scl(s_1, a0)) + abs2(scl(s_1, a1)) + abs2(scl(s_1, a2));
+            s2 += abs2(scl(s_2, b0)) + abs2(scl(s_2, b1)) + abs2(scl(s_2, b2));
+          }
+        }
+      }
+      s0 = wave_sum(s0);
+      s1 = wave_sum(s1);
+      s2 = wave_sum(s2);
+      if (lane == 0) {
+        double* R = red + (wv * nn + n) * 3;
+        R[0] = s0;
+        R[1] = s1;
+        R[2] = s2;
+      }
+    }
+    __syncthreads();
+    // ---------------- B: node drag matrices and B_drag ----------------------------------
+    for (int n = tid; n < nn; n += kThreads) {
+      double sums[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        double s = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) s += red[(w * nn + n) * 3 + c];
+        sums[c] = s;
+      }
+      node_bmat(node, nn, n, d.rho, sums, bm + 9 * n);
+    }
+    __syncthreads();
+    if (tid < 36) {
+      const int i = tid / 6, j = tid % 6;
+      double s = 0;
+      for (int n = 0; n < nn; ++n)
+        s += t3to6(bm + 9 * n, nf(node, nn, RH_NF_XX, n), nf(node, nn, RH_NF_XY, n), nf(node, nn, RH_NF_XZ, n), i, j);
+      bd[tid] = s;
+    }
+    __syncthreads();
+    // ---------------- C: excitation, Z(w), LU solve, convergence flags ------------------
+    bool my_ok = true, my_nan = false, my_sing = false;
+#pragma unroll 1
+    for (int j = 0; j < NB; ++j) {
+      const int b = tid + kThreads * j;
+      if (b >= nw) continue;
+      const double w = d.w[b];
+      cd F[6];
+      drag_exc_bin(node, nn, bm, Uh, nw, b, F);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        cd f = add(scl(ld(Fe + c * nw + b), zt[j]), scl(F[c], zt[j]));   // F_lin + F_drag
+        if (a.c.fext) f = add(f, ld(a.c.fext + ((size_t)ic * 6 + c) * nw + b));
+        F[c] = f;
+      }
+      cd Z[6][6];
+      assemble_z(d, mbc, b, w, bd, Z);
+      if (a.o.Z) {
+        rh_c128* Zo = a.o.Z + ((size_t)ic * nw + b) * 36;
+#pragma unroll
+        for (int e = 0; e < 36; ++e) st(Zo + e, Z[e / 6][e % 6]);
+      }
+      my_sing |= !lu_solve<6>(Z, F);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const cd x = F[c];
+        const cd xlast = ld(XL + c * nw + b);
+        my_nan |= (x.r != x.r) || (x.i != x.i);
+        // tolCheck = |Xi - XiLast| / (|Xi| + tol) < tol  (raft/raft_model.py:961-962)
+        const double t = cabs(sub(x, xlast)) / (cabs(x) + tol);
+        my_ok = my_ok && (t < tol);
+        st(Xo + c * nw + b, x);
+        // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged
+        st(XL + c * nw + b, add(scl(xlast, 0.2), scl(x, 0.8)));
+      }
+    }
+    const int all_ok = __syncthreads_and(my_ok ? 1 : 0);
+    const int any_nan = __syncthreads_or(my_nan ? 1 : 0);
+    const int any_sing = __syncthreads_or(my_sing ? 1 : 0);
+    if (any_nan) {
+      status = RH_CASE_NAN;
+      iters = it + 1;
+      break;
+    }
+    if (any_sing) {
+      status = RH_CASE_SINGULAR;
+      iters = it + 1;
+      break;
+    }
+    if (all_ok) {
+      status = RH_CASE_CONVERGED;
+      iters = it + 1;
+      break;
+    }
+  }
+
+  // ---------------- outputs ------------------------------------------------------------
+  if (tid == 0) {
+    a.o.iters[ic] = iters;
+    a.o.status[ic] = status;
+  }
+  if (a.o.B_drag && tid < 36) a.o.B_drag[(size_t)ic * 36 + tid] = bd[tid];
+  if (a.o.Bmat)
+    for (int e = tid; e < nn * 9; e += kThreads) a.o.Bmat[(size_t)ic * nn * 9 + e] = bm[e];
+  if (a.o.psd || a.o.std || a.o.rao) {
+    double ss[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int b = tid + kThreads * j;
+      if (b >= nw) continue;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const cd x = ld(Xo + c * nw + b);
+        const cd xd = c >= 3 ? scl(x, kRad2Deg) : x;
+        const double m2 = abs2(xd);
+        ss[c] += m2;
+        if (a.o.psd) a.o.psd[((size_t)ic * 6 + c) * nw + b] = 0.5 * m2 / d.dw;
+        if (a.o.rao) {
+          const double z = zt[j];
+          st(a.o.rao + ((size_t)ic * 6 + c) * nw + b, fabs(z) > 1e-6 ? cd{x.r / z, x.i / z} : mk(0, 0));
+        }
+      }
+    }
+    if (a.o.std) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const double s = wave_sum(ss[c]);
+        if (lane == 0) sred[wv * 6 + c] = s;
+      }
+      __syncthreads();
+      if (tid < 6) {
+        double s = 0;
+        for (int w = 0; w < kWaves; ++w) s += sred[w * 6 + tid];
+        a.o.std[(size_t)ic * 6 + tid] = sqrt(0.5 * s);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// k_heading_resp: thread per (case, bin)
+// ----------------------------------------------------------------------------------------
+struct HeadArgs {
+  const DevDesign* designs;
+  int ncase;
+  const int* design_idx;
+  const int* head;
+  const double* zeta;
+  const double* B_drag;
+  const double* Bmat;
+  rh_c128* Xi;
+};
+
+__global__ __launch_bounds__(kThreads, 2) void k_heading_resp(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int ic = blockIdx.y;
+  const rh_design& d = a.designs[a.design_idx[ic]].d;
+  const int nw = d.nw, nn = d.nn;
+  double* bm = smem;
+  double* bd = bm + 9 * nn;
+  double* mbc = bd + 36;
+  load_mbc(d, mbc, threadIdx.x);
+  for (int e = threadIdx.x; e < nn * 9; e += blockDim.x) bm[e] = a.Bmat[(size_t)ic * nn * 9 + e];
+  if (threadIdx.x < 36) bd[threadIdx.x] = a.B_drag[(size_t)ic * 36 + threadIdx.x];
+  __syncthreads();
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nw) return;
+  const int head = a.head[ic];
+  const rh_c128* Uh = d.uhat + (size_t)head * nn * 3 * nw;
+  const rh_c128* Fe = d.finer + (size_t)head * 6 * nw;
+  const double z = a.zeta[(size_t)ic * nw + b];
+  cd F[6];
+  drag_exc_bin(d.node, nn, bm, Uh, nw, b, F);
+#pragma unroll
+  for (int c = 0; c < 6; ++c) F[c] = add(scl(ld(Fe + c * nw + b), z), scl(F[c], z));
+  cd Z[6][6];
+  assemble_z(d, mbc, b, d.w[b], bd, Z);
+  lu_solve<6>(Z, F);
+#pragma unroll
+  for (int c = 0; c < 6; ++c) st(a.Xi + ((size_t)ic * 6 + c) * nw + b, F[c]);
+}
+
+// ----------------------------------------------------------------------------------------
+// stand-alone linearisation (FOWT.calcHydroLinearization for a given Xi)
+// ----------------------------------------------------------------------------------------
+// pass 1: block per node, reduce over bins
+__global__ __launch_bounds__(kThreads) void k_lin_sums(rh_design d, int head, const rh_c128* __restrict__ Xi,
+                                                       const double* __restrict__ zeta, double* __restrict__ Bmat) {
+  __shared__ double red[kWaves][3];
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nw = d.nw, nn = d.nn;
+  const double* node = d.node;
+  const rh_c128* U = d.uhat + ((size_t)head * nn + n) * 3 * nw;
+  const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
+  const double q0 = nf(node, nn, RH_NF_QX, n), q1 = nf(node, nn, RH_NF_QY, n), q2 = nf(node, nn, RH_NF_QZ, n);
+  const double a0 = nf(node, nn, RH_NF_P1X, n), a1 = nf(node, nn, RH_NF_P1Y, n), a2 = nf(node, nn, RH_NF_P1Z, n);
+  const double b0 = nf(node, nn, RH_NF_P2X, n), b1 = nf(node, nn, RH_NF_P2Y, n), b2 = nf(node, nn, RH_NF_P2Z, n);
+  const bool circ = nf(node, nn, RH_NF_CIRC, n) != 0.0;
+  double s0 = 0, s1 = 0, s2 = 0;
+  for (int b = tid; b < nw; b += kThreads) {
+    const double w = d.w[b], z = zeta[b];
+    const cd u0 = scl(ld(U + b), z), u1 = scl(ld(U + nw + b), z), u2 = scl(ld(U + 2 * nw + b), z);
+    cd X[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) X[c] = ld(Xi + c * nw + b);
+    const cd dr0 = add(X[0], add(scl(X[5], -ry), scl(X[4], rz)));
+    const cd dr1 = add(X[1], sub(scl(X[5], rx), scl(X[3], rz)));
+    const cd dr2 = add(X[2], add(scl(X[4], -rx), scl(X[3], ry)));
+    const cd v0 = sub(u0, iw(w, dr0)), v1 = sub(u1, iw(w, dr1)), v2 = sub(u2, iw(w, dr2));
+    const cd sq = add(add(scl(v0, q0), scl(v1, q1)), scl(v2, q2));
+    const cd vq0 = scl(sq, q0), vq1 = scl(sq, q1), vq2 = scl(sq, q2);
+    s0 += abs2(vq0) + abs2(vq1) + abs2(vq2);
+    if (circ) {
+      s1 += abs2(sub(v0, vq0)) + abs2(sub(v1, vq1)) + abs2(sub(v2, vq2));
+    } else {
+      const cd s_1 = add(add(scl(v0, a0), scl(v1, a1)), scl(v2, a2));
+      const cd s_2 = add(add(scl(v0, b0), scl(v1, b1)), scl(v2, b2));
+      s1 += abs2(scl(s_1, a0)) + abs2(scl(s_1, a1)) + abs2(scl(s_1, a2));
+      s2 += abs2(scl(s_2, b0)) + abs2(scl(s_2, b1)) + abs2(scl(s_2, b2));
+    }
+  }
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane == 0) {
+    red[wv][0] = s0;
+    red[wv][1] = s1;
+    red[wv][2] = s2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double sums[3];
+    for (int c = 0; c < 3; ++c) {
+      double s = 0;
+      for (int w = 0; w < kWaves; ++w) s += red[w][c];
+      sums[c] = s;
+    }
+    node_bmat(node, nn, n, d.rho, sums, Bmat + 9 * n);
+  }
+}
+
+// pass 2: B_drag (36 threads) -- sequential node order like the reference's running sum
+__global__ void k_lin_bdrag(rh_design d, const double* __restrict__ Bmat, double* __restrict__ B_drag) {
+  const int t = threadIdx.x;
+  if (t >= 36) return;
+  const int nn = d.nn;
+  double s = 0;
+  for (int n = 0; n < nn; ++n)
+    s += t3to6(Bmat + 9 * n, nf(d.node, nn, RH_NF_XX, n), nf(d.node, nn, RH_NF_XY, n), nf(d.node, nn, RH_NF_XZ, n),
+               t / 6, t % 6);
+  B_drag[t] = s;
+}
+
+// drag excitation for a given Bmat: thread per bin
+__global__ __launch_bounds__(kThreads) void k_drag_exc(rh_design d, int head, const double* __restrict__ zeta,
+                                                        const double* __restrict__ Bmat, rh_c128* __restrict__ Fd) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nw = d.nw, nn = d.nn;
+  for (int e = threadIdx.x; e < nn * 9; e += blockDim.x) smem[e] = Bmat[e];
+  __syncthreads();
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nw) return;
+  const rh_c128* Uh = d.uhat + (size_t)head * nn * 3 * nw;
+  cd F[6];
+  drag_exc_bin(d.node, nn, smem, Uh, nw, b, F);
+  const double z = zeta[b];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) st(Fd + c * nw + b, scl(F[c], z));
+}
+
+// motion statistics over rows: block per case
+__global__ __launch_bounds__(kThreads) void k_motion_stats(int nrow, int nw, double dw, const rh_c128* __restrict__ Xi,
+                                                            double* __restrict__ psd, double* __restrict__ stdv) {
+  __shared__ double sred[kWaves][6];
+  const int ic = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double ss[6] = {0, 0, 0, 0, 0, 0};
+  for (int b = tid; b < nw; b += kThreads) {
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      double p = 0;
+      for (int r = 0; r < nrow; ++r) {
+        const cd x = ld(Xi + (((size_t)ic * nrow + r) * 6 + c) * nw + b);
+        const double m2 = abs2(c >= 3 ? scl(x, kRad2Deg) : x);
+        p += 0.5 * m2 / dw;
+        ss[c] += m2;
+      }
+      if (psd) psd[((size_t)ic * 6 + c) * nw + b] = p;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    const double s = wave_sum(ss[c]);
+    if (lane == 0) sred[wv][c] = s;
+  }
+  __syncthreads();
+  if (tid < 6 && stdv) {
+    double s = 0;
+    for (int w = 0; w < kWaves; ++w) s += sred[w][tid];
+    stdv[(size_t)ic * 6 + tid] = sqrt(0.5 * s);
+  }
+}
+
+// coupled array solve (raft/raft_model.py:1021-1065), thread per bin, matrix in LDS
+// (6N x 6N with N <= 2 FOWTs is too large for registers; this path is not throughput-critical).
+constexpr int kSysThreads = 32;
+__global__ __launch_bounds__(kSysThreads) void k_system_solve(int N, int nw, const rh_c128* __restrict__ Z,
+                                                                const double* __restrict__ K,
+                                                                const rh_c128* __restrict__ F, rh_c128* __restrict__ Xi) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int t = threadIdx.x;
+  const int b = blockIdx.x * blockDim.x + t;
+  // A[i][j] of this thread at smem[2*((i*N + j)*kSysThreads + t)], x[i] after the matrix
+  auto Ar = [&](int i, int j) -> double& { return smem[2 * ((i * N + j) * kSysThreads + t)]; };
+  auto Ai = [&](int i, int j) -> double& { return smem[2 * ((i * N + j) * kSysThreads + t) + 1]; };
+  double* xs = smem + 2 * N * N * kSysThreads;
+  auto xr = [&](int i) -> double& { return xs[2 * (i * kSysThreads + t)]; };
+  auto xi = [&](int i) -> double& { return xs[2 * (i * kSysThreads + t) + 1]; };
+  if (b >= nw) return;
+  const int nf = N / 6;
+  for (int i = 0; i < N; ++i) {
+    for (int j = 0; j < N; ++j) {
+      Ar(i, j) = K ? K[i * N + j] : 0.0;
+      Ai(i, j) = 0.0;
+    }
+    const cd f = ld(F + (size_t)i * nw + b);
+    xr(i) = f.r;
+    xi(i) = f.i;
+  }
+  for (int f = 0; f < nf; ++f)
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 6; ++j) {
+        const cd z = ld(Z + ((size_t)f * nw + b) * 36 + 6 * i + j);
+        // Z_sys[i1:i2, i1:i2] += fowt.Z then += K : the reference adds K after the blocks
+        const double kr = Ar(6 * f + i, 6 * f + j);
+        Ar(6 * f + i, 6 * f + j) = z.r + kr;
+        Ai(6 * f + i, 6 * f + j) = z.i;
+      }
+  for (int k = 0; k < N; ++k) {
+    int p = k;
+    double best = fabs(Ar(k, k)) + fabs(Ai(k, k));
+    for (int i = k + 1; i < N; ++i) {
+      const double v = fabs(Ar(i, k)) + fabs(Ai(i, k));
+      if (v > best) { best = v; p = i; }
+    }
+    if (p != k) {
+      for (int j = k; j < N; ++j) {
+        double tr = Ar(k, j), ti = Ai(k, j);
+        Ar(k, j) = Ar(p, j); Ai(k, j) = Ai(p, j);
+        Ar(p, j) = tr; Ai(p, j) = ti;
+      }
+      double tr = xr(k), ti = xi(k);
+      xr(k) = xr(p); xi(k) = xi(p);
+      xr(p) = tr; xi(p) = ti;
+    }
+    const cd rinv = cdiv(mk(1.0, 0.0), best != 0.0 ? mk(Ar(k, k), Ai(k, k)) : mk(1.0, 0.0));
+    for (int i = k + 1; i < N; ++i) {
+      const cd l = mul(mk(Ar(i, k), Ai(i, k)), rinv);
+      for (int j = k + 1; j < N; ++j) {
+        const cd v = sub(mk(Ar(i, j), Ai(i, j)), mul(l, mk(Ar(k, j), Ai(k, j))));
+        Ar(i, j) = v.r; Ai(i, j) = v.i;
+      }
+      const cd v = sub(mk(xr(i), xi(i)), mul(l, mk(xr(k), xi(k))));
+      xr(i) = v.r; xi(i) = v.i;
+    }
+  }
+  for (int k = N - 1; k >= 0; --k) {
+    cd s = mk(xr(k), xi(k));
+    for (int j = k + 1; j < N; ++j) s = sub(s, mul(mk(Ar(k, j), Ai(k, j)), mk(xr(j), xi(j))));
+    s = cdiv(s, mk(Ar(k, k), Ai(k, k)));
+    xr(k) = s.r; xi(k) = s.i;
+    st(Xi + (size_t)k * nw + b, s);
+  }
+}
+
+}  // namespace rh

@@ -1,0 +1,283 @@
+"""FOWT: one floating wind turbine's frequency-domain hydrodynamics on the device.
+
+Mirrors the hot-path surface of the reference class (raft/raft_fowt.py): same method names,
+argument meaning, return values and the side-effect attributes downstream code reads
+(SURVEY.md §8(b)).  The per-node / per-bin arithmetic runs in librafthip; this class owns
+the per-design preparation (members, node tables, linear matrices) and the device buffers.
+
+Not built here: statics (calcStatics needs member inertia and
+hydrostatics -- supply them with setStatics()), MoorPy mooring, rotor aerodynamics
+(CCBlade), BEM (pyHAMS) and QTF file I/O.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .hydro_math import DEG2RAD, get_from_dict, wave_numbers, translate_matrix_6to6
+from .member import Member
+from .prep import DeviceDesign
+
+STATICS_KEYS = ["M_struc", "B_struc", "C_struc", "C_hydro", "W_struc", "W_hydro"]
+
+
+class FOWT:
+    def __init__(self, design, w, mpb=None, depth=600, x_ref=0, y_ref=0, heading_adjust=0, device=0):
+        self.nDOF = 6
+        self.w = np.array(w, dtype=float)
+        self.nw = len(self.w)
+        self.dw = self.w[1] - self.w[0]
+        self.depth = float(depth)
+        self.x_ref, self.y_ref = x_ref, y_ref
+        self.heading_adjust = heading_adjust
+        self.r6 = np.zeros(6)
+        self.Xi0 = np.zeros(6)
+        self.Xi = np.zeros([self.nDOF, self.nw], dtype=complex)
+        self.device_index = device
+        self.k = wave_numbers(self.w, self.depth)          # raft/raft_fowt.py:113
+        site = design["site"]
+        self.rho_water = get_from_dict(site, "rho_water", default=1025.0)
+        self.g = get_from_dict(site, "g", default=9.81)
+        plat = design["platform"]
+        self.potModMaster = get_from_dict(plat, "potModMaster", dtype=int, default=0)
+        dlsMax = get_from_dict(plat, "dlsMax", default=5.0)
+        self.memberList = []
+        for mi in plat["members"]:
+            mi = dict(mi)
+            if self.potModMaster in [1]:
+                mi["potMod"] = False
+            elif self.potModMaster in [2, 3]:
+                mi["potMod"] = True
+            if "dlsMax" not in mi:
+                mi["dlsMax"] = dlsMax
+            headings = get_from_dict(mi, "heading", shape=-1, default=0.)
+            for hd in np.atleast_1d(headings):
+                self.memberList.append(Member(mi, self.nw, heading=float(hd) + heading_adjust))
+        self.nrotors = 0
+        self._rotor_submerged = False
+        self._aero_mod = []
+        turb = design.get("turbine")
+        if turb:
+            self.nrotors = get_from_dict(turb, "nrotors", dtype=int, shape=0, default=1)
+            towers = turb.get("tower")
+            if towers is not None:
+                for mem in (towers if isinstance(towers, list) else [towers] * self.nrotors):
+                    self.memberList.append(Member(mem, self.nw))
+            nac = turb.get("nacelle")
+            if nac is not None:
+                for mem in (nac if isinstance(nac, list) else [nac] * self.nrotors):
+                    self.memberList.append(Member(mem, self.nw))
+            hhub = np.atleast_1d(get_from_dict(turb, "hHub", shape=-1, default=100.0))
+            self._rotor_submerged = bool(np.any(hhub < 0))
+            self._aero_mod = np.atleast_1d(get_from_dict(turb, "aeroServoMod", shape=-1, default=1))
+        self.potSecOrder = get_from_dict(plat, "potSecOrder", dtype=int, default=0)
+        if self.potSecOrder == 1:
+            mn, mx = plat["min_freq2nd"], plat["max_freq2nd"]
+            df = plat.get("df_freq2nd", mn)
+            self.w1_2nd = np.arange(mn, mx + 0.5 * mn, df) * 2 * np.pi   # raft/raft_fowt.py:240
+            self.w2_2nd = self.w1_2nd.copy()
+            self.k1_2nd = wave_numbers(self.w1_2nd, self.depth)
+            self.k2_2nd = self.k1_2nd.copy()
+        elif self.potSecOrder == 2:
+            raise NotImplementedError("potSecOrder=2 (external .12d QTF file) is outside the accelerated path")
+        self.outFolderQTF = plat.get("outFolderQTF")
+        self.C_moor = np.zeros([6, 6])
+        self.F_moor0 = np.zeros(6)
+        self.A_BEM = np.zeros([6, 6, self.nw])
+        self.B_BEM = np.zeros([6, 6, self.nw])
+        self.A_hydro_morison = np.zeros([6, 6])
+        self.B_gyro = np.zeros([6, 6, max(self.nrotors, 1)])
+        self.A_aero = np.zeros([6, 6, self.nw, self.nrotors])
+        self.B_aero = np.zeros([6, 6, self.nw, self.nrotors])
+        self._statics = None
+        self._dd = None            # DeviceDesign (built lazily, invalidated on setPosition)
+        self.nWaves = 1
+
+    # ------------------------------------------------------------------ set-up
+    def setPosition(self, r6):
+        """raft/raft_fowt.py:260-288 (members only; MoorPy is not available)."""
+        self.r6 = np.array(r6, dtype=float)
+        self.Xi0 = self.r6 - np.array([self.x_ref, self.y_ref, 0, 0, 0, 0])
+        for mem in self.memberList:
+            mem.setPosition(r6=self.r6)
+        self._dd = None
+
+    def setStatics(self, statics):
+        """Provide the outputs of calcStatics (M_struc, B_struc, C_struc, C_hydro, ...) and
+        optionally C_moor; the statics restatement is SURVEY.md §8(f) row 1."""
+        self._statics = {k: np.array(v, dtype=float) for k, v in statics.items()}
+
+    def calcStatics(self):
+        if self._statics is None:
+            raise NotImplementedError("FOWT.calcStatics (member inertia/hydrostatics, raft/raft_fowt.py:291-565) "
+                                      "is not restated yet: call setStatics() with the design's statics")
+        for k in STATICS_KEYS:
+            if k in self._statics:
+                setattr(self, k, self._statics[k].copy())
+        if "B_struc" not in self._statics:
+            self.B_struc = np.zeros([6, 6])
+        if "C_moor" in self._statics:
+            self.C_moor = self._statics["C_moor"].copy()
+
+    def calcTurbineConstants(self, case, ptfm_pitch=0):
+        """raft/raft_fowt.py:773-845 restricted to what the accelerated path supports: rotor
+        aerodynamics (CCBlade) are out of scope, so only cases without aero loads run."""
+        status = get_from_dict(case, "turbine_status", shape=0, dtype=str, default="operating")
+        speed = get_from_dict(case, "wind_speed", shape=0, default=10.0)
+        self.A_aero = np.zeros([6, 6, self.nw, self.nrotors])
+        self.B_aero = np.zeros([6, 6, self.nw, self.nrotors])
+        self.f_aero0 = np.zeros([6, self.nrotors])
+        self.B_gyro = np.zeros([6, 6, max(self.nrotors, 1)])
+        if self._rotor_submerged:
+            raise NotImplementedError("underwater rotors (raft/raft_rotor.py) are outside the accelerated path")
+        if status == "operating" and self.nrotors > 0 and speed > 0.0 and np.any(np.asarray(self._aero_mod) > 0):
+            raise NotImplementedError("rotor aerodynamics (CCBlade, raft/raft_rotor.py:788-1005) are outside the "
+                                      "accelerated path: run with wind_speed=0 or a non-operating turbine")
+
+    def calcHydroConstants(self):
+        """raft/raft_fowt.py:848-880 (strip-theory members)."""
+        self.A_hydro_morison = np.zeros([6, 6])
+        for mem in self.memberList:
+            k_array = self.k if mem.MCF else None
+            self.A_hydro_morison += mem.calcHydroConstants(r_ref=self.r6[:3], rho=self.rho_water, g=self.g,
+                                                           k_array=k_array)
+        self._dd = None
+
+    def device_design(self):
+        """The DeviceDesign of the current pose and coefficients (built on first use)."""
+        if self._dd is None:
+            self._dd = DeviceDesign(self, device=self.device_index)
+        return self._dd
+
+    # ------------------------------------------------------------------ sea state
+    def _sea_state(self, case):
+        """raft/raft_fowt.py:982-1014: normalises `case` in place (tiled arrays), returns
+        heading [deg], spectrum codes, Hs, Tp, gamma per sea state."""
+        hd = case["wave_heading"]
+        self.nWaves = 1 if np.isscalar(hd) else len(hd)
+        nW = self.nWaves
+        case["wave_heading"] = get_from_dict(case, "wave_heading", shape=nW, dtype=float, default=0)
+        case["wave_spectrum"] = get_from_dict(case, "wave_spectrum", shape=nW, dtype=str, default="JONSWAP")
+        case["wave_period"] = get_from_dict(case, "wave_period", shape=nW, dtype=float)
+        case["wave_height"] = get_from_dict(case, "wave_height", shape=nW, dtype=float)
+        case["wave_gamma"] = get_from_dict(case, "wave_gamma", shape=nW, dtype=float, default=0)
+        for sp in case["wave_spectrum"]:
+            if sp not in N.SPECTRUM_CODES:
+                raise ValueError(f"Wave spectrum input '{sp}' not recognized.")
+        self.beta = case["wave_heading"] * DEG2RAD
+        return (np.array(case["wave_heading"], dtype=float), [N.SPECTRUM_CODES[s] for s in case["wave_spectrum"]],
+                np.array(case["wave_height"], dtype=float), np.array(case["wave_period"], dtype=float),
+                np.array(case["wave_gamma"], dtype=float))
+
+    def calcHydroExcitation(self, case, memberList=[], dgamma=0):
+        """Sea state + strip-theory inertial excitation (raft/raft_fowt.py:972-1149) on the
+        device.  Sets beta, S, zeta, F_hydro_iner [nWaves,6,nw], F_BEM and the per-member
+        kinematics mem.u/ud/pDyn like the reference."""
+        import torch
+        dd = self.device_design()
+        hd, spec, Hs, Tp, gam = self._sea_state(case)
+        nW = self.nWaves
+        heads = dd.ensure_headings(hd * DEG2RAD)
+        dev = dd.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        S = torch.empty([nW, self.nw], **f64)
+        zeta = torch.empty([nW, self.nw], **f64)
+        spec_t = torch.tensor(spec, dtype=torch.int32, device=dev)
+        Hs_t, Tp_t, g_t = (torch.tensor(x, **f64) for x in (Hs, Tp, gam))
+        N.check(N.lib().rh_sea_state(N.context(dd.dev_index), nW, self.nw, N.ptr(dd.w), float(self.dw), N.ptr(spec_t),
+                                     N.ptr(Hs_t), N.ptr(Tp_t), N.ptr(g_t), N.ptr(S), N.ptr(zeta),
+                                     N.stream_handle(torch, dev)), "rh_sea_state")
+        hidx = torch.tensor(heads, dtype=torch.long, device=dev)
+        F = dd.finer.index_select(0, hidx) * zeta[:, None, :]
+        self._zeta_dev = zeta
+        self._heads = heads
+        self.S = S.cpu().numpy()
+        self.zeta = zeta.cpu().numpy().astype(complex)
+        self.F_hydro_iner = F.cpu().numpy()
+        self.F_BEM = np.zeros([nW, 6, self.nw], dtype=complex)
+        self._fill_member_kinematics(memberList, dd, heads, zeta)
+
+    def _fill_member_kinematics(self, memberList, dd, heads, zeta):
+        """mem.u / ud / pDyn side effects (raft/raft_fowt.py:1021-1024,1108-1110)."""
+        if not memberList:
+            return
+        U = (dd.uhat.index_select(0, dd.torch.tensor(heads, dtype=dd.torch.long, device=dd.device))
+             * zeta[:, None, None, :]).cpu().numpy()
+        w = self.w
+        j = 0
+        for mem in self.memberList:
+            mem.u = np.zeros([self.nWaves, mem.ns, 3, self.nw], dtype=complex)
+            mem.ud = np.zeros_like(mem.u)
+            for il in range(mem.ns):
+                if mem.r[il, 2] < 0:
+                    mem.u[:, il] = U[:, j]
+                    mem.ud[:, il] = 1j * w * U[:, j]
+                    j += 1
+
+    # ------------------------------------------------------------------ drag
+    def calcHydroLinearization(self, Xi):
+        """Borgman drag linearisation for the response Xi [6,nw] (raft/raft_fowt.py:1152-1266):
+        returns B_hydro_drag [6,6]; sets mem.Bmat, self.F_hydro_drag (sea state 0)."""
+        import torch
+        dd = self.device_design()
+        if getattr(self, "_zeta_dev", None) is None:
+            raise RuntimeError("calcHydroExcitation must be called first (wave kinematics)")
+        dev = dd.device
+        Xi_t = torch.tensor(np.asarray(Xi, dtype=complex), dtype=torch.complex128, device=dev).contiguous()
+        B = torch.empty(36, dtype=torch.float64, device=dev)
+        Bm = torch.zeros([max(dd.nn, 1), 9], dtype=torch.float64, device=dev)
+        F = torch.empty([6, self.nw], dtype=torch.complex128, device=dev)
+        z0 = self._zeta_dev[0].contiguous()
+        d = dd.struct()
+        N.check(N.lib().rh_linearize(N.context(dd.dev_index), ctypes.byref(d), int(self._heads[0]), N.ptr(Xi_t),
+                                     N.ptr(z0), N.ptr(B), N.ptr(Bm), N.ptr(F), N.stream_handle(torch, dev)),
+                "rh_linearize")
+        self._Bmat_dev = Bm
+        self.B_hydro_drag = B.reshape(6, 6).cpu().numpy()
+        self.F_hydro_drag = F.cpu().numpy()
+        self._scatter_bmat(Bm.cpu().numpy())
+        return self.B_hydro_drag
+
+    def _scatter_bmat(self, bm):
+        j = 0
+        for mem in self.memberList:
+            mem.Bmat = np.zeros([mem.ns, 3, 3])
+            for il in range(mem.ns):
+                if mem.r[il, 2] < 0:
+                    mem.Bmat[il] = bm[j].reshape(3, 3)
+                    j += 1
+
+    def calcDragExcitation(self, ih):
+        """raft/raft_fowt.py:1270-1293"""
+        import torch
+        dd = self.device_design()
+        dev = dd.device
+        F = torch.empty([6, self.nw], dtype=torch.complex128, device=dev)
+        d = dd.struct()
+        z = self._zeta_dev[ih].contiguous()
+        N.check(N.lib().rh_drag_excitation(N.context(dd.dev_index), ctypes.byref(d), int(self._heads[ih]), N.ptr(z),
+                                           N.ptr(self._Bmat_dev), N.ptr(F), N.stream_handle(torch, dev)),
+                "rh_drag_excitation")
+        self.F_hydro_drag = F.cpu().numpy()
+        return self.F_hydro_drag
+
+    # ------------------------------------------------------------------ outputs
+    def saveTurbineOutputs(self, results, case):
+        """Motion part of raft/raft_fowt.py:1821-1875 plus wave_PSD (:1974).  The rotor,
+        tower-base and mooring-tension channels need statics/rotor/MoorPy data that the
+        accelerated path does not build."""
+        self.Xi0 = self.r6 - np.array([self.x_ref, self.y_ref, 0, 0, 0, 0])
+        stats = getattr(self, "_stats", None)
+        for i, dof in enumerate(["surge", "sway", "heave", "roll", "pitch", "yaw"]):
+            conv = 57.29577951308232 if i >= 3 else 1.0
+            x = self.Xi[:, i, :] * conv
+            avg = self.Xi0[i] * conv
+            std = stats["std"][i] if stats is not None else np.sqrt(0.5 * np.sum(np.abs(x) ** 2))
+            psd = stats["psd"][i] if stats is not None else np.sum(0.5 * np.abs(x) ** 2 / self.dw, axis=0)
+            results[f"{dof}_avg"] = avg
+            results[f"{dof}_std"] = std
+            results[f"{dof}_max"] = avg + 3 * std
+            results[f"{dof}_min"] = avg - 3 * std
+            results[f"{dof}_PSD"] = psd
+            results[f"{dof}_RA"] = x
+        results["wave_PSD"] = np.sum(0.5 * np.abs(self.zeta) ** 2 / self.dw, axis=0)

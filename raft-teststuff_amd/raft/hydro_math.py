@@ -1,0 +1,130 @@
+"""Host-side scalar/vector math used by the per-design preparation.
+
+Restatements of the reference helpers the prep needs (raft/helpers.py); the per-bin and
+per-node arithmetic of the response solve itself runs in librafthip (no NumPy hot loops
+here).  Everything is plain NumPy on small arrays, executed once per design.
+"""
+import numpy as np
+
+RAD2DEG = 57.29577951308232       # raft/helpers.py:25
+DEG2RAD = 0.017453292519943295    # raft/helpers.py:27
+
+
+def rad2deg(x):
+    return x * RAD2DEG
+
+
+def deg2rad(x):
+    return x * DEG2RAD
+
+
+def wave_numbers(omegas, h, e=0.001, g=9.81):
+    """Vectorised form of the reference's scalar fixed-point dispersion iteration
+    (raft/helpers.py:295-310): every element iterates independently until ITS OWN
+    relative change is <= e, so each result is bit-identical to the scalar loop
+    (tolerance 1e-3, not the exact root)."""
+    w = np.atleast_1d(np.asarray(omegas, dtype=float))
+    k1 = w * w / g
+    k2 = w * w / (np.tanh(k1 * h) * g)
+    active = np.abs(k2 - k1) / k1 > e
+    while active.any():
+        k1 = np.where(active, k2, k1)
+        k2n = w * w / (np.tanh(k1 * h) * g)
+        k2 = np.where(active, k2n, k2)
+        active = active & (np.abs(k2 - k1) / k1 > e)
+    return k2
+
+
+def rotation_matrix(x3, x2, x1):
+    """z-y-x intrinsic rotation (raft/helpers.py:357-384)."""
+    s1, c1 = np.sin(x1), np.cos(x1)
+    s2, c2 = np.sin(x2), np.cos(x2)
+    s3, c3 = np.sin(x3), np.cos(x3)
+    return np.array([[c1 * c2, c1 * s2 * s3 - c3 * s1, s1 * s3 + c1 * c3 * s2],
+                     [c2 * s1, c1 * c3 + s1 * s2 * s3, c3 * s1 * s2 - c1 * s3],
+                     [-s2, c2 * s3, c2 * c3]])
+
+
+def alternator(r):
+    """getH (raft/helpers.py:346-355)."""
+    return np.array([[0, r[2], -r[1]], [-r[2], 0, r[0]], [r[1], -r[0], 0]])
+
+
+def translate_matrix_3to6(Min, r):
+    """raft/helpers.py:455-478"""
+    H = alternator(r)
+    out = np.zeros([6, 6])
+    out[:3, :3] = Min
+    out[:3, 3:] = Min @ H
+    out[3:, :3] = out[:3, 3:].T
+    out[3:, 3:] = H @ Min @ H.T
+    return out
+
+
+def translate_matrix_6to6(Min, r):
+    """raft/helpers.py:481-503"""
+    H = alternator(r)
+    out = np.zeros([6, 6])
+    out[:3, :3] = Min[:3, :3]
+    out[:3, 3:] = Min[:3, :3] @ H + Min[:3, 3:]
+    out[3:, :3] = out[:3, 3:].T
+    out[3:, 3:] = H @ Min[:3, :3] @ H.T + Min[3:, :3] @ H + H.T @ Min[:3, 3:] + Min[3:, 3:]
+    return out
+
+
+def get_from_dict(d, key, shape=0, dtype=float, default=None, index=None):
+    """Input parsing with the reference's tiling / indexing rules (raft/helpers.py:697-775).
+
+    Note the reference's rule for a 1-D list with `index`: it returns val[index] tiled,
+    which is how e.g. `Cd: [1.5, 2.2]` becomes Cd_p1 = 1.5, Cd_p2 = 2.2."""
+    if key in d:
+        val = d[key]
+        if shape == 0:
+            if np.isscalar(val):
+                return dtype(val)
+            raise ValueError(f"Value for key '{key}' is expected to be a scalar but instead is: {val}")
+        if shape == -1:
+            return dtype(val) if np.isscalar(val) else np.array(val, dtype=dtype)
+        if np.isscalar(val):
+            return np.tile(dtype(val), shape)
+        if np.isscalar(shape):
+            if len(val) != shape:
+                raise ValueError(f"Value for key '{key}' is not the expected size of {shape} and is instead: {val}")
+            if index is None:
+                return np.array([dtype(v) for v in val])
+            ks = np.array(val).shape
+            if len(ks) == 1:
+                if index in range(ks[0]):
+                    return np.tile(val[index], shape)
+                raise ValueError(f"Value for index '{index}' is not within the size of {val} (len={ks[0]})")
+            if index in range(ks[1]):
+                return np.array([v[index] for v in val])
+            raise ValueError(f"Value for index '{index}' is not within the size of {val} (len={ks[0]})")
+        vala = np.array(val, dtype=dtype)
+        if list(vala.shape) == list(shape):
+            return vala
+        if len(shape) > 2:
+            raise ValueError("Function getFromDict isn't set up for shapes larger than 2 dimensions")
+        if vala.ndim == 1 and len(vala) == shape[1]:
+            return np.tile(vala, [shape[0], 1])
+        raise ValueError(f"Value for key '{key}' is not a compatible size for target size of {shape} and is instead: {val}")
+    if default is None:
+        raise ValueError(f"Key '{key}' not found in input file...")
+    if shape == 0 or shape == -1:
+        return default
+    if np.isscalar(default):
+        return np.tile(default, shape)
+    return np.tile(default, [shape, 1])
+
+
+def get_rao(Xi, zeta):
+    """raft/helpers.py:665-684 (host convenience for small arrays)."""
+    zeta = np.asarray(zeta)
+    if zeta.ndim != 1:
+        raise Exception("zeta must be a 1D array")
+    if Xi.shape[-1] != len(zeta):
+        raise Exception("The last dimension of Xi must be the same length as zeta")
+    idx = np.where(np.abs(zeta) > 1e-6)
+    out = np.zeros_like(Xi, dtype=complex)
+    out[..., idx] = Xi[..., idx] / zeta[idx]
+    return out

@@ -1,0 +1,149 @@
+"""Per-design device tables: the host -> HBM layout of everything the kernels read.
+
+Layout in HBM (one design, nn submerged nodes, nw bins, nh headings):
+  node      float64 [RH_NF_COUNT][nn]     struct-of-arrays node table (wave-uniform reads)
+  imat_mcf  complex128 [nn][9][nw]        only when some member uses MacCamy-Fuchs
+  uhat      complex128 [nh][nn][3][nw]    unit-amplitude wave velocity, bins contiguous
+  finer     complex128 [nh][6][nw]        unit-amplitude inertial excitation
+  M, B      float64 [36] or [nw][36]      M_lin, B_lin (raft/raft_model.py:911-912)
+  C         float64 [36]                  C_lin (raft/raft_model.py:913)
+uhat is what the case kernel streams twice per drag iteration; bins are contiguous so a
+wavefront (64 consecutive bins) reads 1 KiB per component per node.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+SQRT_8_PI_NOTE = "Borgman factor sqrt(8/pi) applied on the device (raft/raft_fowt.py:1223)"
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise N.NativeError("librafthip needs a visible MI355X (torch.cuda.is_available() is False); "
+                            "there is no CPU fallback")
+    return torch
+
+
+def node_table(fowt):
+    """Gather the submerged strip nodes of all members (reference member/node order) into
+    the [RH_NF_COUNT][nn] table and the optional MCF Imat block.  Areas follow
+    raft/raft_fowt.py:1199-1238 (incl. SURVEY.md Q4 for the rectangular axial area)."""
+    cols = []
+    mcf_blocks = []
+    any_mcf = False
+    for mem in fowt.memberList:
+        circ = mem.shape == "circular"
+        for il in range(mem.ns):
+            if not (mem.r[il, 2] < 0):
+                continue
+            ds, drs, dls = np.atleast_1d(mem.ds[il]), np.atleast_1d(mem.drs[il]), mem.dls[il]
+            if circ:
+                a_q = np.pi * ds[0] * dls
+                a_p1 = ds[0] * dls
+                a_p2 = ds[0] * dls
+                a_end = np.abs(np.pi * ds[0] * drs[0])
+            else:
+                a_q = 2 * (ds[0] + ds[0]) * dls
+                a_p1 = ds[0] * dls
+                a_p2 = ds[1] * dls
+                a_end = np.abs((ds[0] + drs[0]) * (ds[1] + drs[1]) - (ds[0] - drs[0]) * (ds[1] - drs[1]))
+            r = mem.r[il]
+            rr = mem.r[il] - fowt.r6[:3]
+            use_mcf = bool(mem.MCF and mem.Imat_MCF is not None)
+            any_mcf |= use_mcf
+            col = [r[0], r[1], r[2], rr[0], rr[1], rr[2], *mem.q, *mem.p1, *mem.p2,
+                   a_q, a_p1, a_p2, a_end,
+                   mem.coef("Cd_q", il), mem.coef("Cd_p1", il), mem.coef("Cd_p2", il), mem.coef("Cd_End", il),
+                   1.0 if circ else 0.0, mem.a_i[il], 1.0 if use_mcf else 0.0, *mem.Imat[il].ravel()]
+            cols.append(col)
+            mcf_blocks.append(mem.Imat_MCF[il].reshape(9, -1) if use_mcf else None)
+    table = np.array(cols, dtype=float).T.copy() if cols else np.zeros([N.NF_COUNT, 0])
+    imat = None
+    if any_mcf:
+        imat = np.zeros([len(cols), 9, fowt.nw], dtype=complex)
+        for i, blk in enumerate(mcf_blocks):
+            if blk is not None:
+                imat[i] = blk
+    return table, imat
+
+
+def linear_matrices(fowt):
+    """M_lin, B_lin, C_lin without rotor aero (raft/raft_model.py:911-913).  Returns
+    (M, B, C, per_bin) with M, B of shape [nw,6,6] when frequency dependent else [6,6]."""
+    A_BEM = np.asarray(fowt.A_BEM)
+    B_BEM = np.asarray(fowt.B_BEM)
+    B_gyro = np.sum(fowt.B_gyro, axis=2) if getattr(fowt, "B_gyro", None) is not None and np.ndim(fowt.B_gyro) == 3 \
+        else np.zeros([6, 6])
+    per_bin = bool(np.any(A_BEM) or np.any(B_BEM))
+    C = (fowt.C_struc + fowt.C_moor) + fowt.C_hydro
+    if per_bin:
+        M = (fowt.M_struc[:, :, None] + A_BEM) + fowt.A_hydro_morison[:, :, None]
+        B = (fowt.B_struc[:, :, None] + B_BEM) + B_gyro[:, :, None]
+        return np.moveaxis(M, 2, 0).copy(), np.moveaxis(B, 2, 0).copy(), C, True
+    M = fowt.M_struc + fowt.A_hydro_morison
+    B = fowt.B_struc + B_gyro
+    return M, B, C, False
+
+
+class DeviceDesign:
+    """Device-resident tables of one FOWT design (caller-owned torch buffers)."""
+
+    def __init__(self, fowt, device=0):
+        torch = _torch()
+        self.torch = torch
+        self.device = torch.device("cuda", device)
+        self.dev_index = device
+        self.nw = fowt.nw
+        table, imat = node_table(fowt)
+        self.nn = table.shape[1]
+        f64 = dict(dtype=torch.float64, device=self.device)
+        self.w = torch.tensor(fowt.w, **f64)
+        self.k = torch.tensor(fowt.k, **f64)
+        self.node = torch.tensor(table if self.nn else np.zeros([N.NF_COUNT, 1]), **f64).contiguous()
+        self.imat = torch.tensor(imat, dtype=torch.complex128, device=self.device) if imat is not None else None
+        M, B, C, per_bin = linear_matrices(fowt)
+        self.per_bin = per_bin
+        self.M = torch.tensor(M, **f64).contiguous()
+        self.B = torch.tensor(B, **f64).contiguous()
+        self.C = torch.tensor(C, **f64).contiguous()
+        self.dw, self.depth, self.rho, self.g = float(fowt.dw), float(fowt.depth), float(fowt.rho_water), float(fowt.g)
+        self.headings = None           # tuple of tabulated headings (rad)
+        self.uhat = None
+        self.finer = None
+
+    def struct(self):
+        d = N.RhDesign()
+        d.nw, d.nn = self.nw, self.nn
+        d.nhead = 0 if self.headings is None else len(self.headings)
+        d.mb_per_bin = 1 if self.per_bin else 0
+        d.dw, d.depth, d.rho, d.g = self.dw, self.depth, self.rho, self.g
+        d.pdyn_rho_g = 1025.0 * 9.81   # getWaveKin defaults (raft/helpers.py:105, raft/raft_fowt.py:1109)
+        d.w, d.k, d.node = N.ptr(self.w), N.ptr(self.k), N.ptr(self.node)
+        d.imat_mcf = N.ptr(self.imat)
+        d.uhat, d.finer = N.ptr(self.uhat), N.ptr(self.finer)
+        d.M, d.B, d.C = N.ptr(self.M), N.ptr(self.B), N.ptr(self.C)
+        return d
+
+    def ensure_headings(self, betas):
+        """Tabulate unit-amplitude kinematics for the given headings (rad).  Returns the
+        table index of each requested heading."""
+        betas = [float(b) for b in np.atleast_1d(betas)]
+        have = list(self.headings) if self.headings is not None else []
+        missing = [b for b in dict.fromkeys(betas) if b not in have]
+        if missing or self.uhat is None:
+            allh = have + missing
+            torch = self.torch
+            nh = len(allh)
+            self.uhat = torch.empty([nh, max(self.nn, 1), 3, self.nw], dtype=torch.complex128, device=self.device)
+            self.finer = torch.empty([nh, 6, self.nw], dtype=torch.complex128, device=self.device)
+            self.headings = tuple(allh)
+            beta_t = torch.tensor(allh, dtype=torch.float64, device=self.device)
+            d = self.struct()
+            N.check(N.lib().rh_wave_tables(N.context(self.dev_index), ctypes.byref(d), N.ptr(beta_t),
+                                           N.ptr(self.uhat), N.ptr(self.finer), N.stream_handle(torch, self.device)),
+                    "rh_wave_tables")
+            self._beta_keep = beta_t
+        return [self.headings.index(b) for b in betas]

@@ -1,0 +1,121 @@
+"""Batched response solve on the device: the throughput path behind Model.solveDynamics /
+analyzeCases and bench.py.
+
+A batch is any number of sea-state cases over one or more DeviceDesigns that share a
+frequency grid.  One C-ABI call (rh_solve_cases) runs the full drag fixed point of every
+case, one workgroup per case; cases are launched sorted by (design, heading) so the
+blocks an XCD receives stream the same wave tables out of its L2.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .hydro_math import DEG2RAD
+
+
+class CaseSet:
+    """Host description of a batch of cases, all with a single sea state (nWaves = 1).
+
+    design_idx : index into the design list, per case
+    heading    : wave heading [deg]
+    spectrum   : 'JONSWAP' | 'unit' | 'constant' | 'none' (or integer codes)
+    Hs, Tp, gamma : wave_height, wave_period, wave_gamma (0 -> IEC automatic)
+    """
+
+    def __init__(self, design_idx, heading, spectrum, Hs, Tp, gamma):
+        n = len(heading)
+        self.n = n
+        self.design_idx = np.broadcast_to(np.asarray(design_idx, dtype=np.int32), (n,)).copy()
+        self.heading = np.asarray(heading, dtype=float)
+        sp = np.broadcast_to(np.asarray(spectrum, dtype=object), (n,))
+        self.spectrum = np.array([s if isinstance(s, (int, np.integer)) else N.SPECTRUM_CODES[str(s)] for s in sp],
+                                 dtype=np.int32)
+        self.Hs = np.broadcast_to(np.asarray(Hs, dtype=float), (n,)).copy()
+        self.Tp = np.broadcast_to(np.asarray(Tp, dtype=float), (n,)).copy()
+        self.gamma = np.broadcast_to(np.asarray(gamma, dtype=float), (n,)).copy()
+
+
+class BatchResult(dict):
+    """Device tensors of one batched solve (keys: Xi, iters, status, zeta, B_drag, psd, std,
+    Bmat, rao, Z when requested)."""
+
+    def host(self):
+        return {k: v.cpu().numpy() for k, v in self.items()}
+
+
+def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std", "zeta", "B_drag"),
+                fext=None, stream=None, prepared=None):
+    """Run rh_solve_cases.  `designs`: list of DeviceDesign (same nw); `cases`: CaseSet.
+    Returns a BatchResult of device tensors (stream-ordered; caller synchronises)."""
+    d0 = designs[0]
+    torch = d0.torch
+    dev = d0.device
+    nw = d0.nw
+    for d in designs:
+        if d.nw != nw:
+            raise ValueError("all designs in a batch must share the frequency grid")
+    prep = prepared if prepared is not None else prepare_batch(designs, cases)
+    ncase = cases.n
+    out = BatchResult()
+    c128 = dict(dtype=torch.complex128, device=dev)
+    f64 = dict(dtype=torch.float64, device=dev)
+    out["Xi"] = torch.empty([ncase, 6, nw], **c128)
+    xl = torch.empty([ncase, 6, nw], **c128)
+    out["iters"] = torch.empty([ncase], dtype=torch.int32, device=dev)
+    out["status"] = torch.empty([ncase], dtype=torch.int32, device=dev)
+    nnmax = max(d.nn for d in designs)
+    if "zeta" in want:
+        out["zeta"] = torch.empty([ncase, nw], **f64)
+    if "B_drag" in want:
+        out["B_drag"] = torch.empty([ncase, 6, 6], **f64)
+    if "Bmat" in want:
+        out["Bmat"] = torch.empty([ncase, nnmax, 3, 3], **f64)
+    if "psd" in want:
+        out["psd"] = torch.empty([ncase, 6, nw], **f64)
+    if "std" in want:
+        out["std"] = torch.empty([ncase, 6], **f64)
+    if "rao" in want:
+        out["rao"] = torch.empty([ncase, 6, nw], **c128)
+    if "Z" in want:
+        out["Z"] = torch.empty([ncase, nw, 6, 6], **c128)
+    cs = N.RhCases()
+    cs.ncase = ncase
+    cs.design, cs.head, cs.spectrum = N.ptr(prep["design"]), N.ptr(prep["head"]), N.ptr(prep["spectrum"])
+    cs.Hs, cs.Tp, cs.gamma = N.ptr(prep["Hs"]), N.ptr(prep["Tp"]), N.ptr(prep["gamma"])
+    cs.nIter, cs.XiStart, cs.tol = int(nIter), float(XiStart), float(tol)
+    cs.fext = N.ptr(fext)
+    cs.order = N.ptr(prep["order"])
+    o = N.RhSolveOut()
+    o.Xi, o.Xi_last, o.iters, o.status = N.ptr(out["Xi"]), N.ptr(xl), N.ptr(out["iters"]), N.ptr(out["status"])
+    for k in ["zeta", "B_drag", "Bmat", "psd", "std", "rao", "Z"]:
+        setattr(o, k, N.ptr(out.get(k)))
+    arr = (N.RhDesign * len(designs))(*[d.struct() for d in designs])
+    s = stream if stream is not None else N.stream_handle(torch, dev)
+    N.check(N.lib().rh_solve_cases(N.context(d0.dev_index), arr, len(designs), ctypes.byref(cs), ctypes.byref(o), s),
+            "rh_solve_cases")
+    out._keep = (xl, prep, arr)
+    return out
+
+
+def prepare_batch(designs, cases):
+    """Upload per-case parameters and make sure every design has the wave tables its cases
+    need.  Reusable across repeated solves of the same batch (bench steady state)."""
+    torch = designs[0].torch
+    dev = designs[0].device
+    head = np.zeros(cases.n, dtype=np.int32)
+    for di, d in enumerate(designs):
+        sel = np.nonzero(cases.design_idx == di)[0]
+        if len(sel) == 0:
+            continue
+        betas = cases.heading[sel] * DEG2RAD
+        head[sel] = d.ensure_headings(betas)
+    if cases.design_idx.min() < 0 or cases.design_idx.max() >= len(designs):
+        raise ValueError("design index out of range")
+    order = np.lexsort((head, cases.design_idx)).astype(np.int32)
+    i32 = dict(dtype=torch.int32, device=dev)
+    f64 = dict(dtype=torch.float64, device=dev)
+    return dict(design=torch.tensor(cases.design_idx, **i32), head=torch.tensor(head, **i32),
+                spectrum=torch.tensor(cases.spectrum, **i32), Hs=torch.tensor(cases.Hs, **f64),
+                Tp=torch.tensor(cases.Tp, **f64), gamma=torch.tensor(cases.gamma, **f64),
+                order=torch.tensor(order, **i32), head_host=head)

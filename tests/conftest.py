@@ -1,0 +1,53 @@
+"""Shared test set-up.
+
+Markers: `gpu` -- needs an MI355X and the built librafthip.so (parity tests proper);
+everything else runs on the CPU of the build container (oracle vs golden vectors, host
+preparation, C-ABI symbol check, gloo multi-process logic)."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "raft-teststuff_amd")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X GPU and librafthip.so")
+
+
+def load_golden(tag):
+    return dict(np.load(os.path.join(GOLDEN, tag + ".npz")))
+
+
+def load_design(name):
+    with open(os.path.join(GOLDEN, "designs", name + ".json")) as f:
+        return json.load(f)
+
+
+def golden_cases(T):
+    """Case dicts of a golden_solve fixture (scalars for single sea states)."""
+    out = []
+    for c in json.loads(str(T["cases_json"])):
+        case = {k: (v if len(v) > 1 else v[0]) for k, v in c.items() if v is not None}
+        case.setdefault("wind_speed", 0)
+        out.append(case)
+    return out
+
+
+STATICS_KEYS = ["M_struc", "B_struc", "C_struc", "C_hydro", "C_moor", "W_struc", "W_hydro"]
+
+
+def statics_of(T):
+    return {k: T[k] for k in STATICS_KEYS}
+
+
+@pytest.fixture(scope="session")
+def golden():
+    return load_golden

@@ -1,0 +1,300 @@
+"""Generate the committed golden fixtures by running the READ-ONLY reference
+(/root/reference/raft, RAFT v1.3.1 fork) inside the build container.
+
+This script is test infrastructure only.  It never ships to the GPU box; what it
+writes (tests/golden/*.npz, *.json) are plain data files: reference INPUT tables
+and reference OUTPUT vectors.  No reference source text is copied.
+
+Run (from the repo root, in the build container):
+
+    PYTHONDONTWRITEBYTECODE=1 OPENBLAS_NUM_THREADS=1 \
+    PYTHONPATH=tests/golden/refshim:/root/reference python tests/golden/make_golden.py [which...]
+
+`tests/golden/refshim` holds inert stand-ins for the two absent third-party
+packages the reference imports at module scope (MoorPy, CCBlade).
+Neither is on the hot path: mooring stiffness is an INPUT matrix (set explicitly
+from C_MOOR below, as SURVEY.md §8(c) prescribes) and every golden case runs with
+wind_speed = 0, so rotor aerodynamics are never evaluated
+(reference raft/raft_fowt.py:801).
+
+Iteration counts are read from the reference's own display=2 message
+"Iteration k, converged" (raft/raft_model.py:963-964).
+"""
+import contextlib
+import io
+import json
+import os
+import re
+import sys
+import time
+
+import numpy as np
+import yaml
+
+import raft  # the reference, from PYTHONPATH
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+# Stand-in mooring stiffness (SURVEY.md §6 / BASELINE.md: diag(7e4,7e4,2e4,1e7,1e7,1e8)).
+C_MOOR = np.diag([7e4, 7e4, 2e4, 1e7, 1e7, 1e8])
+
+
+def load_design(path, **settings):
+    with open(path) as f:
+        design = yaml.load(f, Loader=yaml.FullLoader)
+    for k, v in settings.items():
+        design["settings"][k] = v
+    return design
+
+
+def prepare_fowt(fowt, case):
+    """Per-case preparation exactly as Model.analyzeCases/solveStatics would leave the
+    FOWT for solveDynamics when the platform sits at its reference position
+    (raft/raft_model.py:258-260, :286 with zero mean offset)."""
+    fowt.setPosition(np.array([fowt.x_ref, fowt.y_ref, 0, 0, 0, 0], dtype=float))
+    fowt.calcStatics()
+    fowt.calcTurbineConstants(case, ptfm_pitch=0)
+    fowt.calcHydroConstants()
+    fowt.C_moor = C_MOOR.copy()
+
+
+def design_tables(fowt):
+    """Dump every per-design input the hot path consumes, node by node, in reference
+    order (member list order, node order within member).  Only submerged nodes
+    (r_z < 0 strictly, raft/raft_fowt.py:1104,1188) carry hydrodynamics."""
+    rows = []
+    for im, mem in enumerate(fowt.memberList):
+        circ = mem.shape == "circular"
+        for il in range(mem.ns):
+            ls = mem.ls[il]
+            row = dict(
+                member=im, node=il, circ=int(circ), sub=int(mem.r[il, 2] < 0),
+                mcf=int(bool(mem.MCF)),
+                r=mem.r[il, :].copy(), r_rel=(mem.r[il, :] - fowt.r6[:3]).copy(),
+                q=mem.q.copy(), p1=mem.p1.copy(), p2=mem.p2.copy(),
+                ds=np.atleast_1d(mem.ds[il]).astype(float),
+                drs=np.atleast_1d(mem.drs[il]).astype(float),
+                dls=float(mem.dls[il]),
+                Cd_q=np.interp(ls, mem.stations, mem.Cd_q), Cd_p1=np.interp(ls, mem.stations, mem.Cd_p1),
+                Cd_p2=np.interp(ls, mem.stations, mem.Cd_p2), Cd_End=np.interp(ls, mem.stations, mem.Cd_End),
+                Ca_p1=np.interp(ls, mem.stations, mem.Ca_p1), Ca_p2=np.interp(ls, mem.stations, mem.Ca_p2),
+                Ca_End=np.interp(ls, mem.stations, mem.Ca_End),
+                a_i=float(mem.a_i[il]),
+                Imat=mem.Imat[il].copy(),
+            )
+            rows.append((row, mem.Imat_MCF[il] if mem.MCF else None))
+    n = len(rows)
+    out = {}
+    for key in ["member", "node", "circ", "sub", "mcf"]:
+        out["node_" + key] = np.array([r[0][key] for r in rows], dtype=np.int64)
+    for key in ["r", "r_rel", "q", "p1", "p2"]:
+        out["node_" + key] = np.array([r[0][key] for r in rows])
+    out["node_ds"] = np.array([np.resize(r[0]["ds"], 2) for r in rows])
+    out["node_drs"] = np.array([np.resize(r[0]["drs"], 2) for r in rows])
+    for key in ["dls", "Cd_q", "Cd_p1", "Cd_p2", "Cd_End", "Ca_p1", "Ca_p2", "Ca_End", "a_i"]:
+        out["node_" + key] = np.array([r[0][key] for r in rows], dtype=float)
+    out["node_Imat"] = np.array([r[0]["Imat"] for r in rows])
+    nw = fowt.nw
+    imcf = np.zeros((n, 3, 3, nw), dtype=complex)
+    for i, (_, im) in enumerate(rows):
+        if im is not None:
+            imcf[i] = im
+    if out["node_mcf"].any():
+        out["node_Imat_MCF"] = imcf
+    out["w"] = fowt.w.copy()
+    out["k"] = fowt.k.copy()
+    out["dw"] = np.float64(fowt.dw)
+    out["depth"] = np.float64(fowt.depth)
+    out["rho"] = np.float64(fowt.rho_water)
+    out["g"] = np.float64(fowt.g)
+    out["r6"] = fowt.r6.copy()
+    for key in ["M_struc", "B_struc", "C_struc", "C_hydro", "C_moor", "A_hydro_morison", "W_struc", "W_hydro"]:
+        out[key] = np.array(getattr(fowt, key), dtype=float)
+    out["A_BEM"] = fowt.A_BEM.copy()
+    out["B_BEM"] = fowt.B_BEM.copy()
+    out["member_names"] = np.array([m.name for m in fowt.memberList])
+    return out
+
+
+def run_solve(model, case, tol=0.01):
+    buf = io.StringIO()
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(buf):
+        Xi = model.solveDynamics(case, tol=tol, display=2)
+    dt = time.perf_counter() - t0
+    txt = buf.getvalue()
+    m = re.findall(r"Iteration (\d+), converged", txt)
+    if m:
+        iters, conv = int(m[0]) + 1, 1
+    else:
+        iters, conv = int(model.nIter) + 1, 0
+    return np.array(Xi), iters, conv, dt
+
+
+def case_dict(design, row):
+    c = dict(zip(design["cases"]["keys"], row))
+    c["wind_speed"] = 0  # golden cases: no rotor aerodynamics (see module doc)
+    return c
+
+
+def golden_solve(tag, yaml_path, cases, settings=None, keep_Z=False):
+    settings = settings or {}
+    design = load_design(yaml_path, **settings)
+    model = raft.Model(design)
+    fowt = model.fowtList[0]
+    out = {}
+    caseout = {k: [] for k in ["Xi", "iters", "conv", "B_drag", "F_iner", "F_drag", "zeta", "S", "seconds"]}
+    if keep_Z:
+        caseout["Z"] = []
+    metrics = []
+    for c in cases:
+        case = dict(c)
+        prepare_fowt(fowt, case)
+        if not out:
+            out.update(design_tables(fowt))
+        Xi, iters, conv, dt = run_solve(model, case)
+        caseout["Xi"].append(Xi)
+        caseout["iters"].append(iters)
+        caseout["conv"].append(conv)
+        caseout["B_drag"].append(fowt.B_hydro_drag.copy())
+        caseout["F_iner"].append(fowt.F_hydro_iner.copy())
+        caseout["F_drag"].append(fowt.F_hydro_drag.copy())
+        caseout["zeta"].append(fowt.zeta.copy())
+        caseout["S"].append(fowt.S.copy())
+        caseout["seconds"].append(dt)
+        if keep_Z:
+            caseout["Z"].append(fowt.Z.copy())
+        res = {}
+        fowt.saveTurbineOutputs(res, case)
+        metrics.append(res)
+        print(f"  {tag}: case {c} iters={iters} conv={conv} t={dt:.2f}s", file=sys.stderr)
+    for k, v in caseout.items():
+        out["out_" + k] = np.array(v)
+    # motion outputs of saveTurbineOutputs (raft/raft_fowt.py:1831-1875)
+    for dof in ["surge", "sway", "heave", "roll", "pitch", "yaw"]:
+        out[f"out_{dof}_std"] = np.array([m[f"{dof}_std"] for m in metrics])
+        out[f"out_{dof}_PSD"] = np.array([m[f"{dof}_PSD"] for m in metrics])
+    out["out_wave_PSD"] = np.array([m["wave_PSD"] for m in metrics])
+    out["nIter"] = np.int64(model.nIter)
+    out["XiStart"] = np.float64(model.XiStart)
+    keys = ["wave_spectrum", "wave_period", "wave_height", "wave_heading", "wave_gamma"]
+    meta = [{k: (np.atleast_1d(c[k]).tolist() if k in c else None) for k in keys} for c in cases]
+    out["cases_json"] = np.array(json.dumps(meta))
+    np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
+    print(f"wrote {tag}.npz", file=sys.stderr)
+
+
+def golden_fowt_unit(tag, yaml_path):
+    """The reference test_fowt.py workloads: F_hydro_iner over 9 headings x 4 periods x
+    2 heights (tests/test_fowt.py:214-250) and B_hydro_drag/F_hydro_drag for the
+    synthetic Xi = 0.1 exp(i linspace(0, 2pi, 6 nw)) (tests/test_fowt.py:252-277)."""
+    design = load_design(yaml_path)
+    model = raft.Model(design)
+    fowt = model.fowtList[0]
+    fowt.setPosition(np.zeros(6))
+    fowt.calcStatics()
+    out = {}
+    fowt.calcHydroConstants()
+    out.update(design_tables(fowt))
+    F = []
+    cases = []
+    for hd in [0, 45, 90, 135, 180, 225, 270, 315, 360]:
+        for tp in [5, 10, 15, 20]:
+            for hs in [1, 2]:
+                tc = {"wave_heading": hd, "wave_period": tp, "wave_height": hs}
+                fowt.calcHydroConstants()
+                fowt.calcHydroExcitation(tc, memberList=fowt.memberList)
+                F.append(fowt.F_hydro_iner.copy())
+                cases.append([hd, tp, hs])
+    out["exc_cases"] = np.array(cases, dtype=float)
+    out["exc_F_iner"] = np.array(F)
+    tc = {"wave_spectrum": "unit", "wave_heading": 0, "wave_period": 10, "wave_height": 2}
+    fowt.calcHydroExcitation(tc, memberList=fowt.memberList)
+    phase = np.linspace(0, 2 * np.pi, fowt.nw * 6).reshape(6, fowt.nw)
+    Xi = 0.1 * np.exp(1j * phase)
+    out["lin_Xi"] = Xi
+    out["lin_B_drag"] = fowt.calcHydroLinearization(Xi)
+    out["lin_F_drag"] = fowt.calcDragExcitation(0)
+    np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
+    print(f"wrote {tag}.npz", file=sys.stderr)
+
+
+def seeded_cases(n, seed, headings=(0, 30, 60, 90), hs=(1.0, 10.0), tp=(6.0, 18.0)):
+    """C2 synthetic sea states: Hs~U(1,10), Tp~U(6,18), gamma=0
+    (IEC auto), heading from the listed set, wind 0, current 0."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        out.append(dict(wind_speed=0, wind_heading=0, turbulence=0, turbine_status="operating",
+                        yaw_misalign=0, wave_spectrum="JONSWAP",
+                        wave_period=float(rng.uniform(*tp)), wave_height=float(rng.uniform(*hs)),
+                        wave_heading=float(rng.choice(headings)), wave_gamma=0.0))
+    return out
+
+
+DESIGNS = {
+    "OC3spar": "designs/OC3spar.yaml",
+    "VolturnUS-S_example": "examples/VolturnUS-S_example.yaml",
+    "VolturnUS-S_test": "tests/test_data/VolturnUS-S.yaml",
+    "OC3spar_test": "tests/test_data/OC3spar.yaml",
+    "OC4semi-RAFT_QTF": "examples/OC4semi-RAFT_QTF.yaml",
+    "VolturnUS-S_farm": "tests/test_data/VolturnUS-S_farm.yaml",
+}
+
+
+def export_designs():
+    """Design inputs as JSON fixtures (the GPU box has no /root/reference).  Only the
+    sections the accelerated path reads are kept: blade/airfoil aero tables and the
+    MoorPy line definitions are dropped (rotor aero and mooring are out of scope)."""
+    os.makedirs(os.path.join(HERE, "designs"), exist_ok=True)
+    for name, rel in DESIGNS.items():
+        with open(os.path.join(REF, rel)) as f:
+            d = yaml.load(f, Loader=yaml.FullLoader)
+        for tk in ("turbine", "turbines"):
+            ts = d.get(tk)
+            for t in (ts if isinstance(ts, list) else [ts] if ts else []):
+                for drop in ("blade", "airfoils", "pitch_control", "torque_control", "wt_ops", "gear_ratio"):
+                    t.pop(drop, None)
+        for mk in ("mooring", "moorings"):
+            if mk in d and d[mk]:
+                ms = d[mk] if isinstance(d[mk], list) else [d[mk]]
+                kept = [{"water_depth": m.get("water_depth")} for m in ms]
+                d[mk] = kept if isinstance(d[mk], list) else kept[0]
+        if "array_mooring" in d:
+            d["array_mooring"] = {"file": os.path.basename(d["array_mooring"].get("file", ""))}
+        with open(os.path.join(HERE, "designs", name + ".json"), "w") as f:
+            json.dump(d, f, indent=1, default=str)
+    print("wrote designs/*.json", file=sys.stderr)
+
+
+def main(which):
+    if "designs" in which:
+        export_designs()
+    ex = os.path.join(REF, "examples", "VolturnUS-S_example.yaml")
+    td = os.path.join(REF, "tests", "test_data")
+    if "unit" in which:
+        golden_fowt_unit("fowt_VolturnUS-S", os.path.join(td, "VolturnUS-S.yaml"))
+        golden_fowt_unit("fowt_OC3spar", os.path.join(td, "OC3spar.yaml"))
+    if "c1" in which:
+        d = load_design(os.path.join(REF, "designs", "OC3spar.yaml"))
+        cases = [case_dict(d, row) for row in d["cases"]["data"]]
+        golden_solve("c1_OC3spar", os.path.join(REF, "designs", "OC3spar.yaml"), cases, keep_Z=True)
+    if "c2small" in which:
+        # VolturnUS-S example at nw=200 (min_freq 0.001 Hz, the example's own grid)
+        cases = seeded_cases(8, 20241016)
+        golden_solve("c2_nw200", ex, cases, keep_Z=False)
+    if "c2" in which:
+        # C2 grid: min_freq 0.0002 Hz, max 0.2 Hz -> nw = 1000
+        cases = seeded_cases(4, 20241017)
+        golden_solve("c2_nw1000", ex, cases, settings=dict(min_freq=0.0002))
+    if "multi" in which:
+        # two wave headings in one case (nWaves = 2, raft/raft_model.py:1049-1065)
+        c = dict(wind_speed=0, wind_heading=0, turbulence=0, turbine_status="operating", yaw_misalign=0,
+                 wave_spectrum=["JONSWAP", "JONSWAP"], wave_period=[12.0, 8.0], wave_height=[6.0, 2.0],
+                 wave_heading=[0.0, 60.0], wave_gamma=[0.0, 2.0])
+        golden_solve("multi_heading", os.path.join(td, "VolturnUS-S.yaml"), [c])
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or ["designs", "unit", "c1", "c2small", "multi", "c2"])
