@@ -1,0 +1,178 @@
+"""Throughput benchmark of the RAFT frequency-domain response solve on MI355X.
+
+Workload (BASELINE.json configs[1]): examples/VolturnUS-S_example.yaml
+at min_freq 0.0002 Hz -> nw = 1000 bins, 53 submerged strip nodes (20 circular +
+33 rectangular), nIter = 4; a step = one batch of 512 synthetic JONSWAP sea states
+(Hs~U(1,10) m, Tp~U(6,18) s, gamma 0 = IEC auto, heading in {0,30,60,90} deg), solved to
+converged RAO + motion PSD in one device call.  Inputs (design tables, case parameters)
+are resident in HBM before the timed region.  Multi-GPU: one process per GPU, every rank
+solves its own 512-case shard (weak scaling, no data-path collective); the only
+collective is the barrier/max-time reduction of the harness.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raft-teststuff_amd"))
+
+NCASE = 512
+PEAK_FP64 = 78.6e12   # MI355X FP64 dense peak (vector = matrix rate), FLOP/s
+
+
+def flops_per_case(n_loop, nw, nc, nr, nsub):
+    """SURVEY.md §8(d) fixed formula: F_case = n_loop*nw*(142 Nc + 158 Nr + 1340) + nw*(100 Nsub + 1400)."""
+    return n_loop * nw * (142 * nc + 158 * nr + 1340) + nw * (100 * nsub + 1400)
+
+
+def build_model(device):
+    import raft
+    from raft import _native  # noqa: F401
+    T = dict(np.load(os.path.join(ROOT, "tests", "golden", "c2_nw1000.npz")))
+    with open(os.path.join(ROOT, "tests", "golden", "designs", "VolturnUS-S_example.json")) as f:
+        design = json.load(f)
+    design["settings"]["min_freq"] = 0.0002
+    statics = {k: T[k] for k in ["M_struc", "B_struc", "C_struc", "C_hydro", "C_moor"]}
+    m = raft.Model(design, statics=[statics], device=device)
+    f = m.fowtList[0]
+    f.setPosition(T["r6"])
+    f.calcStatics()
+    f.calcHydroConstants()
+    return m, f, T
+
+
+def sea_states(n, seed):
+    rng = np.random.default_rng(seed)
+    return [dict(wave_spectrum="JONSWAP", wave_period=float(rng.uniform(6, 18)), wave_height=float(rng.uniform(1, 10)),
+                 wave_heading=float(rng.choice([0, 30, 60, 90])), wave_gamma=0.0) for _ in range(n)]
+
+
+def cpu_baseline(T, seconds=20.0):
+    """Reference-structured NumPy port (oracle, loop flavour) on ONE host core for a bounded
+    sample of the same workload: whole C2 cases, as many as fit in ~`seconds`."""
+    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+    sys.path.insert(0, ROOT)
+    from oracle import raft_oracle as O
+    cases = sea_states(64, 99)
+    t0 = time.perf_counter()
+    done = 0
+    for c in cases:
+        O.solve_dynamics(T, dict(c), int(T["nIter"]), float(T["XiStart"]), loop=True)
+        done += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "cases/s", "cores": 1, "kind": "port",
+            "sample": f"{done} C2 cases (nw=1000) through oracle/raft_oracle.py loop=True, "
+                      f"{dt:.1f} s on 1 core, OPENBLAS_NUM_THREADS=1"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--ncase", type=int, default=NCASE)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = local
+    torch.cuda.set_device(device)
+
+    from raft.solver import CaseSet, prepare_batch, solve_batch
+    m, f, T = build_model(device)
+    dd = f.device_design()
+    cases = sea_states(args.ncase, 20241016 + rank)          # each rank: its own shard of sea states
+    cs = CaseSet(np.zeros(len(cases), dtype=np.int32), [c["wave_heading"] for c in cases],
+                 ["JONSWAP"] * len(cases), [c["wave_height"] for c in cases], [c["wave_period"] for c in cases],
+                 [0.0] * len(cases))
+    prep = prepare_batch([dd], cs)
+    want = ("psd", "std", "zeta", "rao")
+
+    def step():
+        return solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=want, prepared=prep)
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        res = step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{device}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt_max = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    iters = res["iters"].cpu().numpy()
+    status = res["status"].cpu().numpy()
+    circ = dd.node[N_CIRC()].cpu().numpy() if dd.nn else np.zeros(0)
+    nc, nr = int((circ != 0).sum()), int((circ == 0).sum())
+    flops = float(sum(flops_per_case(int(n), dd.nw, nc, nr, dd.nn) for n in iters))
+    achieved = flops / (kern_ms * 1e-3)
+
+    total_cases = args.ncase * world * args.steps
+    line = {
+        "metric": "sea-state cases/sec (converged RAO+PSD)",
+        "value": total_cases / dt_max,
+        "unit": "cases/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": "C2: VolturnUS-S_example nw=1000, 512 JONSWAP sea states per GPU per step",
+                   "cases_per_step_per_gpu": args.ncase, "nw": dd.nw, "submerged_nodes": dd.nn,
+                   "nodes_circ_rect": [nc, nr], "nIter": int(m.nIter), "parallelism": f"case-sharded x{world}"},
+        "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_FP64, "traffic": None,
+                     "kernel": "rh::k_solve_cases<4>", "kernel_ms": kern_ms,
+                     "flops_per_launch": flops, "note": "FP64 compute bound; algorithmic FLOPs from SURVEY.md §8(d)"},
+        "iterations_mean": float(iters.mean()),
+        "converged_frac": float((status == 1).mean()),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(T)
+    if rank == 0:
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def N_CIRC():
+    from raft import _native as N
+    return N.NF["CIRC"]
+
+
+if __name__ == "__main__":
+    main()

@@ -170,6 +170,7 @@ class Nodes:
         self.Imat = g("node_Imat")
         self.Imat_MCF = np.asarray(T["node_Imat_MCF"])[sub] if "node_Imat_MCF" in T else None
         self.n = len(self.idx)
+        self.r_rel_dry = np.asarray(T["node_r_rel"])[~sub]   # only for the loop flavour's cost shape
 
 
 def sea_state(case, w, dw):
@@ -316,7 +317,8 @@ def solve_dynamics(T, case, nIter, XiStart=0.0, tol=0.01, loop=False):
     dw = float(T["dw"])
     beta, S, zeta = sea_state(case, w, dw)
     nH = len(beta)
-    u, ud, pDyn, F_iner = hydro_excitation(T, nodes, beta, zeta)
+    exc = _hydro_excitation_loop if loop else hydro_excitation
+    u, ud, pDyn, F_iner = exc(T, nodes, beta, zeta)
     M_lin, B_lin, C_lin = linear_matrices(T)
     F_lin = F_iner[0]
     nloop = int(nIter) + 1
@@ -341,11 +343,21 @@ def solve_dynamics(T, case, nIter, XiStart=0.0, tol=0.01, loop=False):
         iiter += 1
     iters = iiter + 1 if converged else nloop
     # system solve (raft/raft_model.py:1021-1065): Zinv = inv(Z) per bin; Xi[ih] = Zinv F_wave
-    Zinv = np.linalg.inv(np.moveaxis(Z, 2, 0))
     XiOut = np.zeros([nH + 1, 6, nw], dtype=complex)
-    for ih in range(nH):
-        F_wave = F_iner[ih] + drag_excitation(nodes, Bmat, u[ih])
-        XiOut[ih] = np.einsum("bij,jb->ib", Zinv, F_wave)
+    if loop:
+        Zinv = np.zeros([6, 6, nw], dtype=complex)
+        for iw in range(nw):
+            Zinv[:, :, iw] = np.linalg.inv(Z[:, :, iw])
+        for ih in range(nH):
+            _, _, _, F_again = _hydro_excitation_loop(T, nodes, beta, zeta)   # the reference recomputes it (:1057)
+            F_wave = F_again[ih] + _drag_excitation_loop(nodes, Bmat, u[ih])
+            for iw in range(nw):
+                XiOut[ih, :, iw] = np.matmul(Zinv[:, :, iw], F_wave[:, iw])
+    else:
+        Zinv = np.linalg.inv(np.moveaxis(Z, 2, 0))
+        for ih in range(nH):
+            F_wave = F_iner[ih] + drag_excitation(nodes, Bmat, u[ih])
+            XiOut[ih] = np.einsum("bij,jb->ib", Zinv, F_wave)
     return dict(Xi=XiOut, iters=iters, converged=converged, B_drag=B_drag, Bmat=Bmat, Z=Z,
                 F_iner=F_iner, F_drag=F_drag, zeta=zeta, S=S, beta=beta)
 
@@ -380,6 +392,10 @@ def _linearize_loop(T, nodes, Xi, u0):
     B = np.zeros([6, 6])
     F = np.zeros([6, nw], dtype=complex)
     Bmat = np.zeros([nodes.n, 3, 3])
+    for r_dry in nodes.r_rel_dry:                # evaluated for dry nodes too
+        dr = np.zeros([3, nw], dtype=complex)
+        for i in range(nw):
+            dr[:, i] = Xi[:3, i] + small_rotate(r_dry, Xi[3:, i])
     for j in range(nodes.n):
         dr = np.zeros([3, nw], dtype=complex)
         for i in range(nw):                      # getKinematics per bin (helpers.py:95-98)
@@ -404,6 +420,51 @@ def _linearize_loop(T, nodes, Xi, u0):
             f = np.matmul(Bmat[j], u0[j, :, i])
             F[:, i] += np.concatenate([f, np.cross(nodes.r_rel[j], f)])
     return B, Bmat, F
+
+
+def _wave_kin_loop(zeta0, beta, w, k, h, r, rho=1025.0, g=9.81):
+    """getWaveKin with the reference's per-bin scalar loop (raft/helpers.py:114-152)."""
+    nw = len(w)
+    u = np.zeros([3, nw], dtype=complex)
+    ud = np.zeros([3, nw], dtype=complex)
+    pDyn = np.zeros(nw, dtype=complex)
+    z = r[2]
+    for i in range(nw):
+        zeta = zeta0[i] * np.exp(-1j * (k[i] * (np.cos(beta) * r[0] + np.sin(beta) * r[1])))
+        if z <= 0:
+            if k[i] * h > 89.4:
+                s_sh = np.exp(k[i] * z)
+                c_sh = np.exp(k[i] * z)
+                c_ch = np.exp(k[i] * z) + np.exp(-k[i] * (z + 2.0 * h))
+            else:
+                s_sh = np.sinh(k[i] * (z + h)) / np.sinh(k[i] * h)
+                c_sh = np.cosh(k[i] * (z + h)) / np.sinh(k[i] * h)
+                c_ch = np.real(np.cosh(k[i] * (z + h))) / np.cosh(k[i] * h)
+            u[0, i] = w[i] * zeta * c_sh * np.cos(beta)
+            u[1, i] = w[i] * zeta * c_sh * np.sin(beta)
+            u[2, i] = 1j * w[i] * zeta * s_sh
+            ud[:, i] = 1j * w[i] * u[:, i]
+            pDyn[i] = rho * g * zeta * c_ch
+    return u, ud, pDyn
+
+
+def _hydro_excitation_loop(T, nodes, beta, zeta):
+    """calcHydroExcitation with the reference's loop shape (raft/raft_fowt.py:1098-1124)."""
+    w, k, h = T["w"], T["k"], float(T["depth"])
+    nH, nw = zeta.shape
+    u = np.zeros([nH, nodes.n, 3, nw], dtype=complex)
+    ud = np.zeros_like(u)
+    pDyn = np.zeros([nH, nodes.n, nw], dtype=complex)
+    F = np.zeros([nH, 6, nw], dtype=complex)
+    for j in range(nodes.n):
+        for ih in range(nH):
+            u[ih, j], ud[ih, j], pDyn[ih, j] = _wave_kin_loop(zeta[ih], beta[ih], w, k, h, nodes.r[j])
+        for ih in range(nH):
+            for i in range(nw):
+                Im = nodes.Imat_MCF[j][:, :, i] if nodes.mcf[j] else nodes.Imat[j]
+                f = np.matmul(Im, ud[ih, j, :, i]) + pDyn[ih, j, i] * nodes.a_i[j] * nodes.q[j]
+                F[ih, :, i] += np.concatenate([f, np.cross(nodes.r_rel[j], f)])
+    return u, ud, pDyn, F
 
 
 def _drag_excitation_loop(nodes, Bmat, u_ih):

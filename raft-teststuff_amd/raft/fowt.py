@@ -90,6 +90,8 @@ class FOWT:
         self.A_aero = np.zeros([6, 6, self.nw, self.nrotors])
         self.B_aero = np.zeros([6, 6, self.nw, self.nrotors])
         self._statics = None
+        for k in ("M_struc", "B_struc", "C_struc", "C_hydro"):
+            setattr(self, k, np.zeros([6, 6]))   # filled by calcStatics
         self._dd = None            # DeviceDesign (built lazily, invalidated on setPosition)
         self.nWaves = 1
 
@@ -118,6 +120,7 @@ class FOWT:
             self.B_struc = np.zeros([6, 6])
         if "C_moor" in self._statics:
             self.C_moor = self._statics["C_moor"].copy()
+        self._dd = None
 
     def calcTurbineConstants(self, case, ptfm_pitch=0):
         """raft/raft_fowt.py:773-845 restricted to what the accelerated path supports: rotor
@@ -268,16 +271,16 @@ class FOWT:
         accelerated path does not build."""
         self.Xi0 = self.r6 - np.array([self.x_ref, self.y_ref, 0, 0, 0, 0])
         stats = getattr(self, "_stats", None)
+        if stats is None:
+            raise RuntimeError("saveTurbineOutputs needs the device motion statistics of solveDynamics")
         for i, dof in enumerate(["surge", "sway", "heave", "roll", "pitch", "yaw"]):
             conv = 57.29577951308232 if i >= 3 else 1.0
-            x = self.Xi[:, i, :] * conv
             avg = self.Xi0[i] * conv
-            std = stats["std"][i] if stats is not None else np.sqrt(0.5 * np.sum(np.abs(x) ** 2))
-            psd = stats["psd"][i] if stats is not None else np.sum(0.5 * np.abs(x) ** 2 / self.dw, axis=0)
+            std = stats["std"][i]
             results[f"{dof}_avg"] = avg
             results[f"{dof}_std"] = std
             results[f"{dof}_max"] = avg + 3 * std
             results[f"{dof}_min"] = avg - 3 * std
-            results[f"{dof}_PSD"] = psd
-            results[f"{dof}_RA"] = x
+            results[f"{dof}_PSD"] = stats["psd"][i]
+            results[f"{dof}_RA"] = self.Xi[:, i, :] * conv
         results["wave_PSD"] = np.sum(0.5 * np.abs(self.zeta) ** 2 / self.dw, axis=0)
