@@ -58,7 +58,21 @@ enum rh_node_field {
   RH_NF_AI,                              /* signed axial area for dynamic pressure (a_i)    */
   RH_NF_MCF,                             /* 1.0 if Imat is frequency dependent (MacCamy-Fuchs) */
   RH_NF_I00, RH_NF_I01, RH_NF_I02, RH_NF_I10, RH_NF_I11, RH_NF_I12, RH_NF_I20, RH_NF_I21, RH_NF_I22,
+  RH_NF_T,                               /* axial coordinate of the node from its member's end A */
   RH_NF_COUNT
+};
+
+/* member-table fields (struct-of-arrays [RH_MF_COUNT][nm]) for members with submerged nodes.
+ * Every RAFT member is straight, so a node at axial coordinate t has r = rA + t q and
+ *   q.(th x r) = th.(rA x q),  p1.(th x r) = th.(rA x p1) + t p2.th,  p2.(th x r) = th.(rA x p2) - t p1.th
+ * (p2 = q x p1, raft/raft_member.py:276-277): the motion-dependent part of every node's
+ * relative velocity is a per-(member, bin) quantity plus t times another one. */
+enum rh_member_field {
+  RH_MF_CQ0 = 0,                         /* cq = [q ; rA x q]   (6) */
+  RH_MF_C10 = 6,                         /* c1 = [p1; rA x p1]  (6) */
+  RH_MF_C20 = 12,                        /* c2 = [p2; rA x p2]  (6) */
+  RH_MF_QQ = 18, RH_MF_PP1, RH_MF_PP2,   /* |q|^2, |p1|^2, |p2|^2 */
+  RH_MF_COUNT
 };
 
 typedef struct { double re, im; } rh_c128;
@@ -78,9 +92,13 @@ typedef struct {
   const double* w;        /* [nw] rad/s                                       */
   const double* k;        /* [nw] wave numbers (raft/helpers.py:295)          */
   const double* node;     /* [RH_NF_COUNT][nn]                                */
+  int nm;                 /* members with submerged nodes                     */
+  const double* memb;     /* [RH_MF_COUNT][nm]                                */
+  const int* mstart;      /* [nm+1] first node of each member (nodes are member-contiguous) */
   const rh_c128* imat_mcf;/* [nn][9][nw] frequency-dependent Imat (MCF nodes), or NULL */
   const rh_c128* uhat;    /* [nhead][nn][3][nw] unit-amplitude wave velocity (rh_wave_tables) */
   const rh_c128* finer;   /* [nhead][6][nw]     unit-amplitude inertial excitation        */
+  const rh_c128* kproj;   /* [nhead][nn][3][nw] projections (q.uhat, p1.uhat, p2.uhat)    */
   const double* M;        /* mass + added mass      M_lin (raft/raft_model.py:911) */
   const double* B;        /* linear damping         B_lin (:912)                   */
   const double* C;        /* [36] stiffness         C_lin (:913)                   */
@@ -130,10 +148,11 @@ int rh_version(void);
  * and helpers.getWaveKin (raft/helpers.py:105-154):
  *   uhat[h][n][:,b]  = u(zeta0 = 1, beta[h]) at node n, bin b
  *   finer[h][:,b]    = sum_n translateForce3to6DOF(Imat_n(b) iw uhat + pDyn a_i q, r_n)
+ *   kproj[h][n][:,b] = (q.uhat, p1.uhat, p2.uhat) of node n (the only form the drag loop needs)
  * so that for a sea state with amplitudes zeta(b): u = zeta*uhat, F_hydro_iner = zeta*finer.
  * beta: device [nhead] (rad).  Outputs are device buffers sized as in rh_design. */
 int rh_wave_tables(rh_ctx* ctx, const rh_design* d, const double* beta,
-                   rh_c128* uhat, rh_c128* finer, rh_stream stream);
+                   rh_c128* uhat, rh_c128* finer, rh_c128* kproj, rh_stream stream);
 
 /* Drag-linearisation fixed point + per-bin Z assemble / pivoted LU solve for a batch of
  * cases, one workgroup per case.  Replaces Model.solveDynamics' per-FOWT iteration

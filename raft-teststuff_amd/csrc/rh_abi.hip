@@ -47,7 +47,8 @@ int check_design(const rh_design& d, bool need_tables) {
   if (d.nn < 0 || d.nn > kMaxNodes) return fail(RH_EINVAL, "nn=%d outside [0, %d]", d.nn, kMaxNodes);
   if (!d.w || !d.k || (d.nn > 0 && !d.node)) return fail(RH_EINVAL, "design: null w/k/node table");
   if (!d.M || !d.B || !d.C) return fail(RH_EINVAL, "design: null M/B/C");
-  if (need_tables && (!d.uhat || !d.finer || d.nhead < 1))
+  if (d.nn > 0 && (d.nm < 1 || !d.memb || !d.mstart)) return fail(RH_EINVAL, "design: member table missing");
+  if (need_tables && (!d.uhat || !d.finer || !d.kproj || d.nhead < 1))
     return fail(RH_EINVAL, "design: wave tables missing (call rh_wave_tables first)");
   if (!(d.dw > 0)) return fail(RH_EINVAL, "design: dw must be > 0");
   return RH_OK;
@@ -114,13 +115,13 @@ int rh_ctx_destroy(rh_ctx* ctx) {
 }
 
 int rh_wave_tables(rh_ctx* ctx, const rh_design* d, const double* beta, rh_c128* uhat, rh_c128* finer,
-                   rh_stream stream) {
-  if (!ctx || !d || !beta || !uhat || !finer) return fail(RH_EINVAL, "rh_wave_tables: null argument");
+                   rh_c128* kproj, rh_stream stream) {
+  if (!ctx || !d || !beta || !uhat || !finer || !kproj) return fail(RH_EINVAL, "rh_wave_tables: null argument");
   if (int r = check_design(*d, false)) return r;
   if (d->nhead < 1) return fail(RH_EINVAL, "rh_wave_tables: nhead must be >= 1");
   RH_HIP(hipSetDevice(ctx->device));
   dim3 grid((d->nw + 127) / 128, d->nhead);
-  hipLaunchKernelGGL(rh::k_wave_tables, grid, dim3(128), 0, (hipStream_t)stream, *d, beta, uhat, finer);
+  hipLaunchKernelGGL(rh::k_wave_tables, grid, dim3(128), 0, (hipStream_t)stream, *d, beta, uhat, finer, kproj);
   RH_HIP(hipGetLastError());
   return RH_OK;
 }
@@ -154,7 +155,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   a.designs = ctx->d_designs;
   a.c = *cases;
   a.o = *out;
-  const size_t smem = sizeof(double) * (size_t)((kThreads / 64) * nnmax * 3 + nnmax * 9 + 36 + (kThreads / 64) * 6 + 108);
+  const size_t smem = sizeof(double) * (size_t)((kThreads / 64) * nnmax * 3 + nnmax * 9 + 36 + (kThreads / 64) * 6 + 108 + nnmax * 5);
   dim3 grid(cases->ncase), block(kThreads);
   switch (nb_for(nw)) {
     case 1: hipLaunchKernelGGL(rh::k_solve_cases<1>, grid, block, smem, s, a); break;

@@ -79,7 +79,8 @@ __global__ __launch_bounds__(256) void k_sea_state(int nw, const double* __restr
 // k_wave_tables: thread per (heading, bin); loop over nodes.
 // ----------------------------------------------------------------------------------------
 __global__ __launch_bounds__(128) void k_wave_tables(rh_design d, const double* __restrict__ beta,
-                                                      rh_c128* __restrict__ uhat, rh_c128* __restrict__ finer) {
+                                                      rh_c128* __restrict__ uhat, rh_c128* __restrict__ finer,
+                                                      rh_c128* __restrict__ kproj) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   const int h = blockIdx.y;
   const int nw = d.nw, nn = d.nn;
@@ -115,6 +116,15 @@ __global__ __launch_bounds__(128) void k_wave_tables(rh_design d, const double* 
     st(U, u0);
     st(U + nw, u1);
     st(U + 2 * nw, u2);
+    {  // projections on the member axes: the drag loop's only view of the wave field
+      rh_c128* K = kproj + ((size_t)(h * nn + n) * 3) * nw + b;
+      const int fo[3] = {RH_NF_QX, RH_NF_P1X, RH_NF_P2X};
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const double e0 = nf(node, nn, fo[a], n), e1 = nf(node, nn, fo[a] + 1, n), e2 = nf(node, nn, fo[a] + 2, n);
+        st(K + a * nw, add(add(scl(u0, e0), scl(u1, e1)), scl(u2, e2)));
+      }
+    }
     // inertial excitation: Imat ud + pDyn a_i q, ud = i w u  (raft/raft_fowt.py:1113-1124)
     const cd ud[3] = {iw(w, u0), iw(w, u1), iw(w, u2)};
     const cd pd = scl(scl(e, d.pdyn_rho_g), c_ch);
@@ -159,8 +169,13 @@ __global__ __launch_bounds__(128) void k_wave_tables(rh_design d, const double* 
 
 // Node drag matrix from the three bin-summed squared relative-velocity magnitudes
 // (raft/raft_fowt.py:1213-1248).  sums = {sum|vrel_q|^2, sum|vrel_p or p1|^2, sum|vrel_p2|^2}.
+__device__ __forceinline__ double nrm2(const double* node, int nn, int f, int n) {
+  const double a = nf(node, nn, f, n), b = nf(node, nn, f + 1, n), c = nf(node, nn, f + 2, n);
+  return a * a + b * b + c * c;
+}
+
 __device__ __forceinline__ void node_bmat(const double* node, int nn, int n, double rho, const double* sums,
-                                          double* bm) {
+                                          double* bm, double* B4 = nullptr) {
   const bool circ = nf(node, nn, RH_NF_CIRC, n) != 0.0;
   const double vq = sqrt(0.5 * sums[0]);
   const double vp1 = sqrt(0.5 * sums[1]);
@@ -169,6 +184,12 @@ __device__ __forceinline__ void node_bmat(const double* node, int nn, int n, dou
   const double Bp1 = kSqrt8Pi * vp1 * 0.5 * rho * nf(node, nn, RH_NF_AP1, n) * nf(node, nn, RH_NF_CDP1, n);
   const double Bp2 = kSqrt8Pi * vp2 * 0.5 * rho * nf(node, nn, RH_NF_AP2, n) * nf(node, nn, RH_NF_CDP2, n);
   const double Be = kSqrt8Pi * vq * 0.5 * rho * nf(node, nn, RH_NF_AEND, n) * nf(node, nn, RH_NF_CDEND, n);
+  if (B4) {
+    B4[0] = Bq;
+    B4[1] = Bp1;
+    B4[2] = Bp2;
+    B4[3] = Be;
+  }
   const double q[3] = {nf(node, nn, RH_NF_QX, n), nf(node, nn, RH_NF_QY, n), nf(node, nn, RH_NF_QZ, n)};
   const double p1[3] = {nf(node, nn, RH_NF_P1X, n), nf(node, nn, RH_NF_P1Y, n), nf(node, nn, RH_NF_P1Z, n)};
   const double p2[3] = {nf(node, nn, RH_NF_P2X, n), nf(node, nn, RH_NF_P2Y, n), nf(node, nn, RH_NF_P2Z, n)};
@@ -218,6 +239,42 @@ __device__ __forceinline__ void drag_exc_bin(const double* node, int nn, const d
   }
 }
 
+// Drag excitation of one bin before the zeta factor, member-factored:
+//   f_n = Bmat_n uhat_n = aq q Kq + a1 p1 K1 + a2 p2 K2,  r_n x f_n = rA x f_n + t q x f_n
+// with q x p1 = p2, q x p2 = -p1 (raft/raft_fowt.py:1255-1259, 1283-1289).  al: [nn][5] LDS
+// {aq, a1, a2, t a1, t a2}.
+__device__ __forceinline__ void drag_exc_members(const rh_design& d, const double* al, const rh_c128* __restrict__ Kp,
+                                                 int nw, int b, cd (&F)[6]) {
+#pragma unroll
+  for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
+  const int nm = d.nm;
+  for (int m = 0; m < nm; ++m) {
+    const int n0 = d.mstart[m], n1 = d.mstart[m + 1];
+    cd SQ = mk(0, 0), S1 = mk(0, 0), S2 = mk(0, 0), T1 = mk(0, 0), T2 = mk(0, 0);
+    for (int n = n0; n < n1; ++n) {
+      const rh_c128* K = Kp + (size_t)n * 3 * nw + b;
+      const cd kq = ld(K), k1 = ld(K + nw), k2 = ld(K + 2 * nw);
+      const double* A = al + 5 * n;
+      SQ = add(SQ, scl(kq, A[0]));
+      S1 = add(S1, scl(k1, A[1]));
+      S2 = add(S2, scl(k2, A[2]));
+      T1 = add(T1, scl(k1, A[3]));
+      T2 = add(T2, scl(k2, A[4]));
+    }
+    const double* M = d.memb;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double cq = M[(RH_MF_CQ0 + i) * nm + m], c1 = M[(RH_MF_C10 + i) * nm + m], c2 = M[(RH_MF_C20 + i) * nm + m];
+      F[i] = add(F[i], add(add(scl(SQ, cq), scl(S1, c1)), scl(S2, c2)));
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double p1 = M[(RH_MF_C10 + i) * nm + m], p2 = M[(RH_MF_C20 + i) * nm + m];
+      F[3 + i] = add(F[3 + i], sub(scl(T1, p2), scl(T2, p1)));
+    }
+  }
+}
+
 // Z(w) = -w^2 M + i w (B + B_drag) + C (raft/raft_model.py:944).
 // mbc: LDS image {M[36], B_lin[36], C[36]} of a frequency-independent design (wave-uniform
 // broadcast reads); per-bin M/B (BEM added mass / radiation damping) come from global memory.
@@ -264,7 +321,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
   const int nw = d.nw, nn = d.nn;
   const double* node = d.node;
   const int head = a.c.head[ic];
-  const rh_c128* Uh = d.uhat + (size_t)head * nn * 3 * nw;
+  const int nm = d.nm;
+  const rh_c128* Kp = d.kproj + (size_t)head * nn * 3 * nw;
   const rh_c128* Fe = d.finer + (size_t)head * 6 * nw;
 
   double* red = smem;                     // [kWaves][nn][3]
@@ -272,6 +330,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
   double* bd = bm + nn * 9;               // [36]
   double* sred = bd + 36;                 // [kWaves][6]
   double* mbc = sred + kWaves * 6;        // [108] M, B_lin, C
+  double* al = mbc + 108;                 // [nn][5] drag coefficients per node
   load_mbc(d, mbc, tid);
 
   const int spec = a.c.spectrum[ic];
@@ -298,68 +357,94 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
   int status = RH_CASE_NOT_CONVERGED, iters = nloop;
   for (int it = 0; it < nloop; ++it) {
     // ---------------- A: per-node sums of squared relative-velocity components ----------
-    cd xl[NB][6];
+    // Member-factored (see rh_member_field): per (member, bin) the motion terms
+    //   Bq = iw cq.Xi, B1 = iw c1.Xi, B2 = iw c2.Xi, E1 = iw p2.th, E2 = -iw p1.th
+    // then per node  s_q = z Kq - Bq,  s_1 = z K1 - (B1 + t E1),  s_2 = z K2 - (B2 + t E2)
+    // are the relative-velocity projections of raft/raft_fowt.py:1205-1211.
+    for (int m = 0; m < nm; ++m) {
+      const int n0 = d.mstart[m], n1 = d.mstart[m + 1];
+      double cq[6], c1[6], c2[6];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int b = tid + kThreads * j;
-#pragma unroll
-      for (int c = 0; c < 6; ++c) xl[j][c] = (b < nw) ? ld(XL + c * nw + b) : mk(0, 0);
-    }
-    for (int n = 0; n < nn; ++n) {
-      const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
-      const double q0 = nf(node, nn, RH_NF_QX, n), q1 = nf(node, nn, RH_NF_QY, n), q2 = nf(node, nn, RH_NF_QZ, n);
-      const bool circ = nf(node, nn, RH_NF_CIRC, n) != 0.0;
-      double s0 = 0, s1 = 0, s2 = 0;
+      for (int i = 0; i < 6; ++i) {
+        cq[i] = d.memb[(RH_MF_CQ0 + i) * nm + m];
+        c1[i] = d.memb[(RH_MF_C10 + i) * nm + m];
+        c2[i] = d.memb[(RH_MF_C20 + i) * nm + m];
+      }
+      cd Bq[NB], B1[NB], B2[NB], E1[NB], E2[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int b = tid + kThreads * j;
-        if (b < nw) {
-          const double w = d.w[b];
-          const rh_c128* U = Uh + (size_t)n * 3 * nw + b;
-          const cd u0 = scl(ld(U), zt[j]), u1 = scl(ld(U + nw), zt[j]), u2 = scl(ld(U + 2 * nw), zt[j]);
-          const cd* X = xl[j];
-          // getKinematics: dr = Xi[:3] + th x r ; v = i w dr  (raft/helpers.py:95-97)
-          const cd dr0 = add(X[0], add(scl(X[5], -ry), scl(X[4], rz)));
-          const cd dr1 = add(X[1], sub(scl(X[5], rx), scl(X[3], rz)));
-          const cd dr2 = add(X[2], add(scl(X[4], -rx), scl(X[3], ry)));
-          const cd v0 = sub(u0, iw(w, dr0)), v1 = sub(u1, iw(w, dr1)), v2 = sub(u2, iw(w, dr2));
-          const cd sq = add(add(scl(v0, q0), scl(v1, q1)), scl(v2, q2));
-          const cd vq0 = scl(sq, q0), vq1 = scl(sq, q1), vq2 = scl(sq, q2);
-          s0 += abs2(vq0) + abs2(vq1) + abs2(vq2);
-          if (circ) {
-            s1 += abs2(sub(v0, vq0)) + abs2(sub(v1, vq1)) + abs2(sub(v2, vq2));
-          } else {
-            const double a0 = nf(node, nn, RH_NF_P1X, n), a1 = nf(node, nn, RH_NF_P1Y, n), a2 = nf(node, nn, RH_NF_P1Z, n);
-            const double b0 = nf(node, nn, RH_NF_P2X, n), b1 = nf(node, nn, RH_NF_P2Y, n), b2 = nf(node, nn, RH_NF_P2Z, n);
-            const cd s_1 = add(add(scl(v0, a0), scl(v1, a1)), scl(v2, a2));
-            const cd s_2 = add(add(scl(v0, b0), scl(v1, b1)), scl(v2, b2));
-            s1 += abs2(scl(s_1, a0)) + abs2(scl(s_1, a1)) + abs2(scl(s_1, a2));
-            s2 += abs2(scl(s_2, b0)) + abs2(scl(s_2, b1)) + abs2(scl(s_2, b2));
+        cd X[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) X[c] = (b < nw) ? ld(XL + c * nw + b) : mk(0, 0);
+        const double w = (b < nw) ? d.w[b] : 0.0;
+        cd Aq = mk(0, 0), A1 = mk(0, 0), A2 = mk(0, 0);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          Aq = add(Aq, scl(X[c], cq[c]));
+          A1 = add(A1, scl(X[c], c1[c]));
+          A2 = add(A2, scl(X[c], c2[c]));
+        }
+        const cd D1 = add(add(scl(X[3], c2[0]), scl(X[4], c2[1])), scl(X[5], c2[2]));   // p2 . th
+        const cd D2 = add(add(scl(X[3], c1[0]), scl(X[4], c1[1])), scl(X[5], c1[2]));   // p1 . th
+        Bq[j] = iw(w, Aq);
+        B1[j] = iw(w, A1);
+        B2[j] = iw(w, A2);
+        E1[j] = iw(w, D1);
+        E2[j] = iw(-w, D2);
+      }
+      for (int n = n0; n < n1; ++n) {
+        const double t = nf(node, nn, RH_NF_T, n);
+        const rh_c128* K = Kp + (size_t)n * 3 * nw;
+        double s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const int b = tid + kThreads * j;
+          if (b < nw) {
+            const double z = zt[j];
+            const cd sq = sub(scl(ld(K + b), z), Bq[j]);
+            const cd sp1 = sub(scl(ld(K + nw + b), z), add(B1[j], scl(E1[j], t)));
+            const cd sp2 = sub(scl(ld(K + 2 * nw + b), z), add(B2[j], scl(E2[j], t)));
+            s0 += abs2(sq);
+            s1 += abs2(sp1);
+            s2 += abs2(sp2);
           }
         }
-      }
-      s0 = wave_sum(s0);
-      s1 = wave_sum(s1);
-      s2 = wave_sum(s2);
-      if (lane == 0) {
-        double* R = red + (wv * nn + n) * 3;
-        R[0] = s0;
-        R[1] = s1;
-        R[2] = s2;
+        s0 = wave_sum(s0);
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        if (lane == 0) {
+          double* R = red + (wv * nn + n) * 3;
+          R[0] = s0;
+          R[1] = s1;
+          R[2] = s2;
+        }
       }
     }
     __syncthreads();
     // ---------------- B: node drag matrices and B_drag ----------------------------------
     for (int n = tid; n < nn; n += kThreads) {
-      double sums[3];
+      double r3[3];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         double s = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) s += red[(w * nn + n) * 3 + c];
-        sums[c] = s;
+        r3[c] = s;
       }
-      node_bmat(node, nn, n, d.rho, sums, bm + 9 * n);
+      // sum|vrel_q|^2 = sum|s_q|^2 |q|^2 ; circular: |vrel_p|^2 = |s_1|^2|p1|^2 + |s_2|^2|p2|^2
+      const double qq = nrm2(node, nn, RH_NF_QX, n), pp1 = nrm2(node, nn, RH_NF_P1X, n), pp2 = nrm2(node, nn, RH_NF_P2X, n);
+      const bool circ = nf(node, nn, RH_NF_CIRC, n) != 0.0;
+      const double sums[3] = {r3[0] * qq, circ ? r3[1] * pp1 + r3[2] * pp2 : r3[1] * pp1, r3[2] * pp2};
+      double B4[4];
+      node_bmat(node, nn, n, d.rho, sums, bm + 9 * n, B4);
+      const double t = nf(node, nn, RH_NF_T, n);
+      double* A = al + 5 * n;
+      A[0] = B4[0] + B4[3];     // axial: side + end   (qMat terms of Bmat, raft/raft_fowt.py:1228-1248)
+      A[1] = B4[1];
+      A[2] = B4[2];
+      A[3] = t * B4[1];
+      A[4] = t * B4[2];
     }
     __syncthreads();
     if (tid < 36) {
@@ -378,7 +463,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
       if (b >= nw) continue;
       const double w = d.w[b];
       cd F[6];
-      drag_exc_bin(node, nn, bm, Uh, nw, b, F);
+      drag_exc_members(d, al, Kp, nw, b, F);
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
         cd f = add(scl(ld(Fe + c * nw + b), zt[j]), scl(F[c], zt[j]));   // F_lin + F_drag

@@ -21,9 +21,10 @@ SPECTRUM_CODES = {"JONSWAP": 0, "unit": 1, "constant": 2, "none": 3, "still": 3}
 # node-table field order (enum rh_node_field)
 NODE_FIELDS = ["RX", "RY", "RZ", "XX", "XY", "XZ", "QX", "QY", "QZ", "P1X", "P1Y", "P1Z", "P2X", "P2Y", "P2Z",
                "AQ", "AP1", "AP2", "AEND", "CDQ", "CDP1", "CDP2", "CDEND", "CIRC", "AI", "MCF",
-               "I00", "I01", "I02", "I10", "I11", "I12", "I20", "I21", "I22"]
+               "I00", "I01", "I02", "I10", "I11", "I12", "I20", "I21", "I22", "T"]
 NF = {name: i for i, name in enumerate(NODE_FIELDS)}
 NF_COUNT = len(NODE_FIELDS)
+MF_COUNT = 21   # enum rh_member_field: cq[6], c1[6], c2[6], |q|^2, |p1|^2, |p2|^2
 
 _p = ctypes.c_void_p
 
@@ -32,7 +33,8 @@ class RhDesign(ctypes.Structure):
     _fields_ = [("nw", ctypes.c_int), ("nn", ctypes.c_int), ("nhead", ctypes.c_int), ("mb_per_bin", ctypes.c_int),
                 ("dw", ctypes.c_double), ("depth", ctypes.c_double), ("rho", ctypes.c_double), ("g", ctypes.c_double),
                 ("pdyn_rho_g", ctypes.c_double),
-                ("w", _p), ("k", _p), ("node", _p), ("imat_mcf", _p), ("uhat", _p), ("finer", _p),
+                ("w", _p), ("k", _p), ("node", _p), ("nm", ctypes.c_int), ("memb", _p), ("mstart", _p),
+                ("imat_mcf", _p), ("uhat", _p), ("finer", _p), ("kproj", _p),
                 ("M", _p), ("B", _p), ("C", _p)]
 
 
@@ -68,7 +70,7 @@ def lib():
             for name, args in {
                 "rh_ctx_create": [ctypes.c_int, ctypes.POINTER(_p)],
                 "rh_ctx_destroy": [_p],
-                "rh_wave_tables": [_p, ctypes.POINTER(RhDesign), _p, _p, _p, _p],
+                "rh_wave_tables": [_p, ctypes.POINTER(RhDesign), _p, _p, _p, _p, _p],
                 "rh_solve_cases": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.POINTER(RhCases),
                                    ctypes.POINTER(RhSolveOut), _p],
                 "rh_heading_response": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.c_int, _p, _p, _p, _p,

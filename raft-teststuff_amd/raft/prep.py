@@ -34,8 +34,16 @@ def node_table(fowt):
     cols = []
     mcf_blocks = []
     any_mcf = False
+    mcols, mstart = [], [0]
     for mem in fowt.memberList:
         circ = mem.shape == "circular"
+        nsub = int(np.sum(mem.r[:, 2] < 0))
+        if nsub:
+            rA = mem.rA - fowt.r6[:3]
+            q, p1, p2 = mem.q, mem.p1, mem.p2
+            mcols.append([*q, *np.cross(rA, q), *p1, *np.cross(rA, p1), *p2, *np.cross(rA, p2),
+                          q @ q, p1 @ p1, p2 @ p2])
+            mstart.append(mstart[-1] + nsub)
         for il in range(mem.ns):
             if not (mem.r[il, 2] < 0):
                 continue
@@ -57,17 +65,19 @@ def node_table(fowt):
             col = [r[0], r[1], r[2], rr[0], rr[1], rr[2], *mem.q, *mem.p1, *mem.p2,
                    a_q, a_p1, a_p2, a_end,
                    mem.coef("Cd_q", il), mem.coef("Cd_p1", il), mem.coef("Cd_p2", il), mem.coef("Cd_End", il),
-                   1.0 if circ else 0.0, mem.a_i[il], 1.0 if use_mcf else 0.0, *mem.Imat[il].ravel()]
+                   1.0 if circ else 0.0, mem.a_i[il], 1.0 if use_mcf else 0.0, *mem.Imat[il].ravel(),
+                   mem.ls[il]]
             cols.append(col)
             mcf_blocks.append(mem.Imat_MCF[il].reshape(9, -1) if use_mcf else None)
     table = np.array(cols, dtype=float).T.copy() if cols else np.zeros([N.NF_COUNT, 0])
+    members = np.array(mcols, dtype=float).T.copy() if mcols else np.zeros([N.MF_COUNT, 0])
     imat = None
     if any_mcf:
         imat = np.zeros([len(cols), 9, fowt.nw], dtype=complex)
         for i, blk in enumerate(mcf_blocks):
             if blk is not None:
                 imat[i] = blk
-    return table, imat
+    return table, imat, members, np.array(mstart, dtype=np.int32)
 
 
 def linear_matrices(fowt):
@@ -97,13 +107,16 @@ class DeviceDesign:
         self.device = torch.device("cuda", device)
         self.dev_index = device
         self.nw = fowt.nw
-        table, imat = node_table(fowt)
+        table, imat, members, mstart = node_table(fowt)
         self.nn = table.shape[1]
+        self.nm = members.shape[1]
         f64 = dict(dtype=torch.float64, device=self.device)
         self.w = torch.tensor(fowt.w, **f64)
         self.k = torch.tensor(fowt.k, **f64)
         self.node = torch.tensor(table if self.nn else np.zeros([N.NF_COUNT, 1]), **f64).contiguous()
         self.imat = torch.tensor(imat, dtype=torch.complex128, device=self.device) if imat is not None else None
+        self.memb = torch.tensor(members if self.nm else np.zeros([N.MF_COUNT, 1]), **f64).contiguous()
+        self.mstart = torch.tensor(mstart, dtype=torch.int32, device=self.device)
         M, B, C, per_bin = linear_matrices(fowt)
         self.per_bin = per_bin
         self.M = torch.tensor(M, **f64).contiguous()
@@ -113,6 +126,7 @@ class DeviceDesign:
         self.headings = None           # tuple of tabulated headings (rad)
         self.uhat = None
         self.finer = None
+        self.kproj = None
 
     def struct(self):
         d = N.RhDesign()
@@ -122,8 +136,9 @@ class DeviceDesign:
         d.dw, d.depth, d.rho, d.g = self.dw, self.depth, self.rho, self.g
         d.pdyn_rho_g = 1025.0 * 9.81   # getWaveKin defaults (raft/helpers.py:105, raft/raft_fowt.py:1109)
         d.w, d.k, d.node = N.ptr(self.w), N.ptr(self.k), N.ptr(self.node)
+        d.nm, d.memb, d.mstart = self.nm, N.ptr(self.memb), N.ptr(self.mstart)
         d.imat_mcf = N.ptr(self.imat)
-        d.uhat, d.finer = N.ptr(self.uhat), N.ptr(self.finer)
+        d.uhat, d.finer, d.kproj = N.ptr(self.uhat), N.ptr(self.finer), N.ptr(self.kproj)
         d.M, d.B, d.C = N.ptr(self.M), N.ptr(self.B), N.ptr(self.C)
         return d
 
@@ -139,11 +154,13 @@ class DeviceDesign:
             nh = len(allh)
             self.uhat = torch.empty([nh, max(self.nn, 1), 3, self.nw], dtype=torch.complex128, device=self.device)
             self.finer = torch.empty([nh, 6, self.nw], dtype=torch.complex128, device=self.device)
+            self.kproj = torch.empty([nh, max(self.nn, 1), 3, self.nw], dtype=torch.complex128, device=self.device)
             self.headings = tuple(allh)
             beta_t = torch.tensor(allh, dtype=torch.float64, device=self.device)
             d = self.struct()
             N.check(N.lib().rh_wave_tables(N.context(self.dev_index), ctypes.byref(d), N.ptr(beta_t),
-                                           N.ptr(self.uhat), N.ptr(self.finer), N.stream_handle(torch, self.device)),
+                                           N.ptr(self.uhat), N.ptr(self.finer), N.ptr(self.kproj),
+                                           N.stream_handle(torch, self.device)),
                     "rh_wave_tables")
             self._beta_keep = beta_t
         return [self.headings.index(b) for b in betas]

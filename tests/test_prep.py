@@ -37,7 +37,7 @@ def test_node_tables_match_reference(tag, design, settings):
     T = load_golden(tag)
     m, f = _model(design, settings, T)
     assert sum(mm.ns for mm in f.memberList) == len(T["node_sub"])
-    tab, imat = node_table(f)
+    tab, imat, _, _ = node_table(f)
     sub = T["node_sub"].astype(bool)
     assert tab.shape == (N.NF_COUNT, sub.sum())
     ref = {"RX": T["node_r"][sub, 0], "RY": T["node_r"][sub, 1], "RZ": T["node_r"][sub, 2],
@@ -65,7 +65,7 @@ def test_drag_areas_follow_reference_formulas():
     from raft.prep import node_table
     T = load_golden("c2_nw200")
     m, f = _model("VolturnUS-S_example", {}, T)
-    tab, _ = node_table(f)
+    tab, _, _, _ = node_table(f)
     sub = T["node_sub"].astype(bool)
     ds, dls, drs, circ = T["node_ds"][sub], T["node_dls"][sub], T["node_drs"][sub], T["node_circ"][sub].astype(bool)
     aq = np.where(circ, np.pi * ds[:, 0] * dls, 2 * (ds[:, 0] + ds[:, 0]) * dls)
