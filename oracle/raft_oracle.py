@@ -153,6 +153,38 @@ def translate_force_3to6(F, r):
 # ----------------------------------------------------------------------------------
 # per-design node view
 # ----------------------------------------------------------------------------------
+def imat_mcf(T):
+    """MacCamy-Fuchs inertia matrices Imat_MCF[node,3,3,nw] of the MCF nodes
+    (raft/raft_member.py:972-1088), rebuilt from the node tables with scipy's hankel1."""
+    from scipy.special import hankel1
+    rho = float(T["rho"])
+    k = T["k"]
+    n = len(T["node_sub"])
+    out = np.zeros([n, 3, 3, len(k)], dtype=complex)
+    for i in range(n):
+        if not (T["node_mcf"][i] and T["node_sub"][i]):
+            continue
+        ds, drs, dls, z = T["node_ds"][i], T["node_drs"][i], T["node_dls"][i], T["node_r"][i, 2]
+        circ = bool(T["node_circ"][i])
+        v = 0.25 * np.pi * ds[0] ** 2 * dls if circ else ds[0] * ds[1] * dls
+        if z + 0.5 * dls > 0:
+            v = v * (0.5 * dls - z) / dls
+        ve = np.pi / 12.0 * abs((ds[0] + drs[0]) ** 3 - (ds[0] - drs[0]) ** 3)
+        q, p1, p2 = T["node_q"][i], T["node_p1"][i], T["node_p2"][i]
+        Iend = rho * ve * T["node_Ca_End"][i] * np.outer(q, q)
+        c10, c20 = 1. + T["node_Ca_p1"][i], 1. + T["node_Ca_p2"][i]
+        R = ds[0] / 2
+        Tr = np.pi / 5 / R
+        for ik, kk in enumerate(k):
+            Hp1 = 0.5 * (hankel1(0, kk * R) - hankel1(2, kk * R))
+            Cm = 4j / (np.pi * (kk * R) ** 2 * Hp1)
+            ramp = 0.5 * (1 - np.cos(np.pi * (kk - 0) / Tr)) if kk < Tr else 1
+            ramp = 0 if kk <= 0 else ramp
+            c1, c2 = Cm * ramp + c10 * (1 - ramp), Cm * ramp + c20 * (1 - ramp)
+            out[i, :, :, ik] = rho * v * (c1 * np.outer(p1, p1) + c2 * np.outer(p2, p2)) + Iend
+    return out
+
+
 class Nodes:
     """Submerged-node view of the design tables (order = reference member/node order)."""
 
@@ -168,7 +200,12 @@ class Nodes:
         self.a_i = g("node_a_i")
         self.mcf = g("node_mcf").astype(bool)
         self.Imat = g("node_Imat")
-        self.Imat_MCF = np.asarray(T["node_Imat_MCF"])[sub] if "node_Imat_MCF" in T else None
+        if "node_Imat_MCF" in T:
+            self.Imat_MCF = np.asarray(T["node_Imat_MCF"])[sub]
+        elif np.any(np.asarray(T["node_mcf"])[sub]):
+            self.Imat_MCF = imat_mcf(T)[sub]
+        else:
+            self.Imat_MCF = None
         self.n = len(self.idx)
         self.r_rel_dry = np.asarray(T["node_r_rel"])[~sub]   # only for the loop flavour's cost shape
 
@@ -307,10 +344,14 @@ def linear_matrices(T):
     return M, B, C
 
 
-def solve_dynamics(T, case, nIter, XiStart=0.0, tol=0.01, loop=False):
-    """Single-FOWT Model.solveDynamics (raft/raft_model.py:852-1146), potSecOrder = 0.
+def solve_dynamics(T, case, nIter, XiStart=0.0, tol=0.01, loop=False, second_order=None):
+    """Single-FOWT Model.solveDynamics (raft/raft_model.py:852-1146).
 
-    Returns dict(Xi=[nH+1,6,nw], iters, converged, B_drag, Bmat, Z, F_iner, zeta, S)."""
+    second_order: None (potSecOrder = 0) or dict(w1_2nd, k1_2nd) for potSecOrder = 1
+    (raft/raft_model.py:966-989): at the first convergence the RAO feeds the slender-body
+    QTF, its difference-frequency force is added to F_lin (Q5) and the loop continues with
+    iiter reset to 0 then incremented and XiLast NOT relaxed (Q6).
+    Returns dict(Xi=[nH+1,6,nw], iters, converged, B_drag, Bmat, Z, F_iner, zeta, S, ...)."""
     nodes = Nodes(T)
     w = T["w"]
     nw = len(w)
@@ -327,6 +368,10 @@ def solve_dynamics(T, case, nIter, XiStart=0.0, tol=0.01, loop=False):
     solve = _solve_bins_loop if loop else _solve_bins
     iiter = 0
     converged = False
+    F2 = np.zeros([6, nw], dtype=complex)
+    qtf_done = second_order is None
+    pair = []
+    extra = {}
     while iiter < nloop:
         B_drag, Bmat, F_drag = lin(T, nodes, XiLast, u[0])
         F_drag = (_drag_excitation_loop if loop else drag_excitation)(nodes, Bmat, u[0])
@@ -337,9 +382,21 @@ def solve_dynamics(T, case, nIter, XiStart=0.0, tol=0.01, loop=False):
             raise Exception("Nan detected in response vector Xi.")
         tolCheck = np.abs(Xi - XiLast) / ((np.abs(Xi) + tol))
         if (tolCheck < tol).all():
-            converged = True
-            break
-        XiLast = 0.2 * XiLast + 0.8 * Xi
+            pair.append(iiter + 1)
+            if qtf_done:
+                converged = True
+                break
+            from .qtf_oracle import hydro_force_2nd, qtf_slender
+            Xi0 = get_rao(Xi, zeta[0])
+            qtf = qtf_slender(T, Xi0, second_order["w1_2nd"], second_order["k1_2nd"], beta[0])
+            fm, f = hydro_force_2nd(qtf, second_order["w1_2nd"], w, S[0], dw)
+            F2 = f.astype(complex)
+            F_lin = F_lin + F2                                   # Q5: F_lin[0] += Fhydro_2nd
+            extra.update(Xi0=Xi0, qtf=qtf, Fhydro_2nd=F2, Fhydro_2nd_mean=fm)
+            qtf_done = True
+            iiter = 0
+        else:
+            XiLast = 0.2 * XiLast + 0.8 * Xi
         iiter += 1
     iters = iiter + 1 if converged else nloop
     # system solve (raft/raft_model.py:1021-1065): Zinv = inv(Z) per bin; Xi[ih] = Zinv F_wave
@@ -356,10 +413,10 @@ def solve_dynamics(T, case, nIter, XiStart=0.0, tol=0.01, loop=False):
     else:
         Zinv = np.linalg.inv(np.moveaxis(Z, 2, 0))
         for ih in range(nH):
-            F_wave = F_iner[ih] + drag_excitation(nodes, Bmat, u[ih])
+            F_wave = F_iner[ih] + drag_excitation(nodes, Bmat, u[ih]) + (F2 if ih == 0 else 0)
             XiOut[ih] = np.einsum("bij,jb->ib", Zinv, F_wave)
     return dict(Xi=XiOut, iters=iters, converged=converged, B_drag=B_drag, Bmat=Bmat, Z=Z,
-                F_iner=F_iner, F_drag=F_drag, zeta=zeta, S=S, beta=beta)
+                F_iner=F_iner, F_drag=F_drag, zeta=zeta, S=S, beta=beta, iters_pair=pair, **extra)
 
 
 def _solve_bins(w, M, B, C, F):

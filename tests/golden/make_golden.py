@@ -114,6 +114,10 @@ def design_tables(fowt):
     out["A_BEM"] = fowt.A_BEM.copy()
     out["B_BEM"] = fowt.B_BEM.copy()
     out["member_names"] = np.array([m.name for m in fowt.memberList])
+    out["member_rA"] = np.array([m.rA for m in fowt.memberList])
+    out["member_rB"] = np.array([m.rB for m in fowt.memberList])
+    out["member_circ"] = np.array([int(m.shape == "circular") for m in fowt.memberList])
+    out["member_mcf"] = np.array([int(bool(m.MCF)) for m in fowt.memberList])
     return out
 
 
@@ -268,7 +272,92 @@ def export_designs():
     print("wrote designs/*.json", file=sys.stderr)
 
 
+def bilinear_interp2d(x, y, z, bounds_error=False, fill_value=0):
+    """Restatement of the removed scipy.interpolate.interp2d(kind='linear') as the reference
+    uses it (raft/raft_fowt.py:1792-1793): bilinear on the regular grid,
+    z[y_i, x_j] orientation, fill_value strictly outside [x0, x1] x [y0, y1]."""
+    from scipy.interpolate import RegularGridInterpolator
+    x = np.asarray(x, dtype=float)
+    y = np.asarray(y, dtype=float)
+    rgi = RegularGridInterpolator((y, x), np.asarray(z, dtype=float), method="linear", bounds_error=False,
+                                  fill_value=fill_value)
+
+    def f(xn, yn):
+        X, Y = np.meshgrid(np.asarray(xn, dtype=float), np.asarray(yn, dtype=float))
+        return rgi(np.stack([Y.ravel(), X.ravel()], axis=-1)).reshape(X.shape)
+    return f
+
+
+def golden_qtf():
+    """C3: OC4semi-RAFT_QTF with potSecOrder=1 through the reference's full path
+    (first convergence -> RAO -> calcQTF_slenderBody -> calcHydroForce_2ndOrd -> second
+    pass, raft/raft_model.py:966-989), plus QTF entries of the n2=400 grid (df 0.000825 Hz)
+    on a seeded 24-frequency subset (every pair of a frequency subset is an entry of the
+    full 400x400 matrix: the per-frequency tables depend only on the frequency)."""
+    import raft.raft_fowt as rf
+    rf.interp2d = bilinear_interp2d
+    design = load_design(os.path.join(REF, "examples", "OC4semi-RAFT_QTF.yaml"))
+    design["platform"].pop("outFolderQTF", None)
+    model = raft.Model(design)
+    fowt = model.fowtList[0]
+    case = dict(zip(design["cases"]["keys"], design["cases"]["data"][0]))
+    case["wind_speed"] = 0
+    prepare_fowt(fowt, case)
+    out = design_tables(fowt)
+    mcf = out.pop("node_Imat_MCF", None)
+    if mcf is not None:                      # keep a sample of bins only (fixture size)
+        out["node_Imat_MCF_bins"] = np.arange(0, fowt.nw, 37)
+        out["node_Imat_MCF_sample"] = mcf[..., ::37]
+    captured = {}
+    orig = fowt.calcQTF_slenderBody
+
+    def spy(waveHeadInd, Xi0=None, verbose=False, iCase=None, iWT=None):
+        captured["Xi0"] = np.array(Xi0)
+        t0 = time.perf_counter()
+        r = orig(waveHeadInd, Xi0=Xi0, verbose=False, iCase=iCase, iWT=iWT)
+        captured["qtf_seconds"] = time.perf_counter() - t0
+        return r
+    fowt.calcQTF_slenderBody = spy
+    buf = io.StringIO()
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(buf):
+        Xi = model.solveDynamics(dict(case), display=2)
+    dt = time.perf_counter() - t0
+    its = [int(m) + 1 for m in re.findall(r"Iteration (\d+), converged", buf.getvalue())]
+    out.update(out_Xi=np.array(Xi), out_iters_pair=np.array(its), out_qtf=fowt.qtf.copy(), out_Xi0=captured["Xi0"],
+               out_Fhydro_2nd=fowt.Fhydro_2nd.copy(), out_Fhydro_2nd_mean=fowt.Fhydro_2nd_mean.copy(),
+               out_zeta=fowt.zeta.copy(), out_S=fowt.S.copy(), out_B_drag=fowt.B_hydro_drag.copy(),
+               w1_2nd=fowt.w1_2nd.copy(), k1_2nd=fowt.k1_2nd.copy(), qtf_seconds=captured["qtf_seconds"],
+               seconds=dt, nIter=np.int64(model.nIter), XiStart=np.float64(model.XiStart),
+               cases_json=np.array(json.dumps([{k: np.atleast_1d(case[k]).tolist() for k in
+                                               ["wave_spectrum", "wave_period", "wave_height", "wave_heading"]}])))
+    print(f"  qtf: iters {its}, QTF n2={len(fowt.w1_2nd)} {captured['qtf_seconds']:.1f}s, total {dt:.1f}s",
+          file=sys.stderr)
+    # 400-grid subset
+    w400 = np.arange(0.04, 0.35 + 0.5 * 0.04, 0.000825) * 2 * np.pi
+    rng = np.random.default_rng(20241016)
+    sel = np.sort(rng.choice(len(w400), 24, replace=False))
+    fowt.w1_2nd = w400[sel]
+    fowt.w2_2nd = fowt.w1_2nd.copy()
+    fowt.k1_2nd = np.array([raft.helpers.waveNumber(w, fowt.depth) for w in fowt.w1_2nd])
+    fowt.k2_2nd = fowt.k1_2nd.copy()
+    t0 = time.perf_counter()
+    orig(0, Xi0=captured["Xi0"], verbose=False)
+    out.update(sub400_n2=np.int64(len(w400)), sub400_idx=sel, sub400_w=fowt.w1_2nd.copy(), sub400_k=fowt.k1_2nd.copy(),
+               sub400_qtf=fowt.qtf.copy(), sub400_seconds=time.perf_counter() - t0)
+    # an oblique heading exercises the degree/radian quirk (SURVEY.md Q1) of the wave helpers
+    fowt.beta = np.array([np.deg2rad(30.0)])
+    orig(0, Xi0=captured["Xi0"], verbose=False)
+    out.update(sub400_beta30_qtf=fowt.qtf.copy(), sub400_beta30=np.float64(fowt.beta[0]))
+    print(f"  qtf: 400-grid subset ({len(sel)} freqs, {len(sel)*(len(sel)+1)//2} pairs) "
+          f"{out['sub400_seconds']:.1f}s", file=sys.stderr)
+    np.savez_compressed(os.path.join(HERE, "c3_qtf.npz"), **out)
+    print("wrote c3_qtf.npz", file=sys.stderr)
+
+
 def main(which):
+    if "qtf" in which:
+        golden_qtf()
     if "designs" in which:
         export_designs()
     ex = os.path.join(REF, "examples", "VolturnUS-S_example.yaml")
