@@ -121,6 +121,9 @@ typedef struct {
                              raft/raft_model.py:914), or NULL                  */
   const int* order;       /* optional launch order (a permutation of 0..ncase-1, e.g. cases sorted
                              by design/heading so each XCD's L2 holds few wave tables), or NULL */
+  const rh_c128* Xi_init; /* [ncase][6][nw] initial XiLast instead of XiStart, or NULL          */
+  int first_iter;         /* initial value of the iteration counter (1 for the second pass of
+                             potSecOrder=1, raft/raft_model.py:973-1000), normally 0         */
 } rh_cases;
 
 /* Outputs of rh_solve_cases (device buffers; NULL = not wanted). */
@@ -136,6 +139,8 @@ typedef struct {
   double* std;            /* [ncase][6] motion RMS                             */
   rh_c128* rao;           /* [ncase][6][nw] Xi / zeta (raft/helpers.py:665)   */
   rh_c128* Z;             /* [ncase][nw][36] final impedance (fowt.Z, raft/raft_model.py:1013) */
+  rh_c128* Xi_prev;       /* [ncase][6][nw] XiLast of the final iteration (the un-relaxed iterate the
+                             potSecOrder=1 second pass restarts from, Q6), or NULL */
 } rh_solve_out;
 
 const char* rh_last_error(void);
@@ -197,6 +202,78 @@ int rh_motion_stats(rh_ctx* ctx, int ncase, int nrow, int nw, double dw, const r
  * K: [6nf*6nf] array mooring stiffness (or NULL), F: [6nf][nw], Xi out: [6nf][nw]. */
 int rh_system_solve(rh_ctx* ctx, int nf, int nw, const rh_c128* Z, const double* K,
                     const rh_c128* F, rh_c128* Xi, rh_stream stream);
+
+/* ------------------------------------------------------------------------------------
+ * Slender-body second-order QTF (FOWT.calcQTF_slenderBody, raft/raft_fowt.py:1385-1648)
+ * ------------------------------------------------------------------------------------ */
+
+/* QTF node table fields ([RH_QN_COUNT][nq]): submerged strip nodes (r_z < 0) of the
+ * members that are not entirely above water, member-contiguous, reference order. */
+enum rh_qtf_node_field {
+  RH_QN_RX = 0, RH_QN_RY, RH_QN_RZ,      /* node position (the QTF uses mem.r, :1476)            */
+  RH_QN_QX, RH_QN_QY, RH_QN_QZ,          /* member axis                                          */
+  RH_QN_VI,                              /* side volume incl. partial-submergence scaling (:1532-1538) */
+  RH_QN_VE,                              /* end volume (:1580-1584)                              */
+  RH_QN_AI,                              /* signed end area mem.a_i (:1587)                      */
+  RH_QN_CAE,                             /* Ca_End                                               */
+  RH_QN_CM = 10,                         /* (1+Ca_p1) p1 p1^T + (1+Ca_p2) p2 p2^T   (9)          */
+  RH_QN_CA = 19,                         /* Ca_p1 p1 p1^T + Ca_p2 p2 p2^T           (9)          */
+  RH_QN_P12 = 28,                        /* p1 p1^T + p2 p2^T                       (9)          */
+  RH_QN_QM = 37,                         /* q q^T                                   (9)          */
+  RH_QN_COUNT = 46
+};
+
+/* QTF member table fields ([RH_QM_COUNT][nmq]) */
+enum rh_qtf_member_field {
+  RH_QM_WL = 0,                          /* 1: member crosses the waterline (mem.r[-1,2]*mem.r[0,2] < 0) */
+  RH_QM_RIX, RH_QM_RIY, RH_QM_RIZ,       /* waterline intersection r_int (:1492)                  */
+  RH_QM_AWL,                             /* waterline section area (:1608-1622)                   */
+  RH_QM_CM = 5,                          /* CmM of the LAST submerged node (the reference reuses the loop's Ca, :1625) (9) */
+  RH_QM_CA = 14,                         /* CaM of the last submerged node (9)                    */
+  RH_QM_P1X = 23, RH_QM_P1Y, RH_QM_P1Z,  /* p1, p2 for the hydrostatic term g_e1 (:1497-1499)    */
+  RH_QM_P2X, RH_QM_P2Y, RH_QM_P2Z,
+  RH_QM_KAY = 29,                        /* 1: Kim & Yue correction active (MCF, piercing)        */
+  RH_QM_PFX, RH_QM_PFY, RH_QM_PFZ,       /* normalised force direction pforce (raft_member.py:1130-1131) */
+  RH_QM_WLX, RH_QM_WLY, RH_QM_WLZ,       /* rwl (raft_member.py:1136)                             */
+  RH_QM_COUNT
+};
+
+/* Kim & Yue radius table ([RH_KR_COUNT][nkr]); for each KAY member the first entry is the
+ * waterline radius, the following ones the submerged node intervals (raft_member.py:1155-1200). */
+enum rh_kay_field {
+  RH_KR_R = 0,                           /* radius R (waterline) or mean radius Rm (interval)    */
+  RH_KR_Z1, RH_KR_Z2,                    /* interval ends (z2 clipped at 0)                      */
+  RH_KR_MX, RH_KR_MY, RH_KR_MZ,          /* interval mid-point 0.5 (r1 + r2)                     */
+  RH_KR_COUNT
+};
+
+typedef struct {
+  int n2, nq, nmq, nkr;
+  double beta, depth, rho, g;
+  const double* w2;        /* [n2] second-order frequencies (rad/s)                     */
+  const double* k2;        /* [n2] their wave numbers                                   */
+  const double* qnode;     /* [RH_QN_COUNT][nq]                                         */
+  const double* qmemb;     /* [RH_QM_COUNT][nmq]                                        */
+  const int* qmstart;      /* [nmq+1] node ranges                                       */
+  const int* kstart;       /* [nmq+1] ranges in the KAY radius table                    */
+  const double* kray;      /* [RH_KR_COUNT][nkr]                                        */
+  const rh_c128* hank;     /* [nkr][n2][12]  0.5 (H1_{n-1}(k R) - H1_{n+1}(k R)), n = 0..11 (scipy hankel1) */
+} rh_qtf_design;
+
+/* Device workspace (bytes) rh_qtf_slender needs for a design. */
+long long rh_qtf_workspace_bytes(const rh_qtf_design* q);
+
+/* Slender-body QTF for one heading: Xi0 [6][nw] motion RAO on the first-order grid w [nw];
+ * M66 [36] structural mass matrix (F1st, :1437-1439); qtf out [n2][n2][6] (full Hermitian
+ * matrix, upper triangle computed, lower filled as :1639-1640).  work: device workspace. */
+int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
+                   const double* M66, rh_c128* qtf, void* work, long long work_bytes, rh_stream stream);
+
+/* Second-order force spectrum, 'qtf' interpolation mode (raft/raft_fowt.py:1788-1810):
+ * qtf [n2][n2][6] on grid w2 [n2] (uniform spacing), spectrum S0 [nw] on grid w [nw]
+ * (uniform spacing dw) -> f [6][nw] (already shifted by one bin), f_mean [6]. */
+int rh_force_2nd(rh_ctx* ctx, int n2, const double* w2, const rh_c128* qtf, int nw, const double* w, double dw,
+                 const double* S0, double* f, double* f_mean, rh_stream stream);
 
 #ifdef __cplusplus
 }

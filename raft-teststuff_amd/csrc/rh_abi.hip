@@ -11,6 +11,7 @@
 #include "rh_device.h"
 
 #include "rh_kernels.hip"   // single translation unit: kernels + their host launchers
+#include "rh_qtf.hip"
 
 struct rh_ctx {
   int device = 0;
@@ -137,6 +138,8 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   if (!out->Xi || !out->Xi_last || !out->iters || !out->status)
     return fail(RH_EINVAL, "rh_solve_cases: Xi, Xi_last, iters and status outputs are required");
   if (cases->nIter < 0) return fail(RH_EINVAL, "rh_solve_cases: nIter=%d", cases->nIter);
+  if (cases->first_iter < 0 || cases->first_iter > cases->nIter)
+    return fail(RH_EINVAL, "rh_solve_cases: first_iter=%d outside [0, nIter=%d]", cases->first_iter, cases->nIter);
   const int nw = designs[0].nw;
   int nnmax = 0;
   for (int i = 0; i < ndesign; ++i) {
@@ -253,6 +256,53 @@ int rh_system_solve(rh_ctx* ctx, int nf, int nw, const rh_c128* Z, const double*
   const size_t smem = sizeof(double) * 2 * (size_t)(N * N + N) * rh::kSysThreads;
   dim3 grid((nw + rh::kSysThreads - 1) / rh::kSysThreads);
   hipLaunchKernelGGL(rh::k_system_solve, grid, dim3(rh::kSysThreads), smem, (hipStream_t)stream, N, nw, Z, K, F, Xi);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
+long long rh_qtf_workspace_bytes(const rh_qtf_design* q) {
+  if (!q) return -1;
+  return (long long)(rh::qtf_work_elems(*q) * sizeof(rh_c128));
+}
+
+int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0, const double* M66,
+                   rh_c128* qtf, void* work, long long work_bytes, rh_stream stream) {
+  if (!ctx || !q || !w || !Xi0 || !M66 || !qtf || !work) return fail(RH_EINVAL, "rh_qtf_slender: null argument");
+  if (q->n2 < 1 || q->nq < 0 || q->nmq < 0 || q->nkr < 0 || nw < 2)
+    return fail(RH_EINVAL, "rh_qtf_slender: bad sizes n2=%d nq=%d nmq=%d nkr=%d nw=%d", q->n2, q->nq, q->nmq, q->nkr, nw);
+  if (!q->w2 || !q->k2 || (q->nq > 0 && !q->qnode) || (q->nmq > 0 && (!q->qmemb || !q->qmstart || !q->kstart)) ||
+      (q->nkr > 0 && (!q->kray || !q->hank)))
+    return fail(RH_EINVAL, "rh_qtf_slender: null table");
+  if (work_bytes < rh_qtf_workspace_bytes(q)) return fail(RH_EINVAL, "rh_qtf_slender: workspace too small");
+  RH_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  rh::QtfWork wk;
+  wk.node = (rh_c128*)work;
+  wk.wl = wk.node + (size_t)q->nq * rh::QT_COUNT * q->n2;
+  wk.freq = wk.wl + (size_t)q->nmq * rh::WT_COUNT * q->n2;
+  const int nb = (q->n2 + 63) / 64;
+  hipLaunchKernelGGL(rh::k_qtf_freq, dim3(nb), dim3(64), 0, s, *q, nw, w, Xi0, M66, wk);
+  RH_HIP(hipGetLastError());
+  if (q->nq > 0) {
+    hipLaunchKernelGGL(rh::k_qtf_nodes, dim3(nb, q->nq), dim3(64), 0, s, *q, wk);
+    RH_HIP(hipGetLastError());
+  }
+  if (q->nmq > 0) {
+    hipLaunchKernelGGL(rh::k_qtf_wl, dim3(nb, q->nmq), dim3(64), 0, s, *q, wk);
+    RH_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(rh::k_qtf_pairs, dim3((q->n2 + rh::kQtfTile - 1) / rh::kQtfTile, q->n2), dim3(rh::kQtfTile), 0, s,
+                     *q, wk, qtf);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
+int rh_force_2nd(rh_ctx* ctx, int n2, const double* w2, const rh_c128* qtf, int nw, const double* w, double dw,
+                 const double* S0, double* f, double* f_mean, rh_stream stream) {
+  if (!ctx || !w2 || !qtf || !w || !S0 || !f || !f_mean) return fail(RH_EINVAL, "rh_force_2nd: null argument");
+  if (n2 < 2 || nw < 2 || !(dw > 0)) return fail(RH_EINVAL, "rh_force_2nd: bad sizes");
+  RH_HIP(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(rh::k_force2nd, dim3(nw), dim3(256), 0, (hipStream_t)stream, n2, w2, qtf, nw, w, dw, S0, f, f_mean);
   RH_HIP(hipGetLastError());
   return RH_OK;
 }

@@ -344,18 +344,20 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
   }
   rh_c128* Xo = a.o.Xi + (size_t)ic * 6 * nw;
   rh_c128* XL = a.o.Xi_last + (size_t)ic * 6 * nw;
+  const rh_c128* XI0 = a.c.Xi_init ? a.c.Xi_init + (size_t)ic * 6 * nw : nullptr;
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int b = tid + kThreads * j;
     if (b < nw)
 #pragma unroll
-      for (int c = 0; c < 6; ++c) st(XL + c * nw + b, mk(a.c.XiStart, 0.0));
+      for (int c = 0; c < 6; ++c) st(XL + c * nw + b, XI0 ? ld(XI0 + c * nw + b) : mk(a.c.XiStart, 0.0));
   }
+  rh_c128* XP = a.o.Xi_prev ? a.o.Xi_prev + (size_t)ic * 6 * nw : nullptr;
 
   const int nloop = a.c.nIter + 1;
   const double tol = a.c.tol;
   int status = RH_CASE_NOT_CONVERGED, iters = nloop;
-  for (int it = 0; it < nloop; ++it) {
+  for (int it = a.c.first_iter; it < nloop; ++it) {
     // ---------------- A: per-node sums of squared relative-velocity components ----------
     // Member-factored (see rh_member_field): per (member, bin) the motion terms
     //   Bq = iw cq.Xi, B1 = iw c1.Xi, B2 = iw c2.Xi, E1 = iw p2.th, E2 = -iw p1.th
@@ -487,6 +489,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
         const double t = cabs(sub(x, xlast)) / (cabs(x) + tol);
         my_ok = my_ok && (t < tol);
         st(Xo + c * nw + b, x);
+        if (XP) st(XP + c * nw + b, xlast);
         // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged
         st(XL + c * nw + b, add(scl(xlast, 0.2), scl(x, 0.8)));
       }

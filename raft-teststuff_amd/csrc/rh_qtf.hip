@@ -1,0 +1,705 @@
+// rh_qtf.hip -- slender-body second-order QTF on gfx950.
+//
+//   k_qtf_freq   : per second-order frequency: RAO resampled from the first-order grid
+//                  (np.interp, left=right=0, raft/raft_fowt.py:1415-1417), first-order force
+//                  F1st = M a (:1437-1439), rotation generator i w theta (:1556-1557)
+//   k_qtf_nodes  : per (node, frequency): incident velocity u, node displacement/velocity,
+//                  grad u (raft/helpers.py:157-195), grad p (:202-225), axial projections
+//   k_qtf_wl     : per (member, frequency): waterline kinematics (raft/raft_fowt.py:1486-1502)
+//   k_qtf_pairs  : per (w1 <= w2) pair: Pinkster IV + every node term + waterline term +
+//                  Kim & Yue correction, then the Hermitian fill (:1449-1640, raft_member.py:1090-1205)
+//   k_force2nd   : difference-frequency force spectrum with on-the-fly bilinear resampling
+//                  of the QTF (raft/raft_fowt.py:1788-1810; interp2d restated per SURVEY.md Q13)
+//
+// Layout: every per-frequency table is frequency-contiguous, so the lanes of a wave (64
+// consecutive w2 of one w1 row) read coalesced rows for the w2 side and a broadcast for the
+// w1 side.
+namespace rh {
+
+constexpr double kDeg2Rad = 0.017453292519943295;   // raft/helpers.py:27-28
+constexpr int kQtfTile = 64;
+
+// per-(node, frequency) table fields (complex) [nq][QT_COUNT][n2]
+enum { QT_U = 0, QT_VP = 3, QT_VA = 6, QT_DR = 7, QT_GU = 10, QT_GP = 19, QT_DWDZ = 22, QT_COUNT = 23 };
+// per-(member, frequency) waterline fields (complex) [nmq][WT_COUNT][n2]
+enum { WT_ETAR = 0, WT_UD = 1, WT_A = 4, WT_GE = 7, WT_COUNT = 10 };
+// per-frequency fields (complex) [FT_COUNT][n2]
+enum { FT_XI = 0, FT_F1 = 6, FT_OM = 12, FT_COUNT = 15 };
+
+struct QtfWork {
+  rh_c128* node;   // [nq][QT_COUNT][n2]
+  rh_c128* wl;     // [nmq][WT_COUNT][n2]
+  rh_c128* freq;   // [FT_COUNT][n2]
+};
+
+__host__ __device__ inline size_t qtf_work_elems(const rh_qtf_design& q) {
+  return (size_t)q.nq * QT_COUNT * q.n2 + (size_t)q.nmq * WT_COUNT * q.n2 + (size_t)FT_COUNT * q.n2;
+}
+
+__device__ __forceinline__ double qn(const rh_qtf_design& q, int f, int n) { return q.qnode[f * q.nq + n]; }
+__device__ __forceinline__ double qm(const rh_qtf_design& q, int f, int m) { return q.qmemb[f * q.nmq + m]; }
+
+// cross products with a real vector (np.cross order)
+__device__ __forceinline__ void cross_cc(const cd* a, const cd* b, cd* o) {
+  o[0] = sub(mul(a[1], b[2]), mul(a[2], b[1]));
+  o[1] = sub(mul(a[2], b[0]), mul(a[0], b[2]));
+  o[2] = sub(mul(a[0], b[1]), mul(a[1], b[0]));
+}
+__device__ __forceinline__ cd cconj(cd a) { return cd{a.r, -a.i}; }
+// real 3x3 (row-major, 9 consecutive fields) times complex 3-vector
+__device__ __forceinline__ void rmv(const double* M, const cd* x, cd* y) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) y[i] = add(add(scl(x[0], M[3 * i]), scl(x[1], M[3 * i + 1])), scl(x[2], M[3 * i + 2]));
+}
+// complex 3x3 times complex 3-vector
+__device__ __forceinline__ void cmv(const cd* M, const cd* x, cd* y) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) y[i] = add(add(mul(M[3 * i], x[0]), mul(M[3 * i + 1], x[1])), mul(M[3 * i + 2], x[2]));
+}
+// [f; r x f] accumulated into Q (translateForce3to6DOF, raft/helpers.py:386-401)
+__device__ __forceinline__ void acc6(cd* Q, const cd* f, double rx, double ry, double rz) {
+  Q[0] = add(Q[0], f[0]);
+  Q[1] = add(Q[1], f[1]);
+  Q[2] = add(Q[2], f[2]);
+  Q[3] = add(Q[3], sub(scl(f[2], ry), scl(f[1], rz)));
+  Q[4] = add(Q[4], sub(scl(f[0], rz), scl(f[2], rx)));
+  Q[5] = add(Q[5], sub(scl(f[1], rx), scl(f[0], ry)));
+}
+
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_qtf_freq(rh_qtf_design q, int nw, const double* __restrict__ w,
+                                                  const rh_c128* __restrict__ Xi0, const double* __restrict__ M66,
+                                                  QtfWork wk) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n2 = q.n2;
+  if (f >= n2) return;
+  const double x = q.w2[f];
+  cd X[6];
+  // np.interp(x, w, Xi0[d], left=0, right=0): j with w[j] <= x < w[j+1]
+  if (x < w[0] || x > w[nw - 1]) {
+#pragma unroll
+    for (int d = 0; d < 6; ++d) X[d] = mk(0, 0);
+  } else if (x == w[nw - 1]) {
+#pragma unroll
+    for (int d = 0; d < 6; ++d) X[d] = ld(Xi0 + (size_t)d * nw + nw - 1);
+  } else {
+    int lo = 0, hi = nw - 1;              // invariant: w[lo] <= x < w[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (w[mid] <= x) lo = mid; else hi = mid;
+    }
+    const double dx = w[lo + 1] - w[lo];
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+      const cd a = ld(Xi0 + (size_t)d * nw + lo), b = ld(Xi0 + (size_t)d * nw + lo + 1);
+      const double sr = (b.r - a.r) / dx, si = (b.i - a.i) / dx;
+      X[d] = mk(sr * (x - w[lo]) + a.r, si * (x - w[lo]) + a.i);
+    }
+  }
+  const double m2 = -(x * x);
+  cd A[6];
+#pragma unroll
+  for (int d = 0; d < 6; ++d) A[d] = scl(X[d], m2);   // -w^2 Xi
+  cd F[6];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) F[d] = scl(A[d], M66[0]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    F[3 + i] = add(add(scl(A[3], M66[6 * (3 + i) + 3]), scl(A[4], M66[6 * (3 + i) + 4])), scl(A[5], M66[6 * (3 + i) + 5]));
+#pragma unroll
+  for (int d = 0; d < 6; ++d) {
+    st(wk.freq + (size_t)(FT_XI + d) * n2 + f, X[d]);
+    st(wk.freq + (size_t)(FT_F1 + d) * n2 + f, F[d]);
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) st(wk.freq + (size_t)(FT_OM + d) * n2 + f, iw(x, X[3 + d]));
+}
+
+// unit-amplitude Airy velocity at a point (raft/helpers.py:105-154, zeta0 = 1)
+__device__ __forceinline__ void airy_u(double w, double k, double beta, double h, double x, double y, double z, cd* u,
+                                       cd* eta_out = nullptr) {
+  const double th = k * (cos(beta) * x + sin(beta) * y);
+  const cd e = mk(cos(th), -sin(th));
+  if (!(z <= 0)) {
+    u[0] = u[1] = u[2] = mk(0, 0);
+    if (eta_out) *eta_out = mk(0, 0);
+    return;
+  }
+  double s_sh, c_sh, c_ch;
+  if (k * h > 89.4) {
+    s_sh = exp(k * z);
+    c_sh = exp(k * z);
+    c_ch = exp(k * z) + exp(-k * (z + 2.0 * h));
+  } else {
+    s_sh = sinh(k * (z + h)) / sinh(k * h);
+    c_sh = cosh(k * (z + h)) / sinh(k * h);
+    c_ch = cosh(k * (z + h)) / cosh(k * h);
+  }
+  const cd we = scl(e, w);
+  u[0] = scl(scl(we, c_sh), cos(beta));
+  u[1] = scl(scl(we, c_sh), sin(beta));
+  u[2] = scl(iw(w, e), s_sh);
+  if (eta_out) *eta_out = scl(e, c_ch);   // pDyn with rho = g = 1 (raft/raft_fowt.py:1493)
+}
+
+__global__ __launch_bounds__(64) void k_qtf_nodes(rh_qtf_design q, QtfWork wk) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = blockIdx.y;
+  const int n2 = q.n2;
+  if (f >= n2) return;
+  const double w = q.w2[f], k = q.k2[f], h = q.depth, beta = q.beta;
+  const double x = qn(q, RH_QN_RX, n), y = qn(q, RH_QN_RY, n), z = qn(q, RH_QN_RZ, n);
+  const double qv[3] = {qn(q, RH_QN_QX, n), qn(q, RH_QN_QY, n), qn(q, RH_QN_QZ, n)};
+  cd X[6];
+#pragma unroll
+  for (int d = 0; d < 6; ++d) X[d] = ld(wk.freq + (size_t)(FT_XI + d) * n2 + f);
+  // getKinematics at the node (raft/helpers.py:95-97): dr = Xi[:3] + th x r ; v = i w dr
+  cd dr[3];
+  dr[0] = add(X[0], add(scl(X[5], -y), scl(X[4], z)));
+  dr[1] = add(X[1], sub(scl(X[5], x), scl(X[3], z)));
+  dr[2] = add(X[2], add(scl(X[4], -x), scl(X[3], y)));
+  cd v[3] = {iw(w, dr[0]), iw(w, dr[1]), iw(w, dr[2])};
+  cd u[3];
+  airy_u(w, k, beta, h, x, y, z, u);
+  // nodeV_axial_rel = (u - nodeV) . q (:1482), before any projection
+  const cd va = add(add(scl(sub(u[0], v[0]), qv[0]), scl(sub(u[1], v[1]), qv[1])), scl(sub(u[2], v[2]), qv[2]));
+  // node velocity after _axdivAcc's in-place projection: every later use is projected
+  const cd vq = add(add(scl(v[0], qv[0]), scl(v[1], qv[1])), scl(v[2], qv[2]));
+  cd vp[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) vp[i] = sub(v[i], scl(vq, qv[i]));
+  // grad u (raft/helpers.py:157-195) with the degree-converted direction cosines (Q1), Q2
+  cd G[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) G[i] = mk(0, 0);
+  cd gp[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+  if (z <= 0 && k > 0) {
+    const double cb = cos(beta * kDeg2Rad), sb = sin(beta * kDeg2Rad);
+    double kxy, kz;
+    if (k * h >= 10) {
+      kxy = exp(k * z);
+      kz = kxy;
+    } else {
+      kxy = cosh(k * (z + h)) / sinh(k * h);
+      kz = sinh(k * (z + h)) / sinh(k * h);
+    }
+    const double th = k * (cos(beta) * x + sin(beta) * y);
+    const cd ph = mk(cos(th), -sin(th));
+    cd aux = scl(ph, w * cb);
+    const cd mi_aux = mk(aux.i, -aux.r);                         // -1j*aux
+    G[0] = scl(scl(scl(mi_aux, kxy), k), cb);
+    G[1] = scl(scl(scl(mi_aux, kxy), k), sb);
+    G[2] = scl(scl(aux, k), kz);
+    aux = scl(ph, w * sb);
+    const cd mi_aux2 = mk(aux.i, -aux.r);
+    G[3] = G[1];
+    G[4] = scl(scl(scl(mi_aux2, kxy), k), sb);
+    G[5] = scl(scl(aux, k), kz);
+    aux = iw(w, ph);
+    G[6] = G[2];
+    G[7] = G[1];                                                 // Q2: grad[2,1] = grad[0,1]
+    G[8] = scl(scl(aux, k), kxy);
+    // grad p1 (raft/helpers.py:202-225): phase with the degree-converted cosines
+    double pxy, pz;
+    if (k * h >= 10) {
+      pxy = exp(k * z);
+      pz = pxy;
+    } else {
+      pxy = cosh(k * (z + h)) / cosh(k * h);
+      pz = sinh(k * (z + h)) / cosh(k * h);
+    }
+    const double th2 = k * (cb * x + sb * y);
+    const cd ph2 = mk(cos(th2), -sin(th2));
+    const double rg = q.rho * q.g;
+    const cd a0 = scl(scl(ph2, rg * pxy), 1.0);
+    gp[0] = mul(a0, mk(0, -k * cb));
+    gp[1] = mul(a0, mk(0, -k * sb));
+    gp[2] = scl(scl(ph2, rg * pz), k);
+  }
+  // dw/dz along the axis for _axdivAcc: (grad u q) . q
+  cd Gq[3];
+  cd qc[3] = {mk(qv[0], 0), mk(qv[1], 0), mk(qv[2], 0)};
+  cmv(G, qc, Gq);
+  const cd dwdz = add(add(scl(Gq[0], qv[0]), scl(Gq[1], qv[1])), scl(Gq[2], qv[2]));
+  rh_c128* T = wk.node + (size_t)n * QT_COUNT * n2 + f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    st(T + (size_t)(QT_U + i) * n2, u[i]);
+    st(T + (size_t)(QT_VP + i) * n2, vp[i]);
+    st(T + (size_t)(QT_DR + i) * n2, dr[i]);
+    st(T + (size_t)(QT_GP + i) * n2, gp[i]);
+  }
+  st(T + (size_t)QT_VA * n2, va);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) st(T + (size_t)(QT_GU + i) * n2, G[i]);
+  st(T + (size_t)QT_DWDZ * n2, dwdz);
+}
+
+__global__ __launch_bounds__(64) void k_qtf_wl(rh_qtf_design q, QtfWork wk) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  const int m = blockIdx.y;
+  const int n2 = q.n2;
+  if (f >= n2) return;
+  rh_c128* T = wk.wl + (size_t)m * WT_COUNT * n2 + f;
+  const double w = q.w2[f], k = q.k2[f];
+  cd X[6];
+#pragma unroll
+  for (int d = 0; d < 6; ++d) X[d] = ld(wk.freq + (size_t)(FT_XI + d) * n2 + f);
+  cd eta = mk(0, 0), ud[3] = {mk(0, 0), mk(0, 0), mk(0, 0)}, dr2 = mk(0, 0), a[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
+  if (qm(q, RH_QM_WL, m) != 0.0) {
+    const double x = qm(q, RH_QM_RIX, m), y = qm(q, RH_QM_RIY, m), z = qm(q, RH_QM_RIZ, m);
+    cd u[3];
+    airy_u(w, k, q.beta, q.depth, x, y, z, u, &eta);
+    ud[0] = iw(w, u[0]);
+    ud[1] = iw(w, u[1]);
+    ud[2] = iw(w, u[2]);
+    cd dr[3];
+    dr[0] = add(X[0], add(scl(X[5], -y), scl(X[4], z)));
+    dr[1] = add(X[1], sub(scl(X[5], x), scl(X[3], z)));
+    dr[2] = add(X[2], add(scl(X[4], -x), scl(X[3], y)));
+#pragma unroll
+    for (int i = 0; i < 3; ++i) a[i] = iw(w, iw(w, dr[i]));
+    dr2 = dr[2];
+  }
+  // g_e1 = -g (cross(th, p1)[2] p1 + cross(th, p2)[2] p2)   (:1497-1499)
+  const double p1[3] = {qm(q, RH_QM_P1X, m), qm(q, RH_QM_P1Y, m), qm(q, RH_QM_P1Z, m)};
+  const double p2[3] = {qm(q, RH_QM_P2X, m), qm(q, RH_QM_P2Y, m), qm(q, RH_QM_P2Z, m)};
+  const cd c1 = sub(scl(X[3], p1[1]), scl(X[4], p1[0]));
+  const cd c2 = sub(scl(X[3], p2[1]), scl(X[4], p2[0]));
+  st(T + (size_t)WT_ETAR * n2, sub(eta, dr2));
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    st(T + (size_t)(WT_UD + i) * n2, ud[i]);
+    st(T + (size_t)(WT_A + i) * n2, a[i]);
+    st(T + (size_t)(WT_GE + i) * n2, scl(add(scl(c1, p1[i]), scl(c2, p2[i])), -q.g));
+  }
+}
+
+// load a 3-vector field of a table
+__device__ __forceinline__ void ld3(const rh_c128* T, int field, size_t n2, int f, cd* o) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o[i] = ld(T + (size_t)(field + i) * n2 + f);
+}
+
+// omega of raft_member.py:1102-1109 from the Hankel derivative table D_n (n = 0..11)
+__device__ __forceinline__ cd kay_omega(const rh_c128* D1, const rh_c128* D2, int n) {
+  const cd HN_ii = ld(D1 + n), HNm1_ii = ld(D1 + n + 1);
+  const cd HN_jj = cconj(ld(D2 + n)), HNm1_jj = cconj(ld(D2 + n + 1));
+  return sub(cdiv(mk(1, 0), mul(HNm1_ii, HN_jj)), cdiv(mk(1, 0), mul(HN_ii, HNm1_jj)));
+}
+
+__global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf) {
+  const int i1 = blockIdx.y;
+  const int i2 = blockIdx.x * kQtfTile + threadIdx.x;
+  const int n2 = q.n2;
+  if (i2 >= n2 || i2 < i1) return;
+  const double w1 = q.w2[i1], w2 = q.w2[i2], k1 = q.k2[i1], k2 = q.k2[i2];
+  if (w2 < w1) return;
+  const double h = q.depth, rho = q.rho, g = q.g, beta = q.beta;
+  cd Q[6];
+  // ---- Pinkster IV: rotation of the first-order force (:1449-1456)
+  {
+    cd th1[3], th2c[3], F1a[3], F1b[3], F2c[3], tmp1[3], tmp2[3];
+    ld3(wk.freq, FT_XI + 3, n2, i1, th1);
+    ld3(wk.freq, FT_XI + 3, n2, i2, th2c);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) th2c[i] = cconj(th2c[i]);
+    for (int part = 0; part < 2; ++part) {
+      ld3(wk.freq, FT_F1 + 3 * part, n2, i2, F2c);
+      ld3(wk.freq, FT_F1 + 3 * part, n2, i1, F1a);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) F2c[i] = cconj(F2c[i]);
+      cross_cc(th1, F2c, tmp1);
+      cross_cc(th2c, F1a, tmp2);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) Q[3 * part + i] = scl(add(tmp1[i], tmp2[i]), 0.25);
+      (void)F1b;
+    }
+  }
+  // ---- pair constants of the second-order potential (raft/helpers.py:254-291, Q1)
+  const bool pot_on = (w1 != w2) && (k1 > 0) && (k2 > 0);
+  double kx = 0, ky = 0, nk = 0, den12 = 1, den21 = 1, tnh = 0, cnh = 1;
+  cd aux2 = mk(0, 0);
+  if (pot_on) {
+    const double b = beta * kDeg2Rad, cb = cos(b), sb = sin(b);
+    kx = k1 * cb - k2 * cb;
+    ky = k1 * sb - k2 * sb;
+    nk = sqrt(kx * kx + ky * ky);
+    const double t1 = tanh(k1 * h), t2 = tanh(k2 * h);
+    tnh = tanh(nk * h);
+    cnh = cosh(nk * h);
+    den12 = (w1 - w2) * (w1 - w2) / g - nk * tnh;
+    den21 = (w2 - w1) * (w2 - w1) / g - nk * tnh;
+    const double n12 = (k1 * k1) * (1 - t1 * t1) - 2 * k1 * k2 * (1 + t1 * t2);
+    const double n21 = (k2 * k2) * (1 - t2 * t2) - 2 * k2 * k1 * (1 + t2 * t1);
+    const cd g12 = scl(mk(0, -g / (2 * w1)), n12 / den12);
+    const cd g21 = scl(mk(0, -g / (2 * w2)), n21 / den21);
+    aux2 = scl(add(g21, cconj(g12)), 0.5);
+  }
+  cd om1[3], om2[3];
+  ld3(wk.freq, FT_OM, n2, i1, om1);
+  ld3(wk.freq, FT_OM, n2, i2, om2);
+  // OMEGA = -getH(i w th):  -H = [[0,-v2,v1],[v2,0,-v0],[-v1,v0,0]]
+  const cd O1[9] = {mk(0, 0), scl(om1[2], -1), om1[1], om1[2], mk(0, 0), scl(om1[0], -1), scl(om1[1], -1), om1[0], mk(0, 0)};
+  const cd O2[9] = {mk(0, 0), scl(om2[2], -1), om2[1], om2[2], mk(0, 0), scl(om2[0], -1), scl(om2[1], -1), om2[0], mk(0, 0)};
+
+  for (int m = 0; m < q.nmq; ++m) {
+    const int n0 = q.qmstart[m], n1 = q.qmstart[m + 1];
+    for (int n = n0; n < n1; ++n) {
+      const rh_c128* T = wk.node + (size_t)n * QT_COUNT * n2;
+      const double rx = qn(q, RH_QN_RX, n), ry = qn(q, RH_QN_RY, n), rz = qn(q, RH_QN_RZ, n);
+      const double qv[3] = {qn(q, RH_QN_QX, n), qn(q, RH_QN_QY, n), qn(q, RH_QN_QZ, n)};
+      double CM[9], CA[9], P12[9], QM[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        CM[i] = qn(q, RH_QN_CM + i, n);
+        CA[i] = qn(q, RH_QN_CA + i, n);
+        P12[i] = qn(q, RH_QN_P12 + i, n);
+        QM[i] = qn(q, RH_QN_QM + i, n);
+      }
+      const double rv = rho * qn(q, RH_QN_VI, n);
+      const double rve = rho * qn(q, RH_QN_VE, n) * qn(q, RH_QN_CAE, n);
+      const double ai = qn(q, RH_QN_AI, n);
+      // second-order potential acceleration and pressure at the node
+      cd acc2[3] = {mk(0, 0), mk(0, 0), mk(0, 0)}, p2 = mk(0, 0);
+      if (pot_on && rz <= 0) {
+        const double kxy = cosh(nk * (rz + h)) / cnh, kz = sinh(nk * (rz + h)) / cnh;
+        const double th = kx * rx + ky * ry + 0 * rz;
+        const cd ph = mk(cos(th), -sin(th));
+        const cd base = mul(scl(aux2, kxy), ph);
+        acc2[0] = scl(base, (w1 - w2) * kx);
+        acc2[1] = scl(base, (w1 - w2) * ky);
+        acc2[2] = mul(mul(scl(aux2, kz), ph), mk(0, (w1 - w2) * nk));
+        p2 = mul(base, mk(0, -rho * (w1 - w2)));
+      }
+      cd u1[3], u2[3], vp1[3], vp2[3], dr1[3], dr2[3], gp1[3], gp2[3], G1[9], G2[9];
+      ld3(T, QT_U, n2, i1, u1);
+      ld3(T, QT_U, n2, i2, u2);
+      ld3(T, QT_VP, n2, i1, vp1);
+      ld3(T, QT_VP, n2, i2, vp2);
+      ld3(T, QT_DR, n2, i1, dr1);
+      ld3(T, QT_DR, n2, i2, dr2);
+      ld3(T, QT_GP, n2, i1, gp1);
+      ld3(T, QT_GP, n2, i2, gp2);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        G1[i] = ld(T + (size_t)(QT_GU + i) * n2 + i1);
+        G2[i] = ld(T + (size_t)(QT_GU + i) * n2 + i2);
+      }
+      const cd va1 = ld(T + (size_t)QT_VA * n2 + i1), va2 = ld(T + (size_t)QT_VA * n2 + i2);
+      const cd dz1 = ld(T + (size_t)QT_DWDZ * n2 + i1), dz2 = ld(T + (size_t)QT_DWDZ * n2 + i2);
+      cd G2c[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) G2c[i] = cconj(G2[i]);
+      cd f[3], t3[3], t4[3], t5[3];
+      // f_2ndPot (:1541-1542) + pressure and axial parts (:1587-1588)
+      rmv(CM, acc2, t3);
+      rmv(QM, acc2, t4);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) f[i] = add(add(scl(t3[i], rv), scl(p2, ai * qv[i])), scl(t4[i], rve));
+      acc6(Q, f, rx, ry, rz);
+      // convective acceleration (:1545-1546, 1589) and Bernoulli pressure drop (:1593-1594)
+      cd c1v[3], c2v[3], conv[3];
+      {
+        cd u2c[3] = {cconj(u2[0]), cconj(u2[1]), cconj(u2[2])};
+        cmv(G1, u2c, c1v);
+        cmv(G2c, u1, c2v);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) conv[i] = scl(add(c1v[i], c2v[i]), 0.25);
+      }
+      rmv(CM, conv, t3);
+      rmv(QM, conv, t4);
+      cd ur1[3], ur2[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        ur1[i] = sub(u1[i], vp1[i]);
+        ur2[i] = sub(u2[i], vp2[i]);
+      }
+      rmv(P12, ur1, t5);
+      cd cu2[3];
+      rmv(CA, ur2, cu2);
+      cd pd = mk(0, 0);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) pd = add(pd, mul(t5[i], cconj(cu2[i])));
+      pd = scl(pd, -2 * 0.25 * 0.5 * rho);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) f[i] = add(add(scl(t3[i], rv), scl(t4[i], rve)), scl(pd, ai * qv[i]));
+      acc6(Q, f, rx, ry, rz);
+      // Rainey axial divergence (raft/helpers.py:228-251)
+      {
+        cd up1[3], up2[3];
+        const cd s1 = add(add(scl(u1[0], qv[0]), scl(u1[1], qv[1])), scl(u1[2], qv[2]));
+        const cd s2 = add(add(scl(u2[0], qv[0]), scl(u2[1], qv[1])), scl(u2[2], qv[2]));
+        cd a[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          up1[i] = sub(u1[i], scl(s1, qv[i]));
+          up2[i] = sub(u2[i], scl(s2, qv[i]));
+          a[i] = scl(add(mul(dz1, cconj(sub(up2[i], vp2[i]))), mul(cconj(dz2), sub(up1[i], vp1[i]))), 0.25);
+        }
+        const cd aq = add(add(scl(a[0], qv[0]), scl(a[1], qv[1])), scl(a[2], qv[2]));
+#pragma unroll
+        for (int i = 0; i < 3; ++i) a[i] = sub(a[i], scl(aq, qv[i]));
+        rmv(CA, a, t3);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) f[i] = scl(t3[i], rv);
+        acc6(Q, f, rx, ry, rz);
+      }
+      // body motion in the first-order field (:1552-1553, 1590-1592)
+      {
+        cd d2c[3] = {cconj(dr2[0]), cconj(dr2[1]), cconj(dr2[2])};
+        cd a1[3], a2[3], an[3];
+        cmv(G1, d2c, a1);
+        cmv(G2c, dr1, a2);
+        // grad du/dt = i w grad u: 0.25 (i w1 G1) conj(dr2) + 0.25 conj(i w2 G2) dr1
+#pragma unroll
+        for (int i = 0; i < 3; ++i) an[i] = add(scl(iw(w1, a1[i]), 0.25), scl(iw(-w2, a2[i]), 0.25));
+        rmv(CM, an, t3);
+        rmv(QM, an, t4);
+        cd pn = mk(0, 0), pm = mk(0, 0);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          pn = add(pn, mul(gp1[i], cconj(dr2[i])));
+          pm = add(pm, mul(cconj(gp2[i]), dr1[i]));
+        }
+        const cd pnab = add(scl(pn, 0.25), scl(pm, 0.25));
+#pragma unroll
+        for (int i = 0; i < 3; ++i) f[i] = add(add(scl(t3[i], rv), scl(t4[i], rve)), scl(pnab, ai * qv[i]));
+        acc6(Q, f, rx, ry, rz);
+      }
+      // Rainey body-rotation terms (:1556-1575)
+      {
+        cd x1[3], x2[3], y1[3], y2[3], s[3];
+        cd va2q[3] = {cconj(scl(va2, qv[0])), cconj(scl(va2, qv[1])), cconj(scl(va2, qv[2]))};
+        cd va1q[3] = {scl(va1, qv[0]), scl(va1, qv[1]), scl(va1, qv[2])};
+        cd O2c[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) O2c[i] = cconj(O2[i]);
+        cmv(O1, va2q, x1);
+        cmv(O2c, va1q, x2);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) s[i] = add(x1[i], x2[i]);
+        rmv(CA, s, t3);
+        cd fr[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) fr[i] = scl(scl(t3[i], -0.25 * 2), rv);
+        cd V1[9], V2c[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+          V1[i] = add(G1[i], O1[i]);
+          V2c[i] = cconj(add(G2[i], O2[i]));
+        }
+        // aux = 0.25 (V1 conj(CaM u2a) + conj(V2) CaM u1a); aux -= qMat aux
+        cd cu1[3];
+        rmv(CA, ur1, cu1);
+        cd cu2c[3] = {cconj(cu2[0]), cconj(cu2[1]), cconj(cu2[2])};
+        cmv(V1, cu2c, x1);
+        cmv(V2c, cu1, x2);
+        cd ax[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) ax[i] = scl(add(x1[i], x2[i]), 0.25);
+        rmv(QM, ax, t4);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) fr[i] = add(fr[i], scl(sub(ax[i], t4[i]), rv));
+        // u_aux -= qMat u_aux ; aux = 0.25 (CaM V1 conj(u2a) + CaM conj(V2) u1a)
+        cd w1a[3], w2a[3];
+        rmv(QM, ur1, t4);
+        rmv(QM, ur2, t5);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          w1a[i] = sub(ur1[i], t4[i]);
+          w2a[i] = cconj(sub(ur2[i], t5[i]));
+        }
+        cmv(V1, w2a, x1);
+        cmv(V2c, w1a, x2);
+        rmv(CA, x1, y1);
+        rmv(CA, x2, y2);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) fr[i] = add(fr[i], scl(scl(add(y1[i], y2[i]), 0.25), -rv));
+        acc6(Q, fr, rx, ry, rz);
+      }
+    }
+    // ---- waterline relative-elevation force (:1602-1630)
+    if (qm(q, RH_QM_WL, m) != 0.0) {
+      const rh_c128* W = wk.wl + (size_t)m * WT_COUNT * n2;
+      const cd e1 = ld(W + (size_t)WT_ETAR * n2 + i1), e2c = cconj(ld(W + (size_t)WT_ETAR * n2 + i2));
+      cd ud1[3], ud2[3], a1[3], a2[3], ge1[3], ge2[3];
+      ld3(W, WT_UD, n2, i1, ud1);
+      ld3(W, WT_UD, n2, i2, ud2);
+      ld3(W, WT_A, n2, i1, a1);
+      ld3(W, WT_A, n2, i2, a2);
+      ld3(W, WT_GE, n2, i1, ge1);
+      ld3(W, WT_GE, n2, i2, ge2);
+      double CM[9], CA[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        CM[i] = qm(q, RH_QM_CM + i, m);
+        CA[i] = qm(q, RH_QM_CA + i, m);
+      }
+      const double ra = rho * qm(q, RH_QM_AWL, m);
+      cd fe[3], ae[3], t3[3], t4[3], fo[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        fe[i] = scl(add(mul(ud1[i], e2c), mul(cconj(ud2[i]), e1)), 0.25);
+        ae[i] = scl(add(mul(a1[i], e2c), mul(cconj(a2[i]), e1)), 0.25);
+      }
+      rmv(CM, fe, t3);
+      rmv(CA, ae, t4);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const cd gt = add(mul(ge1[i], e2c), mul(cconj(ge2[i]), e1));
+        fo[i] = sub(sub(scl(t3[i], ra), scl(t4[i], ra)), scl(gt, 0.25 * ra));
+      }
+      acc6(Q, fo, qm(q, RH_QM_RIX, m), qm(q, RH_QM_RIY, m), qm(q, RH_QM_RIZ, m));
+    }
+    // ---- Kim & Yue second-order diffraction (raft/raft_member.py:1090-1205)
+    if (qm(q, RH_QM_KAY, m) != 0.0) {
+      const int r0 = q.kstart[m], r1 = q.kstart[m + 1];
+      const double cb = cos(beta), sb = sin(beta);
+      const double kkx = k1 * cb - k2 * cb, kky = k1 * sb - k2 * sb;
+      const double wx = qm(q, RH_QM_WLX, m), wy = qm(q, RH_QM_WLY, m), wz = qm(q, RH_QM_WLZ, m);
+      const double thp = kkx * wx + kky * wy + 0 * wz;
+      const cd ph = mk(cos(thp), -sin(thp));
+      const double pf[3] = {qm(q, RH_QM_PFX, m), qm(q, RH_QM_PFY, m), qm(q, RH_QM_PFZ, m)};
+      cd Fk[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) Fk[i] = mk(0, 0);
+      for (int ir = r0; ir < r1; ++ir) {
+        const double R = q.kray[RH_KR_R * q.nkr + ir];
+        const rh_c128* D1 = q.hank + ((size_t)ir * n2 + i1) * 12;
+        const rh_c128* D2 = q.hank + ((size_t)ir * n2 + i2) * 12;
+        const double k1R = k1 * R, k2R = k2 * R;
+        double sre;
+        double px, py, pz;
+        if (ir == r0) {       // waterline term (:1133-1149)
+          const cd c0 = mk(0, -rho * g * R * 2 / M_PI / (k1R * k2R));
+          cd s = mk(0, 0);
+          for (int nn = 0; nn <= 10; ++nn) s = add(s, mul(c0, kay_omega(D1, D2, nn)));
+          sre = s.r;
+          px = wx;
+          py = wy;
+          pz = wz;
+        } else {              // node-interval Bernoulli term (:1155-1200)
+          const double z1 = q.kray[RH_KR_Z1 * q.nkr + ir], z2 = q.kray[RH_KR_Z2 * q.nkr + ir];
+          const double H = h / R;
+          const double k1h = k1R * H, k2h = k2R * H;
+          double Im, Ip;
+          const double a2 = sinh((k1 + k2) * (z2 + h)) / (k1h + k2h), a1 = sinh((k1 + k2) * (z1 + h)) / (k1h + k2h);
+          if (w1 == w2) {
+            Im = 0.5 * (a2 - (z2 + h) / h - a1 + (z1 + h) / h);
+            Ip = 0.5 * (a2 + (z2 + h) / h - a1 - (z1 + h) / h);
+          } else {
+            const double d2 = sinh((k1 - k2) * (z2 + h)) / (k1h - k2h), d1 = sinh((k1 - k2) * (z1 + h)) / (k1h - k2h);
+            Im = 0.5 * (a2 - d2 - a1 + d1);
+            Ip = 0.5 * (a2 + d2 - a1 - d1);
+          }
+          const double ch1 = cosh(k1h), ch2 = cosh(k2h);
+          const double coef = k1h * k2h / sqrt(k1h * tanh(k1h)) / sqrt(k2h * tanh(k2h));
+          const cd c0 = mk(0, rho * g * R * 2 / M_PI / (k1R * k2R));
+          cd s = mk(0, 0);
+          for (int nn = 0; nn <= 10; ++nn) {
+            const double tail = coef * (Im + Ip * nn * (nn + 1) / k1R / k2R) / ch1 / ch2;
+            s = add(s, scl(mul(c0, kay_omega(D1, D2, nn)), tail));
+          }
+          sre = s.r;
+          px = q.kray[RH_KR_MX * q.nkr + ir];
+          py = q.kray[RH_KR_MY * q.nkr + ir];
+          pz = q.kray[RH_KR_MZ * q.nkr + ir];
+        }
+        const cd Fs = scl(ph, sre);    // real part times the phase of the waterline point
+        cd fv[3] = {scl(Fs, pf[0]), scl(Fs, pf[1]), scl(Fs, pf[2])};
+        acc6(Fk, fv, px, py, pz);
+      }
+      const bool cj = k1 < k2;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) Q[i] = add(Q[i], cj ? cconj(Fk[i]) : Fk[i]);
+    }
+  }
+  // Hermitian fill (:1639-1640): qtf + conj(qtf).T - diag(conj(diag(qtf)))
+  rh_c128* up = qtf + ((size_t)i1 * n2 + i2) * 6;
+  if (i1 == i2) {
+#pragma unroll
+    for (int d = 0; d < 6; ++d) st(up + d, sub(add(Q[d], cconj(Q[d])), cconj(Q[d])));
+  } else {
+    rh_c128* lo = qtf + ((size_t)i2 * n2 + i1) * 6;
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+      st(up + d, Q[d]);
+      st(lo + d, cconj(Q[d]));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// second-order force spectrum: block per difference-frequency index mu
+// ---------------------------------------------------------------------------------------
+// RegularGridInterpolator(linear): i = searchsorted(grid, x) - 1 clipped to [0, n-2]
+__device__ __forceinline__ bool grid_cell(const double* g, int n, double x, int& i, double& t) {
+  if (x < g[0] || x > g[n - 1]) return false;          // fill_value = 0 strictly outside
+  int lo = 0, hi = n;                                     // searchsorted side='left'
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (g[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  i = lo - 1;
+  if (i < 0) i = 0;
+  if (i > n - 2) i = n - 2;
+  t = (x - g[i]) / (g[i + 1] - g[i]);
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_force2nd(int n2, const double* __restrict__ w2, const rh_c128* __restrict__ qtf,
+                                                   int nw, const double* __restrict__ w, double dw,
+                                                   const double* __restrict__ S0, double* __restrict__ fout,
+                                                   double* __restrict__ fmean) {
+  __shared__ double red[4][6];
+  const int mu = blockIdx.x;            // 0 = mean drift, 1..nw-1 difference frequencies
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = tid; i + mu < nw; i += 256) {
+    const int j = i + mu;
+    int iy, ix;
+    double ty, tx;
+    cd v[6];
+    // value at (y = w_i, x = w_j): z[y, x] orientation
+    if (grid_cell(w2, n2, w[i], iy, ty) && grid_cell(w2, n2, w[j], ix, tx)) {
+      const rh_c128* a = qtf + ((size_t)iy * n2 + ix) * 6;
+      const rh_c128* b = qtf + ((size_t)iy * n2 + ix + 1) * 6;
+      const rh_c128* c = qtf + ((size_t)(iy + 1) * n2 + ix) * 6;
+      const rh_c128* e = qtf + ((size_t)(iy + 1) * n2 + ix + 1) * 6;
+#pragma unroll
+      for (int d = 0; d < 6; ++d) {
+        const cd A = ld(a + d), B = ld(b + d), C = ld(c + d), E = ld(e + d);
+        v[d] = add(add(add(scl(A, (1 - ty) * (1 - tx)), scl(B, (1 - ty) * tx)), scl(C, ty * (1 - tx))), scl(E, ty * tx));
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < 6; ++d) v[d] = mk(0, 0);
+    }
+    if (mu == 0) {
+#pragma unroll
+      for (int d = 0; d < 6; ++d) acc[d] += S0[i] * v[d].r;
+    } else {
+      const double ss = S0[i] * S0[j];
+#pragma unroll
+      for (int d = 0; d < 6; ++d) acc[d] += ss * abs2(v[d]);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 6; ++d) {
+    const double s = wave_sum(acc[d]);
+    if (lane == 0) red[wv][d] = s;
+  }
+  __syncthreads();
+  if (tid < 6) {
+    const double s = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    if (mu == 0) {
+      fmean[tid] = 2 * s * dw;
+      fout[(size_t)tid * nw + (nw - 1)] = 0.0;           // last bin has no difference frequency
+    } else {
+      fout[(size_t)tid * nw + (mu - 1)] = 4 * sqrt(s) * dw;   // shifted by one bin (:1809-1810)
+    }
+  }
+}
+
+}  // namespace rh

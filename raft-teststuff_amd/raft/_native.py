@@ -41,12 +41,20 @@ class RhDesign(ctypes.Structure):
 class RhCases(ctypes.Structure):
     _fields_ = [("ncase", ctypes.c_int), ("design", _p), ("head", _p), ("spectrum", _p),
                 ("Hs", _p), ("Tp", _p), ("gamma", _p), ("nIter", ctypes.c_int),
-                ("XiStart", ctypes.c_double), ("tol", ctypes.c_double), ("fext", _p), ("order", _p)]
+                ("XiStart", ctypes.c_double), ("tol", ctypes.c_double), ("fext", _p), ("order", _p),
+                ("Xi_init", _p), ("first_iter", ctypes.c_int)]
 
 
 class RhSolveOut(ctypes.Structure):
     _fields_ = [("Xi", _p), ("Xi_last", _p), ("iters", _p), ("status", _p), ("zeta", _p), ("B_drag", _p),
-                ("Bmat", _p), ("psd", _p), ("std", _p), ("rao", _p), ("Z", _p)]
+                ("Bmat", _p), ("psd", _p), ("std", _p), ("rao", _p), ("Z", _p), ("Xi_prev", _p)]
+
+
+class RhQtfDesign(ctypes.Structure):
+    _fields_ = [("n2", ctypes.c_int), ("nq", ctypes.c_int), ("nmq", ctypes.c_int), ("nkr", ctypes.c_int),
+                ("beta", ctypes.c_double), ("depth", ctypes.c_double), ("rho", ctypes.c_double), ("g", ctypes.c_double),
+                ("w2", _p), ("k2", _p), ("qnode", _p), ("qmemb", _p), ("qmstart", _p), ("kstart", _p),
+                ("kray", _p), ("hank", _p)]
 
 
 class NativeError(RuntimeError):
@@ -80,11 +88,16 @@ def lib():
                 "rh_sea_state": [_p, ctypes.c_int, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p, _p, _p, _p],
                 "rh_motion_stats": [_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, _p, _p, _p, _p],
                 "rh_system_solve": [_p, ctypes.c_int, ctypes.c_int, _p, _p, _p, _p, _p],
+                "rh_qtf_slender": [_p, ctypes.POINTER(RhQtfDesign), ctypes.c_int, _p, _p, _p, _p, _p,
+                                   ctypes.c_longlong, _p],
+                "rh_force_2nd": [_p, ctypes.c_int, _p, _p, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p],
             }.items():
                 fn = getattr(L, name)
                 fn.argtypes = args
                 fn.restype = ctypes.c_int
             L.rh_version.restype = ctypes.c_int
+            L.rh_qtf_workspace_bytes.argtypes = [ctypes.POINTER(RhQtfDesign)]
+            L.rh_qtf_workspace_bytes.restype = ctypes.c_longlong
             _lib = L
     return _lib
 

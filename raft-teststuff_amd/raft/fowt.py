@@ -7,8 +7,9 @@ the per-design preparation (members, node tables, linear matrices) and the devic
 
 Not built here: statics (calcStatics needs member inertia and
 hydrostatics -- supply them with setStatics()), MoorPy mooring, rotor aerodynamics
-(CCBlade), BEM (pyHAMS) and QTF file I/O.
+(CCBlade), BEM (pyHAMS) and reading external QTF files (potSecOrder=2).
 """
+import os
 import ctypes
 
 import numpy as np
@@ -93,6 +94,7 @@ class FOWT:
         for k in ("M_struc", "B_struc", "C_struc", "C_hydro"):
             setattr(self, k, np.zeros([6, 6]))   # filled by calcStatics
         self._dd = None            # DeviceDesign (built lazily, invalidated on setPosition)
+        self._qtf_devs = {}        # QtfDevice per heading (same lifetime as _dd)
         self.nWaves = 1
 
     # ------------------------------------------------------------------ set-up
@@ -103,6 +105,7 @@ class FOWT:
         for mem in self.memberList:
             mem.setPosition(r6=self.r6)
         self._dd = None
+        self._qtf_devs = {}
 
     def setStatics(self, statics):
         """Provide the outputs of calcStatics (M_struc, B_struc, C_struc, C_hydro, ...) and
@@ -145,6 +148,7 @@ class FOWT:
             self.A_hydro_morison += mem.calcHydroConstants(r_ref=self.r6[:3], rho=self.rho_water, g=self.g,
                                                            k_array=k_array)
         self._dd = None
+        self._qtf_devs = {}
 
     def device_design(self):
         """The DeviceDesign of the current pose and coefficients (built on first use)."""
@@ -193,6 +197,7 @@ class FOWT:
         hidx = torch.tensor(heads, dtype=torch.long, device=dev)
         F = dd.finer.index_select(0, hidx) * zeta[:, None, :]
         self._zeta_dev = zeta
+        self._S_dev = S
         self._heads = heads
         self.S = S.cpu().numpy()
         self.zeta = zeta.cpu().numpy().astype(complex)
@@ -263,6 +268,81 @@ class FOWT:
                 "rh_drag_excitation")
         self.F_hydro_drag = F.cpu().numpy()
         return self.F_hydro_drag
+
+    # ------------------------------------------------------------------ second order
+    def _qtf_device(self, beta):
+        from .qtf import QtfDevice
+        key = (float(beta), np.asarray(self.w1_2nd, dtype=float).tobytes(), np.asarray(self.k1_2nd, dtype=float).tobytes())
+        if key not in self._qtf_devs:
+            self._qtf_devs[key] = QtfDevice(self, self.w1_2nd, self.k1_2nd, float(beta), self.device_index)
+        return self._qtf_devs[key]
+
+    def calcQTF_slenderBody(self, waveHeadInd, Xi0=None, verbose=False, iCase=None, iWT=None):
+        """Slender-body QTF of the body for heading self.beta[waveHeadInd]
+        (raft/raft_fowt.py:1385-1645) computed by rh_qtf_slender.  Xi0: motion RAOs [6, nw]
+        (numpy or device tensor; None = fixed body).  Sets self.qtf [n2, n2, 1, 6] and
+        self.heads_2nd; with outFolderQTF and verbose, writes the .4 / .12d files."""
+        import torch
+        if getattr(self, "w1_2nd", None) is None:
+            raise RuntimeError("calcQTF_slenderBody needs potSecOrder=1 (min_freq2nd/max_freq2nd)")
+        dd = self.device_design()
+        beta = float(self.beta[waveHeadInd])
+        self.heads_2nd = [beta]
+        qd = self._qtf_device(beta)
+        if Xi0 is None:
+            X = torch.zeros([6, self.nw], dtype=torch.complex128, device=dd.device)
+        elif isinstance(Xi0, torch.Tensor):
+            X = Xi0.to(device=dd.device, dtype=torch.complex128).contiguous()
+        else:
+            X = torch.tensor(np.asarray(Xi0, dtype=complex), dtype=torch.complex128, device=dd.device)
+        M66 = torch.tensor(np.asarray(self.M_struc, dtype=float), dtype=torch.float64, device=dd.device).contiguous()
+        if verbose:
+            print(f" Computing QTF for heading {beta:.2f}")
+        q = qd.qtf(dd.w, X, M66)
+        self._qtf_dev, self._qtf_qd = q, qd
+        self.qtf = q.cpu().numpy()[:, :, None, :]
+        if self.outFolderQTF is not None and verbose:
+            from .qtf_io import write_rao4, qtf_file_names
+            rao_path, qtf_path = qtf_file_names(self.outFolderQTF, beta, iCase, iWT)
+            Xi_2nd = np.array([np.interp(self.w1_2nd, self.w, x, left=0, right=0) for x in X.cpu().numpy()])
+            write_rao4(rao_path, self.w1_2nd, beta, Xi_2nd)
+            self.writeQTF(self.qtf, qtf_path)
+
+    def writeQTF(self, qtfIn, outPath, w=None):
+        """WAMIT .12d writer (raft/raft_fowt.py:1700-1726)."""
+        from .qtf_io import write_qtf12d
+        w1 = self.w1_2nd if w is None else w
+        write_qtf12d(outPath, qtfIn, w1, self.heads_2nd, self.rho_water, self.g)
+
+    def calcHydroForce_2ndOrd(self, beta, S0, iCase=None, iWT=None, interpMode="qtf"):
+        """Difference-frequency force amplitudes and mean drift from the QTF
+        (raft/raft_fowt.py:1728-1818, interpMode 'qtf') on the device.  Returns
+        (f_mean [6], f [6, nw]) like the reference."""
+        import torch
+        if interpMode != "qtf":
+            raise NotImplementedError("calcHydroForce_2ndOrd: only interpMode='qtf' (the reference default) is "
+                                      "accelerated")
+        h2 = getattr(self, "heads_2nd", None)
+        if h2 is None or getattr(self, "_qtf_dev", None) is None:
+            raise RuntimeError("calcHydroForce_2ndOrd needs a QTF (call calcQTF_slenderBody first)")
+        if beta < h2[0]:
+            print(f"Warning in calcHydroForce_2ndOrd: angle {beta} is less than the minimum incidence angle in the "
+                  f"QTF. An incidence of {h2[0]} will be considered for 2nd order loads.")
+        if beta > h2[-1]:
+            print(f"Warning in calcHydroForce_2ndOrd: angle {beta} is more than the maximum incidence angle in the "
+                  f"QTF. An incidence of {h2[-1]} will be considered for 2nd order loads.")
+        from .qtf import force_2nd
+        dd = self.device_design()
+        qd = self._qtf_qd
+        S = S0 if isinstance(S0, torch.Tensor) else torch.tensor(np.asarray(S0, dtype=float), dtype=torch.float64,
+                                                                  device=dd.device)
+        fm, f = force_2nd(qd, self._qtf_dev, dd.w, self.dw, S.to(dd.device).contiguous())
+        self._f2nd_dev = f
+        f_mean, f_h = fm.cpu().numpy(), f.cpu().numpy()
+        if self.outFolderQTF is not None:
+            from .qtf_io import write_f2nd
+            write_f2nd(os.path.join(self.outFolderQTF, f"f_2nd-_Case{iCase + 1}_WT{iWT}.txt"), self.w, f_h)
+        return f_mean, f_h
 
     # ------------------------------------------------------------------ outputs
     def saveTurbineOutputs(self, results, case):

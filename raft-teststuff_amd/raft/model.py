@@ -74,29 +74,41 @@ class Model:
     # --------------------------------------------------------------------- dynamics
     def solveDynamics(self, case, tol=0.01, conv_plot=0, RAO_plot=0, display=0):
         """raft/raft_model.py:852-1146 on the device.  Returns Xi [nWaves+1, 6N, nw] and sets
-        fowt.Xi, fowt.Z, fowt.B_hydro_drag, fowt.F_hydro_drag, member Bmat like the reference."""
+        fowt.Xi, fowt.Z, fowt.B_hydro_drag, fowt.F_hydro_drag, member Bmat like the reference.
+        potSecOrder=1 FOWTs follow :966-989: first convergence -> RAO -> slender-body QTF ->
+        second-order force -> a second drag pass from iteration 1 with the un-relaxed XiLast."""
         import torch
-        nloop = int(self.nIter) + 1
+        iCase = case.get("iCase") if isinstance(case, dict) else None
         Zs, Fws = [], []
         for i, fowt in enumerate(self.fowtList):
             fowt.calcHydroExcitation(case, memberList=fowt.memberList)
-            if fowt.potSecOrder == 1:
-                raise NotImplementedError("potSecOrder=1 inside solveDynamics is not wired to the device QTF yet")
             dd = fowt.device_design()
+            dev = dd.device
+            nW = fowt.nWaves
+            fowt.Fhydro_2nd = np.zeros([nW, 6, self.nw], dtype=complex)
+            fowt.Fhydro_2nd_mean = np.zeros([nW, 6])
+            fowt._f2nd_w = [None] * nW
             cs = CaseSet([0], [case["wave_heading"][0]], [N.SPECTRUM_CODES[case["wave_spectrum"][0]]],
                          [case["wave_height"][0]], [case["wave_period"][0]], [case["wave_gamma"][0]])
             if display > 0:
                 print("Solving for system response to wave excitation in primary wave direction")
-            res = solve_batch([dd], cs, self.nIter, self.XiStart, tol,
-                              want=("zeta", "B_drag", "Bmat", "Z"))
-            iters = int(res["iters"].item())
-            status = int(res["status"].item())
-            if status == N.RH_CASE_NAN:
-                raise Exception("Nan detected in response vector Xi.")
-            if status == N.RH_CASE_SINGULAR:
-                raise np.linalg.LinAlgError("Singular matrix")
-            if display > 1 and status == N.RH_CASE_CONVERGED:
-                print(f" Iteration {iters - 1}, converged (< {tol})")
+            second = fowt.potSecOrder == 1
+            want = ("zeta", "B_drag", "Bmat", "Z") + (("rao", "Xi_prev") if second else ())
+            res = solve_batch([dd], cs, self.nIter, self.XiStart, tol, want=want)
+            status, iters = self._check_pass(res, tol, display)
+            fowt.iterations_pair = [iters]
+            if second and status == N.RH_CASE_CONVERGED:
+                if display > 1:
+                    print("Resolving for system response in primary wave direction, now with second-order wave loads.")
+                fowt.calcQTF_slenderBody(waveHeadInd=0, Xi0=res["rao"][0], verbose=True, iCase=iCase, iWT=i)
+                fm, f = fowt.calcHydroForce_2ndOrd(fowt.beta[0], fowt._S_dev[0], iCase=iCase, iWT=i)
+                fowt.Fhydro_2nd_mean[0], fowt.Fhydro_2nd[0] = fm, f
+                fext = fowt._f2nd_dev.to(torch.complex128)[None].contiguous()
+                fowt._f2nd_w[0] = fext[0]
+                res = solve_batch([dd], cs, self.nIter, self.XiStart, tol, want=("zeta", "B_drag", "Bmat", "Z"),
+                                  fext=fext, Xi_init=res["Xi_prev"].contiguous(), first_iter=1)
+                status, iters = self._check_pass(res, tol, display)
+                fowt.iterations_pair.append(iters)
             if status != N.RH_CASE_CONVERGED and display > 0:
                 print("WARNING - solveDynamics iteration did not converge to the tolerance.")
             fowt.iterations, fowt.converged = iters, status == N.RH_CASE_CONVERGED
@@ -108,21 +120,35 @@ class Model:
             Zs.append(Z)
             # excitation of every sea state with the final linearisation (:1049-1061)
             Fw = []
-            for ih in range(fowt.nWaves):
-                Fd = torch.tensor(fowt.calcDragExcitation(ih), dtype=torch.complex128, device=dd.device)
-                Fw.append(dd.finer[fowt._heads[ih]] * fowt._zeta_dev[ih][None, :] + Fd)
+            for ih in range(nW):
+                Fd = torch.tensor(fowt.calcDragExcitation(ih), dtype=torch.complex128, device=dev)
+                F = dd.finer[fowt._heads[ih]] * fowt._zeta_dev[ih][None, :] + Fd
+                if fowt._f2nd_w[ih] is not None:
+                    F = F + fowt._f2nd_w[ih]
+                Fw.append(F)
             Fws.append(Fw)
             fowt._res = res
         nW = self.fowtList[-1].nWaves           # the last FOWT's nWaves
-        dd0 = self.fowtList[0].device_design()
-        dev = dd0.device
+        dev = self.fowtList[0].device_design().device
         Xi = torch.zeros([nW + 1, self.nDOF, self.nw], dtype=torch.complex128, device=dev)
-        if self.nFOWT == 1 and self.K_array is None:
-            Xi[0] = self.fowtList[0]._res["Xi"][0]                     # Zinv F_wave(0) == last solve
-            for ih in range(1, nW):
+        single = self.nFOWT == 1 and self.K_array is None
+        for ih in range(nW):
+            if single and ih == 0:
+                Xi[0] = self.fowtList[0]._res["Xi"][0]                 # Zinv F_wave(0) == last solve
+            else:
                 Xi[ih] = self._system_solve(Zs, [Fw[ih] for Fw in Fws])
-        else:
-            for ih in range(nW):
+            # second-order loads of the other sea states (:1067-1083)
+            if ih > 0 and any(f.potSecOrder == 1 for f in self.fowtList):
+                for i, fowt in enumerate(self.fowtList):
+                    if fowt.potSecOrder != 1:
+                        continue
+                    z = fowt._zeta_dev[ih]
+                    x = Xi[ih, 6 * i:6 * i + 6]
+                    rao = torch.where(z.abs() > 1e-6, x / torch.where(z == 0, torch.ones_like(z), z), torch.zeros_like(x))
+                    fowt.calcQTF_slenderBody(waveHeadInd=ih, Xi0=rao, verbose=True, iCase=iCase, iWT=i)
+                    fm, f = fowt.calcHydroForce_2ndOrd(fowt.beta[ih], fowt._S_dev[ih])
+                    fowt.Fhydro_2nd_mean[ih], fowt.Fhydro_2nd[ih] = fm, f
+                    Fws[i][ih] = Fws[i][ih] + fowt._f2nd_dev.to(torch.complex128)
                 Xi[ih] = self._system_solve(Zs, [Fw[ih] for Fw in Fws])
         self.Xi = Xi.cpu().numpy()
         for i, fowt in enumerate(self.fowtList):
@@ -135,6 +161,19 @@ class Model:
             fowt.Xi = self.Xi[:, 6 * i:6 * i + 6, :]
         self.results["response"] = {}
         return self.Xi
+
+    @staticmethod
+    def _check_pass(res, tol, display):
+        """Status handling of one drag fixed point (raft/raft_model.py:954-966)."""
+        iters = int(res["iters"].item())
+        status = int(res["status"].item())
+        if status == N.RH_CASE_NAN:
+            raise Exception("Nan detected in response vector Xi.")
+        if status == N.RH_CASE_SINGULAR:
+            raise np.linalg.LinAlgError("Singular matrix")
+        if display > 1 and status == N.RH_CASE_CONVERGED:
+            print(f" Iteration {iters - 1}, converged (< {tol})")
+        return status, iters
 
     def _system_solve(self, Zs, Fs):
         """Z_sys = blockdiag(Z_i) (+ K_array); Xi = Z_sys^-1 F (raft/raft_model.py:1021-1065)."""

@@ -1,0 +1,174 @@
+"""Device tables for the slender-body QTF.
+
+Per design, per second-order grid and heading: the static node/member/Kim-Yue tables of
+include/rafthip.h (rh_qtf_design).  The only host arithmetic is geometry bookkeeping and
+the Hankel-function table 0.5 (H1_{n-1}(kR) - H1_{n+1}(kR)) that the reference evaluates
+with scipy.special.hankel1 (raft/raft_member.py:1104-1107); every per-pair quantity is
+computed on the device by rh_qtf_slender.
+"""
+import ctypes
+
+import numpy as np
+from scipy.special import hankel1
+
+from . import _native as N
+
+QN_COUNT, QM_COUNT, KR_COUNT = 46, 36, 6
+
+
+def _hank_table(kk, R):
+    """[n2, 12] table D_n(k R), n = 0..11 (orders -1..12 of hankel1)."""
+    x = kk * R
+    H = np.array([hankel1(n, x) for n in range(-1, 13)])      # [14, n2]
+    D = 0.5 * (H[0:12] - H[2:14])                              # D_n = 0.5 (H_{n-1} - H_{n+1})
+    return D.T.copy()
+
+
+def build_tables(fowt, w2, k2, beta):
+    """Static QTF tables of a FOWT for grid (w2, k2) and heading beta [rad]."""
+    rho, g, h = float(fowt.rho_water), float(fowt.g), float(fowt.depth)
+    ncols, mcols, kcols, hank = [], [], [], []
+    qmstart, kstart = [0], [0]
+    for mem in fowt.memberList:
+        if mem.rA[2] > 0 and mem.rB[2] > 0:                     # entirely above water (:1461)
+            continue
+        circ = mem.shape == "circular"
+        p1M, p2M, qM = mem.p1Mat, mem.p2Mat, mem.qMat
+        last_cm = last_ca = None
+        for il in range(mem.ns):
+            r = mem.r[il]
+            if r[2] >= 0:
+                continue
+            Ca_p1, Ca_p2, Ca_End = mem.coef("Ca_p1", il), mem.coef("Ca_p2", il), mem.coef("Ca_End", il)
+            ds, drs, dls = np.atleast_1d(mem.ds[il]), np.atleast_1d(mem.drs[il]), mem.dls[il]
+            v_i = 0.25 * np.pi * ds[0] ** 2 * dls if circ else ds[0] * ds[1] * dls
+            if r[2] + 0.5 * dls > 0:                             # Q12
+                v_i = v_i * (0.5 * dls - r[2]) / dls
+            if circ:
+                ve = np.pi / 12.0 * abs((ds[0] + drs[0]) ** 3 - (ds[0] - drs[0]) ** 3)
+            else:
+                ve = np.pi / 12.0 * ((np.mean(ds + drs)) ** 3 - (np.mean(ds - drs)) ** 3)
+            CmM = (1. + Ca_p1) * p1M + (1. + Ca_p2) * p2M
+            CaM = Ca_p1 * p1M + Ca_p2 * p2M
+            last_cm, last_ca = CmM, CaM
+            ncols.append([*r, *mem.q, v_i, ve, mem.a_i[il], Ca_End, *CmM.ravel(), *CaM.ravel(),
+                          *(p1M + p2M).ravel(), *qM.ravel()])
+        nsub = len(ncols) - qmstart[-1]
+        qmstart.append(len(ncols))
+        wl = mem.r[-1, 2] * mem.r[0, 2] < 0
+        rint = np.zeros(3)
+        awl = 0.0
+        if wl:
+            rint = mem.r[0] + (mem.r[-1] - mem.r[0]) * (0. - mem.r[0, 2]) / (mem.r[-1, 2] - mem.r[0, 2])
+            i_wl = np.where(mem.r[:, 2] < 0)[0][-1]
+            if circ:
+                d_wl = 0.5 * (mem.ds[i_wl] + mem.ds[i_wl + 1]) if i_wl != len(mem.ds) - 1 else mem.ds[i_wl]
+                awl = 0.25 * np.pi * d_wl ** 2
+            else:
+                if i_wl != len(mem.ds) - 1:
+                    d1, d2 = 0.5 * (mem.ds[i_wl, 0] + mem.ds[i_wl + 1, 0]), 0.5 * (mem.ds[i_wl, 1] + mem.ds[i_wl + 1, 1])
+                else:
+                    d1, d2 = mem.ds[i_wl, 0], mem.ds[i_wl, 1]
+                awl = d1 * d2
+        if nsub == 0:
+            last_cm = last_ca = np.zeros([3, 3])
+        # Kim & Yue (raft_member.py:1111-1200)
+        kay = bool(mem.MCF) and (mem.rA[2] * mem.rB[2] < 0)
+        pf = np.zeros(3)
+        rwl = np.zeros(3)
+        if kay:
+            cb, sb = np.cos(beta), np.sin(beta)
+            bv = np.array([cb, sb, 0])
+            pf = np.dot(bv, mem.p1) * mem.p1 + np.dot(bv, mem.p2) * mem.p2
+            pf = pf / np.linalg.norm(pf)
+            rwl = mem.rA + (mem.rB - mem.rA) * (0 - mem.rA[2]) / (mem.rB[2] - mem.rA[2])
+            R = np.interp(0, mem.r[:, 2], 0.5 * np.array(mem.ds))
+            kcols.append([R, 0.0, 0.0, *rwl])
+            hank.append(_hank_table(k2, R))
+            for il in range(mem.ns - 1):
+                z1 = mem.r[il, 2]
+                if z1 > 0:
+                    continue
+                z2 = mem.r[il + 1, 2]
+                z2 = 0 if z2 > 0 else z2
+                R1 = mem.ds[il] / 2
+                if mem.dls[il] == 0:
+                    R1 = mem.ds[il]
+                R2 = mem.ds[il + 1] / 2
+                if mem.dls[il + 1] == 0:
+                    R2 = mem.ds[il]                               # Q9
+                Rm = 0.5 * (R1 + R2)
+                kcols.append([Rm, z1, z2, *(0.5 * (mem.r[il] + mem.r[il + 1]))])
+                hank.append(_hank_table(k2, Rm))
+        kstart.append(len(kcols))
+        mcols.append([1.0 if wl else 0.0, *rint, awl, *last_cm.ravel(), *last_ca.ravel(), *mem.p1, *mem.p2,
+                      1.0 if kay else 0.0, *pf, *rwl])
+    qnode = np.array(ncols, dtype=float).T.copy() if ncols else np.zeros([QN_COUNT, 0])
+    qmemb = np.array(mcols, dtype=float).T.copy() if mcols else np.zeros([QM_COUNT, 0])
+    kray = np.array(kcols, dtype=float).T.copy() if kcols else np.zeros([KR_COUNT, 0])
+    hk = np.array(hank, dtype=complex) if hank else np.zeros([0, len(w2), 12], dtype=complex)
+    assert qnode.shape[0] == QN_COUNT and qmemb.shape[0] == QM_COUNT
+    return dict(qnode=qnode, qmemb=qmemb, kray=kray, hank=hk, qmstart=np.array(qmstart, dtype=np.int32),
+                kstart=np.array(kstart, dtype=np.int32), rho=rho, g=g, h=h)
+
+
+class QtfDevice:
+    """Device copy of the QTF tables + workspace for one (design, grid, heading)."""
+
+    def __init__(self, fowt, w2, k2, beta, device):
+        import torch
+        self.torch = torch
+        self.dev = torch.device("cuda", device)
+        self.dev_index = device
+        t = build_tables(fowt, w2, k2, beta)
+        f64 = dict(dtype=torch.float64, device=self.dev)
+        self.n2 = len(w2)
+        self.beta = float(beta)
+        self.w2 = torch.tensor(np.asarray(w2, dtype=float), **f64)
+        self.k2 = torch.tensor(np.asarray(k2, dtype=float), **f64)
+        self.nq, self.nmq, self.nkr = t["qnode"].shape[1], t["qmemb"].shape[1], t["kray"].shape[1]
+        pad = lambda a, rows: a if a.shape[1] else np.zeros([rows, 1])
+        self.qnode = torch.tensor(pad(t["qnode"], QN_COUNT), **f64).contiguous()
+        self.qmemb = torch.tensor(pad(t["qmemb"], QM_COUNT), **f64).contiguous()
+        self.kray = torch.tensor(pad(t["kray"], KR_COUNT), **f64).contiguous()
+        self.hank = torch.tensor(t["hank"] if len(t["hank"]) else np.zeros([1, self.n2, 12], dtype=complex),
+                                 dtype=torch.complex128, device=self.dev).contiguous()
+        self.qmstart = torch.tensor(t["qmstart"], dtype=torch.int32, device=self.dev)
+        self.kstart = torch.tensor(t["kstart"], dtype=torch.int32, device=self.dev)
+        self.rho, self.g, self.h = t["rho"], t["g"], t["h"]
+        self.struct_ = self.struct()
+        nbytes = N.lib().rh_qtf_workspace_bytes(ctypes.byref(self.struct_))
+        self.work = torch.empty(int(nbytes) // 16 + 1, dtype=torch.complex128, device=self.dev)
+        self.work_bytes = int(self.work.numel() * 16)
+
+    def struct(self):
+        q = N.RhQtfDesign()
+        q.n2, q.nq, q.nmq, q.nkr = self.n2, self.nq, self.nmq, self.nkr
+        q.beta, q.depth, q.rho, q.g = self.beta, self.h, self.rho, self.g
+        q.w2, q.k2 = N.ptr(self.w2), N.ptr(self.k2)
+        q.qnode, q.qmemb, q.qmstart, q.kstart = N.ptr(self.qnode), N.ptr(self.qmemb), N.ptr(self.qmstart), N.ptr(self.kstart)
+        q.kray, q.hank = N.ptr(self.kray), N.ptr(self.hank)
+        return q
+
+    def qtf(self, w, Xi0, M66, out=None):
+        """Run rh_qtf_slender: w [nw] / Xi0 [6, nw] device tensors -> qtf [n2, n2, 6] device tensor."""
+        torch = self.torch
+        if out is None:
+            out = torch.empty([self.n2, self.n2, 6], dtype=torch.complex128, device=self.dev)
+        N.check(N.lib().rh_qtf_slender(N.context(self.dev_index), ctypes.byref(self.struct_), int(w.numel()), N.ptr(w),
+                                       N.ptr(Xi0), N.ptr(M66), N.ptr(out), N.ptr(self.work),
+                                       ctypes.c_longlong(self.work_bytes), N.stream_handle(torch, self.dev)),
+                "rh_qtf_slender")
+        return out
+
+
+def force_2nd(qdev, qtf, w, dw, S0):
+    """rh_force_2nd: (f_mean [6], f [6, nw]) device tensors."""
+    torch = qdev.torch
+    nw = int(w.numel())
+    f = torch.empty([6, nw], dtype=torch.float64, device=qdev.dev)
+    fm = torch.empty([6], dtype=torch.float64, device=qdev.dev)
+    N.check(N.lib().rh_force_2nd(N.context(qdev.dev_index), qdev.n2, N.ptr(qdev.w2), N.ptr(qtf), nw, N.ptr(w),
+                                 float(dw), N.ptr(S0), N.ptr(f), N.ptr(fm), N.stream_handle(torch, qdev.dev)),
+            "rh_force_2nd")
+    return fm, f

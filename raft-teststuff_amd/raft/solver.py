@@ -45,9 +45,11 @@ class BatchResult(dict):
 
 
 def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std", "zeta", "B_drag"),
-                fext=None, stream=None, prepared=None):
+                fext=None, stream=None, prepared=None, Xi_init=None, first_iter=0):
     """Run rh_solve_cases.  `designs`: list of DeviceDesign (same nw); `cases`: CaseSet.
-    Returns a BatchResult of device tensors (stream-ordered; caller synchronises)."""
+    Returns a BatchResult of device tensors (stream-ordered; caller synchronises).
+    want may include "Xi_prev" (the un-relaxed XiLast of the final iteration); Xi_init /
+    first_iter restart a fixed point from such a state (potSecOrder=1 second pass)."""
     d0 = designs[0]
     torch = d0.torch
     dev = d0.device
@@ -79,6 +81,11 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
         out["rao"] = torch.empty([ncase, 6, nw], **c128)
     if "Z" in want:
         out["Z"] = torch.empty([ncase, nw, 6, 6], **c128)
+    if "Xi_prev" in want:
+        out["Xi_prev"] = torch.empty([ncase, 6, nw], **c128)
+    for t, shape in ((fext, [ncase, 6, nw]), (Xi_init, [ncase, 6, nw])):
+        if t is not None and (list(t.shape) != shape or t.dtype != torch.complex128 or not t.is_contiguous()):
+            raise ValueError(f"expected a contiguous complex128 tensor of shape {shape}")
     cs = N.RhCases()
     cs.ncase = ncase
     cs.design, cs.head, cs.spectrum = N.ptr(prep["design"]), N.ptr(prep["head"]), N.ptr(prep["spectrum"])
@@ -86,15 +93,16 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     cs.nIter, cs.XiStart, cs.tol = int(nIter), float(XiStart), float(tol)
     cs.fext = N.ptr(fext)
     cs.order = N.ptr(prep["order"])
+    cs.Xi_init, cs.first_iter = N.ptr(Xi_init), int(first_iter)
     o = N.RhSolveOut()
     o.Xi, o.Xi_last, o.iters, o.status = N.ptr(out["Xi"]), N.ptr(xl), N.ptr(out["iters"]), N.ptr(out["status"])
-    for k in ["zeta", "B_drag", "Bmat", "psd", "std", "rao", "Z"]:
+    for k in ["zeta", "B_drag", "Bmat", "psd", "std", "rao", "Z", "Xi_prev"]:
         setattr(o, k, N.ptr(out.get(k)))
     arr = (N.RhDesign * len(designs))(*[d.struct() for d in designs])
     s = stream if stream is not None else N.stream_handle(torch, dev)
     N.check(N.lib().rh_solve_cases(N.context(d0.dev_index), arr, len(designs), ctypes.byref(cs), ctypes.byref(o), s),
             "rh_solve_cases")
-    out._keep = (xl, prep, arr)
+    out._keep = (xl, prep, arr, fext, Xi_init)
     return out
 
 

@@ -15,7 +15,7 @@ HEADER = os.path.join(ROOT, "include", "rafthip.h")
 def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(rh_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|long long|const char\*)\s+(rh_\w+)\s*\(", src, flags=re.M)))
 
 
 @pytest.fixture(scope="module")
@@ -29,7 +29,7 @@ def test_header_declares_the_boundary():
     fns = declared_functions()
     for must in ["rh_ctx_create", "rh_ctx_destroy", "rh_last_error", "rh_wave_tables", "rh_solve_cases",
                  "rh_heading_response", "rh_linearize", "rh_drag_excitation", "rh_sea_state", "rh_motion_stats",
-                 "rh_system_solve", "rh_version"]:
+                 "rh_system_solve", "rh_version", "rh_qtf_workspace_bytes", "rh_qtf_slender", "rh_force_2nd"]:
         assert must in fns
 
 
@@ -74,6 +74,7 @@ def test_struct_layout_matches_header():
     assert fields("rh_design") == [f[0] for f in N.RhDesign._fields_]
     assert fields("rh_cases") == [f[0] for f in N.RhCases._fields_]
     assert fields("rh_solve_out") == [f[0] for f in N.RhSolveOut._fields_]
+    assert fields("rh_qtf_design") == [f[0] for f in N.RhQtfDesign._fields_]
 
 
 def test_product_fails_loudly_without_gpu():

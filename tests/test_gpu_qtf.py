@@ -1,0 +1,140 @@
+"""GPU parity of the slender-body QTF path (rh_qtf_slender / rh_force_2nd through the C-ABI)
+against the reference's golden vectors (tests/golden/c3_qtf.npz: OC4semi-RAFT_QTF).
+
+Tolerance (north_star): FP64, 1e-9 relative (normwise) and identical drag-iteration
+counts of both passes of the potSecOrder=1 solve.  Full size (n2 = 400, 80,200 pairs):
+the 24-frequency subset the reference evaluated must equal the matching rows/columns of
+the full 400x400 device QTF (per-frequency tables depend on the frequency only)."""
+import json
+
+import numpy as np
+import pytest
+
+from conftest import load_design, load_golden, statics_of
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-9
+
+
+def rel(a, b):
+    return np.linalg.norm(a - b) / np.linalg.norm(b)
+
+
+@pytest.fixture(scope="module")
+def T():
+    return load_golden("c3_qtf")
+
+
+def _case(T):
+    c = {k: v[0] for k, v in json.loads(str(T["cases_json"]))[0].items()}
+    c["wind_speed"] = 0
+    return c
+
+
+def make(T, out_folder=None):
+    import raft
+    d = load_design("OC4semi-RAFT_QTF")
+    d["platform"]["outFolderQTF"] = out_folder
+    m = raft.Model(d, statics=[statics_of(T)])
+    f = m.fowtList[0]
+    f.setPosition(T["r6"])
+    f.calcStatics()
+    f.calcHydroConstants()
+    return m, f
+
+
+def test_second_order_grid_matches_reference(T):
+    m, f = make(T)
+    np.testing.assert_array_equal(f.w1_2nd, T["w1_2nd"])
+    np.testing.assert_array_equal(f.k1_2nd, T["k1_2nd"])
+
+
+def test_qtf_matches_reference(T):
+    m, f = make(T)
+    f.calcHydroExcitation(_case(T), memberList=f.memberList)
+    f.calcQTF_slenderBody(0, Xi0=T["out_Xi0"])
+    ref = T["out_qtf"]
+    assert f.qtf.shape == ref.shape
+    assert rel(f.qtf, ref) < RTOL, rel(f.qtf, ref)
+    np.testing.assert_allclose(f.qtf, ref, rtol=RTOL, atol=RTOL * np.abs(ref).max())
+    fm, fd = f.calcHydroForce_2ndOrd(f.beta[0], T["out_S"][0])
+    np.testing.assert_allclose(fm, T["out_Fhydro_2nd_mean"][0], rtol=RTOL, atol=RTOL * np.abs(fm).max())
+    assert rel(fd, T["out_Fhydro_2nd"][0].real) < RTOL
+    assert np.all(fd[:, -1] == 0)
+
+
+@pytest.mark.parametrize("key", ["sub400_qtf", "sub400_beta30_qtf"])
+def test_qtf_fine_grid_subset(T, key):
+    m, f = make(T)
+    f.calcHydroExcitation(_case(T), memberList=f.memberList)
+    f.w1_2nd, f.k1_2nd = T["sub400_w"], T["sub400_k"]
+    f.w2_2nd, f.k2_2nd = f.w1_2nd.copy(), f.k1_2nd.copy()
+    if key == "sub400_beta30_qtf":
+        f.beta = np.array([float(T["sub400_beta30"])])
+    f.calcQTF_slenderBody(0, Xi0=T["out_Xi0"])
+    assert rel(f.qtf, T[key]) < RTOL, rel(f.qtf, T[key])
+
+
+def test_qtf_full_size_400_grid(T):
+    """C3 at full size: 400 frequencies (80,200 pairs).  The reference's 24-frequency subset
+    is a principal submatrix of the full QTF; the full matrix is Hermitian-filled."""
+    m, f = make(T)
+    f.calcHydroExcitation(_case(T), memberList=f.memberList)
+    from raft.hydro_math import wave_numbers
+    w400 = np.arange(0.04, 0.35 + 0.5 * 0.04, 0.000825) * 2 * np.pi
+    assert len(w400) == int(T["sub400_n2"])
+    f.w1_2nd, f.k1_2nd = w400, wave_numbers(w400, f.depth)
+    np.testing.assert_array_equal(f.k1_2nd[T["sub400_idx"]], T["sub400_k"])
+    f.calcQTF_slenderBody(0, Xi0=T["out_Xi0"])
+    idx = T["sub400_idx"]
+    sub = f.qtf[np.ix_(idx, idx)]
+    assert rel(sub, T["sub400_qtf"]) < RTOL
+    q = f.qtf[:, :, 0, :]
+    i, j = np.tril_indices(len(w400), -1)
+    np.testing.assert_array_equal(q[i, j], np.conj(q[j, i]))
+    # deterministic
+    q1 = f.qtf.copy()
+    f.calcQTF_slenderBody(0, Xi0=T["out_Xi0"])
+    np.testing.assert_array_equal(f.qtf, q1)
+
+
+def test_fixed_body_qtf_matches_oracle(T):
+    """Xi0=None (fixed body) against the oracle at the n2=42 grid."""
+    from oracle import qtf_oracle as Q
+    m, f = make(T)
+    f.calcHydroExcitation(_case(T), memberList=f.memberList)
+    f.calcQTF_slenderBody(0)
+    ref = Q.qtf_slender(T, np.zeros([6, len(T["w"])], dtype=complex), T["w1_2nd"], T["k1_2nd"], 0.0)
+    assert rel(f.qtf, ref) < RTOL
+
+
+def test_second_order_solve_matches_reference(T):
+    """potSecOrder=1 through Model.solveDynamics (raft/raft_model.py:966-989)."""
+    m, f = make(T)
+    Xi = m.solveDynamics(_case(T))
+    assert f.iterations_pair == list(T["out_iters_pair"]), (f.iterations_pair, T["out_iters_pair"])
+    assert rel(Xi, T["out_Xi"]) < RTOL, rel(Xi, T["out_Xi"])
+    assert rel(f.qtf, T["out_qtf"]) < RTOL
+    assert rel(f.Fhydro_2nd, T["out_Fhydro_2nd"]) < RTOL
+    np.testing.assert_allclose(f.Fhydro_2nd_mean, T["out_Fhydro_2nd_mean"], rtol=RTOL,
+                               atol=RTOL * np.abs(T["out_Fhydro_2nd_mean"]).max())
+    assert rel(f.B_hydro_drag, T["out_B_drag"]) < RTOL
+
+
+def test_qtf_text_outputs(T, tmp_path):
+    """.4 / .12d / f_2nd files (raft/raft_fowt.py:1416-1432, 1700-1726, 1810-1814)."""
+    m, f = make(T, out_folder=str(tmp_path))
+    f.calcHydroExcitation(_case(T), memberList=f.memberList)
+    f.calcQTF_slenderBody(0, Xi0=T["out_Xi0"], verbose=True, iCase=0, iWT=0)
+    n2 = len(T["w1_2nd"])
+    q12 = np.loadtxt(tmp_path / "qtf-slender_body-total_Head0p00_Case1_WT0.12d")
+    assert q12.shape == (6 * n2 * (n2 + 1) // 2, 9)
+    iu, ju = np.triu_indices(n2)
+    ref = T["out_qtf"][iu, ju, 0, 0] / (1025.0 * 9.81)
+    np.testing.assert_allclose(q12[:len(iu), 7], ref.real, rtol=1e-3, atol=1e-4 * np.abs(ref).max())
+    np.testing.assert_allclose(q12[:len(iu), 0], 2 * np.pi / T["w1_2nd"][iu], rtol=1e-4)
+    r4 = np.loadtxt(tmp_path / "raos-slender_body_Head0p00_Case1_WT0.4")
+    assert r4.shape == (6 * n2, 7)
+    f.calcHydroForce_2ndOrd(f.beta[0], T["out_S"][0], iCase=0, iWT=0)
+    f2 = np.loadtxt(tmp_path / "f_2nd-_Case1_WT0.txt")
+    assert f2.shape == (len(T["w"]), 7)
