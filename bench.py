@@ -73,6 +73,106 @@ def cpu_baseline(T, seconds=20.0):
                       f"{dt:.1f} s on 1 core, OPENBLAS_NUM_THREADS=1"}
 
 
+def qtf_flops_per_pair(nsub, nkay, nwl):
+    """SURVEY.md §8(d) fixed formula: F_pair = 1700 Nsub + 900 N_KAYint + 800 N_wl + 200."""
+    return 1700 * nsub + 900 * nkay + 800 * nwl + 200
+
+
+W400 = (0.04, 0.35, 0.000825)      # C3 second-order grid [Hz]: 400 frequencies, 80,200 pairs
+
+
+def build_qtf(device):
+    """C3: OC4semi-RAFT_QTF slender-body QTF on the 400-frequency grid, RAO Xi0 of the
+    reference's first convergence (tests/golden/c3_qtf.npz)."""
+    import raft
+    import torch
+    from raft.hydro_math import wave_numbers
+    from raft.qtf import QtfDevice
+    T = dict(np.load(os.path.join(ROOT, "tests", "golden", "c3_qtf.npz")))
+    with open(os.path.join(ROOT, "tests", "golden", "designs", "OC4semi-RAFT_QTF.json")) as fh:
+        design = json.load(fh)
+    design["platform"]["outFolderQTF"] = None
+    statics = {k: T[k] for k in ["M_struc", "B_struc", "C_struc", "C_hydro", "C_moor"]}
+    m = raft.Model(design, statics=[statics], device=device)
+    f = m.fowtList[0]
+    f.setPosition(T["r6"])
+    f.calcStatics()
+    f.calcHydroConstants()
+    w2 = np.arange(W400[0], W400[1] + 0.5 * W400[0], W400[2]) * 2 * np.pi
+    k2 = wave_numbers(w2, f.depth)
+    qd = QtfDevice(f, w2, k2, 0.0, device)
+    dd = f.device_design()
+    X = torch.tensor(T["out_Xi0"], dtype=torch.complex128, device=dd.device)
+    M66 = torch.tensor(f.M_struc, dtype=torch.float64, device=dd.device).contiguous()
+    qm = qd.host["qmemb"]
+    nkay = qd.nkr - int((qm[29] != 0).sum()) if qd.nmq else 0     # KAY rows minus one waterline row per member
+    nwl = int((qm[0] != 0).sum()) if qd.nmq else 0
+    return T, f, qd, dd, X, M66, w2, k2, nkay, nwl
+
+
+def qtf_cpu_baseline(T, w2, k2, seconds=15.0):
+    """oracle/qtf_oracle.py (vectorised over pairs) on ONE host core: QTFs of growing
+    frequency subsets of the 400 grid until ~`seconds` have passed."""
+    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+    sys.path.insert(0, ROOT)
+    from oracle import qtf_oracle as Q
+    rng = np.random.default_rng(7)
+    pairs, t0 = 0, time.perf_counter()
+    n = 24
+    while time.perf_counter() - t0 < seconds:
+        sel = np.sort(rng.choice(len(w2), n, replace=False))
+        Q.qtf_slender(T, T["out_Xi0"], w2[sel], k2[sel], 0.0)
+        pairs += n * (n + 1) // 2
+    dt = time.perf_counter() - t0
+    return {"value": pairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"{pairs} pairs (24-frequency subsets of the C3 400 grid) through oracle/qtf_oracle.py, "
+                      f"{dt:.1f} s on 1 core; the reference itself takes 19-23 ms/pair/core (SURVEY.md §8(d))"}
+
+
+def bench_qtf(device, steps, warmup, world, rank, dist, cpu):
+    import torch
+    T, f, qd, dd, X, M66, w2, k2, nkay, nwl = build_qtf(device)
+    n2 = len(w2)
+    npair = n2 * (n2 + 1) // 2
+    for _ in range(warmup):
+        q = qd.qtf(dd.w, X, M66)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        q = qd.qtf(dd.w, X, M66)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{device}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt_max = float(t.item())
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    fpp = qtf_flops_per_pair(qd.nq, nkay, nwl)
+    achieved = fpp * npair / (ms * 1e-3) / world
+    out = {"metric": "QTF pairs/sec", "value": npair * steps / dt_max, "unit": "pairs/s", "steps": steps,
+           "ms_per_qtf": dt_max / steps * 1e3, "scaling": "strong", "n2": n2, "pairs_per_qtf": npair,
+           "full_grid_equiv_per_s": n2 * n2 * steps / dt_max,
+           "config": {"workload": "C3: OC4semi-RAFT_QTF slender-body QTF, 400x400 (w1,w2) grid, heading 0",
+                      "submerged_nodes": qd.nq, "kay_intervals": nkay, "waterline_members": nwl,
+                      "parallelism": f"row-sharded x{world} + all-reduce"},
+           "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
+                        "frac": achieved / PEAK_FP64, "traffic": None, "kernel": "rh_qtf_slender (all launches)",
+                        "kernel_ms": ms, "flops_per_pair": fpp,
+                        "note": "FP64 VALU; algorithmic FLOPs from SURVEY.md §8(d); per-GPU rate"}}
+    if cpu:
+        out["cpu_baseline"] = qtf_cpu_baseline(T, w2, k2)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -80,6 +180,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--ncase", type=int, default=NCASE)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-qtf", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -161,6 +262,9 @@ def main():
         "iterations_mean": float(iters.mean()),
         "converged_frac": float((status == 1).mean()),
     }
+    if not args.no_qtf:
+        line["qtf"] = bench_qtf(device, max(3, args.steps // 4), 1, world, rank, dist,
+                                cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(T)
     if rank == 0:

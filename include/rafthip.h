@@ -269,6 +269,18 @@ long long rh_qtf_workspace_bytes(const rh_qtf_design* q);
 int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
                    const double* M66, rh_c128* qtf, void* work, long long work_bytes, rh_stream stream);
 
+/* The upper-triangle rows (w1 <= w2) of one rank of a QTF sharded over nrank devices, no
+   Hermitian fill.  Rows are dealt in snake order: round k gives rank r the row
+   k nrank + (k even ? r : nrank-1-r), which balances the triangle's pairs.  Entries of other
+   rows are not written (the caller zeroes qtf, sums the shards -- an all-reduce over
+   xGMI -- and then calls rh_qtf_hermitian_fill). */
+int rh_qtf_slender_rows(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
+                        const double* M66, int rank, int nrank, rh_c128* qtf, void* work, long long work_bytes,
+                        rh_stream stream);
+
+/* qtf[i2][i1] = conj(qtf[i1][i2]) for i2 > i1 (raft/raft_fowt.py:1639-1640). */
+int rh_qtf_hermitian_fill(rh_ctx* ctx, int n2, rh_c128* qtf, rh_stream stream);
+
 /* Second-order force spectrum, 'qtf' interpolation mode (raft/raft_fowt.py:1788-1810):
  * qtf [n2][n2][6] on grid w2 [n2] (uniform spacing), spectrum S0 [nw] on grid w [nw]
  * (uniform spacing dw) -> f [6][nw] (already shifted by one bin), f_mean [6]. */

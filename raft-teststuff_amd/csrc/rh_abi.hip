@@ -265,15 +265,17 @@ long long rh_qtf_workspace_bytes(const rh_qtf_design* q) {
   return (long long)(rh::qtf_work_elems(*q) * sizeof(rh_c128));
 }
 
-int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0, const double* M66,
-                   rh_c128* qtf, void* work, long long work_bytes, rh_stream stream) {
-  if (!ctx || !q || !w || !Xi0 || !M66 || !qtf || !work) return fail(RH_EINVAL, "rh_qtf_slender: null argument");
+static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
+                      const double* M66, int rank, int nrank, int mirror, rh_c128* qtf, void* work,
+                      long long work_bytes, rh_stream stream, const char* who) {
+  if (!ctx || !q || !w || !Xi0 || !M66 || !qtf || !work) return fail(RH_EINVAL, "%s: null argument", who);
   if (q->n2 < 1 || q->nq < 0 || q->nmq < 0 || q->nkr < 0 || nw < 2)
-    return fail(RH_EINVAL, "rh_qtf_slender: bad sizes n2=%d nq=%d nmq=%d nkr=%d nw=%d", q->n2, q->nq, q->nmq, q->nkr, nw);
+    return fail(RH_EINVAL, "%s: bad sizes n2=%d nq=%d nmq=%d nkr=%d nw=%d", who, q->n2, q->nq, q->nmq, q->nkr, nw);
+  if (nrank < 1 || rank < 0 || rank >= nrank) return fail(RH_EINVAL, "%s: rank %d of %d", who, rank, nrank);
   if (!q->w2 || !q->k2 || (q->nq > 0 && !q->qnode) || (q->nmq > 0 && (!q->qmemb || !q->qmstart || !q->kstart)) ||
       (q->nkr > 0 && (!q->kray || !q->hank)))
-    return fail(RH_EINVAL, "rh_qtf_slender: null table");
-  if (work_bytes < rh_qtf_workspace_bytes(q)) return fail(RH_EINVAL, "rh_qtf_slender: workspace too small");
+    return fail(RH_EINVAL, "%s: null table", who);
+  if (work_bytes < rh_qtf_workspace_bytes(q)) return fail(RH_EINVAL, "%s: workspace too small", who);
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   rh::QtfWork wk;
@@ -291,8 +293,31 @@ int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w,
     hipLaunchKernelGGL(rh::k_qtf_wl, dim3(nb, q->nmq), dim3(64), 0, s, *q, wk);
     RH_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL(rh::k_qtf_pairs, dim3((q->n2 + rh::kQtfTile - 1) / rh::kQtfTile, q->n2), dim3(rh::kQtfTile), 0, s,
-                     *q, wk, qtf);
+  const int rows = (q->n2 + nrank - 1) / nrank;     // snake rounds (k_qtf_pairs skips i1 >= n2)
+  if (rows > 0) {
+    hipLaunchKernelGGL(rh::k_qtf_pairs, dim3((q->n2 + rh::kQtfTile - 1) / rh::kQtfTile, rows), dim3(rh::kQtfTile), 0,
+                       s, *q, wk, qtf, rank, nrank, mirror);
+    RH_HIP(hipGetLastError());
+  }
+  return RH_OK;
+}
+
+int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0, const double* M66,
+                   rh_c128* qtf, void* work, long long work_bytes, rh_stream stream) {
+  return qtf_launch(ctx, q, nw, w, Xi0, M66, 0, 1, 1, qtf, work, work_bytes, stream, "rh_qtf_slender");
+}
+
+int rh_qtf_slender_rows(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
+                        const double* M66, int rank, int nrank, rh_c128* qtf, void* work, long long work_bytes,
+                        rh_stream stream) {
+  return qtf_launch(ctx, q, nw, w, Xi0, M66, rank, nrank, 0, qtf, work, work_bytes, stream, "rh_qtf_slender_rows");
+}
+
+int rh_qtf_hermitian_fill(rh_ctx* ctx, int n2, rh_c128* qtf, rh_stream stream) {
+  if (!ctx || !qtf || n2 < 1) return fail(RH_EINVAL, "rh_qtf_hermitian_fill: bad argument");
+  RH_HIP(hipSetDevice(ctx->device));
+  const size_t n = (size_t)n2 * n2 * 6;
+  hipLaunchKernelGGL(rh::k_qtf_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n2, qtf);
   RH_HIP(hipGetLastError());
   return RH_OK;
 }

@@ -288,11 +288,17 @@ __device__ __forceinline__ cd kay_omega(const rh_c128* D1, const rh_c128* D2, in
   return sub(cdiv(mk(1, 0), mul(HNm1_ii, HN_jj)), cdiv(mk(1, 0), mul(HN_ii, HNm1_jj)));
 }
 
-__global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf) {
-  const int i1 = blockIdx.y;
+// Row k of this rank is i1 = k nrank + (k even ? rank : nrank-1-rank): a snake deal of the
+// upper-triangle rows (longest first), so every rank gets the same pair count to within one
+// row.  mirror = write the Hermitian lower triangle too (single device); sharded runs
+// mirror after the exchange (k_qtf_fill).
+__global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf,
+                                                        int rank, int nrank, int mirror) {
+  const int kr = (int)blockIdx.y;
+  const int i1 = kr * nrank + ((kr & 1) ? nrank - 1 - rank : rank);
   const int i2 = blockIdx.x * kQtfTile + threadIdx.x;
   const int n2 = q.n2;
-  if (i2 >= n2 || i2 < i1) return;
+  if (i1 >= n2 || i2 >= n2 || i2 < i1) return;
   const double w1 = q.w2[i1], w2 = q.w2[i2], k1 = q.k2[i1], k2 = q.k2[i2];
   if (w2 < w1) return;
   const double h = q.depth, rho = q.rho, g = q.g, beta = q.beta;
@@ -617,7 +623,10 @@ __global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork
   }
   // Hermitian fill (:1639-1640): qtf + conj(qtf).T - diag(conj(diag(qtf)))
   rh_c128* up = qtf + ((size_t)i1 * n2 + i2) * 6;
-  if (i1 == i2) {
+  if (!mirror) {
+#pragma unroll
+    for (int d = 0; d < 6; ++d) st(up + d, Q[d]);
+  } else if (i1 == i2) {
 #pragma unroll
     for (int d = 0; d < 6; ++d) st(up + d, sub(add(Q[d], cconj(Q[d])), cconj(Q[d])));
   } else {
@@ -628,6 +637,18 @@ __global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork
       st(lo + d, cconj(Q[d]));
     }
   }
+}
+
+// Hermitian fill of a row-sharded QTF after the exchange: lower[i2][i1] = conj(upper[i1][i2]);
+// the diagonal keeps q + conj(q) - conj(q) == q exactly (raft/raft_fowt.py:1639-1640)
+__global__ __launch_bounds__(256) void k_qtf_fill(int n2, rh_c128* __restrict__ qtf) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)n2 * n2 * 6) return;
+  const int d = (int)(t % 6);
+  const size_t p = t / 6;
+  const int i = (int)(p / n2), j = (int)(p % n2);
+  if (i <= j) return;                                  // lower triangle only
+  st(qtf + p * 6 + d, cconj(ld(qtf + ((size_t)j * n2 + i) * 6 + d)));
 }
 
 // ---------------------------------------------------------------------------------------

@@ -121,6 +121,7 @@ class QtfDevice:
         self.dev = torch.device("cuda", device)
         self.dev_index = device
         t = build_tables(fowt, w2, k2, beta)
+        self.host = t
         f64 = dict(dtype=torch.float64, device=self.dev)
         self.n2 = len(w2)
         self.beta = float(beta)
@@ -150,15 +151,35 @@ class QtfDevice:
         q.kray, q.hank = N.ptr(self.kray), N.ptr(self.hank)
         return q
 
-    def qtf(self, w, Xi0, M66, out=None):
-        """Run rh_qtf_slender: w [nw] / Xi0 [6, nw] device tensors -> qtf [n2, n2, 6] device tensor."""
+    def qtf(self, w, Xi0, M66, out=None, group=None):
+        """Run rh_qtf_slender: w [nw] / Xi0 [6, nw] device tensors -> qtf [n2, n2, 6] device tensor.
+        With an initialised process group of world > 1 the pairs are row-sharded over the
+        ranks (raft/parallel.py) and every rank returns the full matrix."""
         torch = self.torch
+        from .parallel import assemble_qtf, world_of
+        if world_of(group)[1] > 1:
+            return assemble_qtf(lambda o, r, n: self.qtf_rows(w, Xi0, M66, o, r, n), self.hermitian_fill, self.n2,
+                                device=self.dev, group=group)
         if out is None:
             out = torch.empty([self.n2, self.n2, 6], dtype=torch.complex128, device=self.dev)
         N.check(N.lib().rh_qtf_slender(N.context(self.dev_index), ctypes.byref(self.struct_), int(w.numel()), N.ptr(w),
                                        N.ptr(Xi0), N.ptr(M66), N.ptr(out), N.ptr(self.work),
                                        ctypes.c_longlong(self.work_bytes), N.stream_handle(torch, self.dev)),
                 "rh_qtf_slender")
+        return out
+
+
+    def qtf_rows(self, w, Xi0, M66, out, rank, nrank):
+        """rh_qtf_slender_rows: upper-triangle rows i1 = rank (mod nrank) into `out`."""
+        N.check(N.lib().rh_qtf_slender_rows(N.context(self.dev_index), ctypes.byref(self.struct_), int(w.numel()),
+                                            N.ptr(w), N.ptr(Xi0), N.ptr(M66), int(rank), int(nrank), N.ptr(out),
+                                            N.ptr(self.work), ctypes.c_longlong(self.work_bytes),
+                                            N.stream_handle(self.torch, self.dev)), "rh_qtf_slender_rows")
+        return out
+
+    def hermitian_fill(self, out):
+        N.check(N.lib().rh_qtf_hermitian_fill(N.context(self.dev_index), self.n2, N.ptr(out),
+                                              N.stream_handle(self.torch, self.dev)), "rh_qtf_hermitian_fill")
         return out
 
 

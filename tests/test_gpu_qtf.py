@@ -138,3 +138,23 @@ def test_qtf_text_outputs(T, tmp_path):
     f.calcHydroForce_2ndOrd(f.beta[0], T["out_S"][0], iCase=0, iWT=0)
     f2 = np.loadtxt(tmp_path / "f_2nd-_Case1_WT0.txt")
     assert f2.shape == (len(T["w"]), 7)
+
+
+def test_row_sharded_qtf_equals_single_device(T):
+    """rh_qtf_slender_rows over 3 simulated ranks + sum + rh_qtf_hermitian_fill reproduces
+    rh_qtf_slender bit for bit (the multi-GPU exchange of raft/parallel.py)."""
+    import torch
+    m, f = make(T)
+    f.calcHydroExcitation(_case(T), memberList=f.memberList)
+    f.calcQTF_slenderBody(0, Xi0=T["out_Xi0"])
+    qd = f._qtf_qd
+    dd = f.device_design()
+    X = torch.tensor(T["out_Xi0"], dtype=torch.complex128, device=dd.device)
+    M66 = torch.tensor(f.M_struc, dtype=torch.float64, device=dd.device).contiguous()
+    acc = torch.zeros([qd.n2, qd.n2, 6], dtype=torch.complex128, device=dd.device)
+    for r in range(3):
+        part = torch.zeros_like(acc)
+        qd.qtf_rows(dd.w, X, M66, part, r, 3)
+        acc += part
+    qd.hermitian_fill(acc)
+    np.testing.assert_array_equal(acc.cpu().numpy(), f.qtf[:, :, 0, :])

@@ -1,0 +1,95 @@
+"""CPU (gloo, world_size 2): the multi-GPU partitioning of raft/parallel.py -- case blocks
+and their final gather, and the row-sharded QTF exchange (all-reduce of disjoint rows +
+Hermitian fill) -- reproduce the single-process results bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import load_golden
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(fn, world=2, *args):
+    port = _port()
+    mp.spawn(_worker, args=(world, port, fn, args), nprocs=world, join=True)
+
+
+def _worker(rank, world, port, fn, args):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fn(rank, world, *args)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_case_shard_partitions_every_case_once():
+    from raft.parallel import case_shard, qtf_pairs_of, qtf_rows
+    for n in [1, 7, 512, 10000]:
+        for world in [1, 2, 3, 8]:
+            blocks = [case_shard(n, r, world) for r in range(world)]
+            assert blocks[0][0] == 0 and blocks[-1][1] == n
+            assert all(blocks[i][1] == blocks[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in blocks]
+            assert max(sizes) - min(sizes) <= 1
+    for n2 in [42, 400]:
+        for world in [1, 2, 8]:
+            rows = np.concatenate([qtf_rows(n2, r, world) for r in range(world)])
+            assert sorted(rows.tolist()) == list(range(n2))
+            pairs = [qtf_pairs_of(n2, r, world) for r in range(world)]
+            assert sum(pairs) == n2 * (n2 + 1) // 2
+            assert max(pairs) - min(pairs) <= n2                 # snake deal: within one row
+
+
+def _gather_check(rank, world):
+    from raft.parallel import case_shard, gather_cases
+    n = 11
+    rng = np.random.default_rng(5)
+    full_x = rng.standard_normal([n, 6, 7]) + 1j * rng.standard_normal([n, 6, 7])
+    full_i = np.arange(n, dtype=np.int32) * 3
+    lo, hi = case_shard(n, rank, world)
+    got = gather_cases({"Xi": torch.tensor(full_x[lo:hi]), "iters": torch.tensor(full_i[lo:hi])}, n)
+    np.testing.assert_array_equal(got["Xi"].numpy(), full_x)
+    np.testing.assert_array_equal(got["iters"].numpy(), full_i)
+
+
+def test_case_gather_world2():
+    _run(_gather_check)
+
+
+def _qtf_check(rank, world):
+    from oracle import qtf_oracle as Q
+    from raft.parallel import assemble_qtf, qtf_rows
+    T = load_golden("c3_qtf")
+    ref = Q.qtf_slender(T, T["out_Xi0"], T["w1_2nd"], T["k1_2nd"], 0.0)[:, :, 0, :]
+    n2 = len(T["w1_2nd"])
+    iu = np.triu(np.ones([n2, n2], dtype=bool))
+
+    def rows(out, r, w):                      # stand-in for rh_qtf_slender_rows: upper rows of rank r
+        for i1 in qtf_rows(n2, r, w):
+            out[i1, i1:] = torch.tensor(ref[i1, i1:])
+
+    def fill(out):                            # same semantics as k_qtf_fill
+        x = out.numpy()
+        i, j = np.nonzero(~iu)
+        x[i, j] = np.conj(x[j, i])
+
+    q = assemble_qtf(rows, fill, n2).numpy()
+    np.testing.assert_array_equal(q, ref)
+
+
+def test_sharded_qtf_exchange_world2():
+    _run(_qtf_check)
