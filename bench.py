@@ -53,24 +53,64 @@ def sea_states(n, seed):
                  wave_heading=float(rng.choice([0, 30, 60, 90])), wave_gamma=0.0) for _ in range(n)]
 
 
-def cpu_baseline(T, seconds=20.0):
-    """Reference-structured NumPy port (oracle, loop flavour) on ONE host core for a bounded
-    sample of the same workload: whole C2 cases, as many as fit in ~`seconds`."""
-    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+def _cpu_worker(job):
+    """One host-core worker of the CPU baseline (spawned before the parent touches the GPU):
+    ("case", seed) -> one C2 case through oracle/raft_oracle.py loop=True;
+    ("qtf", seed, seconds) -> 24-frequency QTF subsets of C3 through oracle/qtf_oracle.py."""
+    os.environ["OPENBLAS_NUM_THREADS"] = os.environ["OMP_NUM_THREADS"] = "1"
     sys.path.insert(0, ROOT)
-    from oracle import raft_oracle as O
-    cases = sea_states(64, 99)
     t0 = time.perf_counter()
-    done = 0
-    for c in cases:
+    if job[0] == "case":
+        from oracle import raft_oracle as O
+        T = dict(np.load(os.path.join(ROOT, "tests", "golden", "c2_nw1000.npz")))
+        c = sea_states(1, job[1])[0]
         O.solve_dynamics(T, dict(c), int(T["nIter"]), float(T["XiStart"]), loop=True)
-        done += 1
-        if time.perf_counter() - t0 > seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "cases/s", "cores": 1, "kind": "port",
-            "sample": f"{done} C2 cases (nw=1000) through oracle/raft_oracle.py loop=True, "
-                      f"{dt:.1f} s on 1 core, OPENBLAS_NUM_THREADS=1"}
+        return 1, time.perf_counter() - t0
+    from oracle import qtf_oracle as Q
+    from raft.hydro_math import wave_numbers
+    T = dict(np.load(os.path.join(ROOT, "tests", "golden", "c3_qtf.npz")))
+    w2 = np.arange(W400[0], W400[1] + 0.5 * W400[0], W400[2]) * 2 * np.pi
+    k2 = wave_numbers(w2, float(T["depth"]))
+    rng = np.random.default_rng(job[1])
+    pairs = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < job[2]:
+        sel = np.sort(rng.choice(len(w2), 24, replace=False))
+        Q.qtf_slender(T, T["out_Xi0"], w2[sel], k2[sel], 0.0)
+        pairs += 24 * 25 // 2
+    return pairs, time.perf_counter() - t0
+
+
+def cpu_baselines(max_procs=16, qtf_seconds=10.0):
+    """CPU baseline on the box's host cores: P = min(affinity, max_procs)
+    single-threaded worker processes.  C2 leg: P whole cases (one per worker, ~20 s wall);
+    QTF leg: every worker computes C3 sub-grid QTFs for `qtf_seconds`.  Wall clock."""
+    import multiprocessing as mp
+    P = max(1, min(len(os.sched_getaffinity(0)), max_procs))
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((l.split(":", 1)[1].strip() for l in fh if l.startswith("model name")), "unknown")
+    except OSError:
+        model = "unknown"
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(P) as pool:
+        t0 = time.perf_counter()
+        res = pool.map(_cpu_worker, [("case", 99 + i) for i in range(P)], chunksize=1)
+        dt = time.perf_counter() - t0
+        per_case = float(np.mean([r[1] for r in res]))
+        t1 = time.perf_counter()
+        qres = pool.map(_cpu_worker, [("qtf", 7 + i, qtf_seconds) for i in range(P)], chunksize=1)
+        dq = time.perf_counter() - t1
+    npairs = sum(r[0] for r in qres)
+    case = {"value": P / dt, "unit": "cases/s", "cores": P, "kind": "port",
+            "sample": f"{P} C2 cases (nw=1000, seeded JONSWAP) through oracle/raft_oracle.py loop=True (the "
+                      f"reference's per-node/per-bin loop structure), one per single-threaded process on {P} "
+                      f"cores, {dt:.1f} s wall, {per_case:.1f} s/case/core; CPU {model}"}
+    qtf = {"value": npairs / dq, "unit": "pairs/s", "cores": P, "kind": "port",
+           "sample": f"{npairs} pairs (24-frequency subsets of the C3 400 grid) through oracle/qtf_oracle.py "
+                     f"(vectorised over pairs, faster per pair than the reference's 19-23 ms) on {P} cores, "
+                     f"{dq:.1f} s wall; CPU {model}"}
+    return case, qtf
 
 
 def qtf_flops_per_pair(nsub, nkay, nwl):
@@ -110,26 +150,7 @@ def build_qtf(device):
     return T, f, qd, dd, X, M66, w2, k2, nkay, nwl
 
 
-def qtf_cpu_baseline(T, w2, k2, seconds=15.0):
-    """oracle/qtf_oracle.py (vectorised over pairs) on ONE host core: QTFs of growing
-    frequency subsets of the 400 grid until ~`seconds` have passed."""
-    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
-    sys.path.insert(0, ROOT)
-    from oracle import qtf_oracle as Q
-    rng = np.random.default_rng(7)
-    pairs, t0 = 0, time.perf_counter()
-    n = 24
-    while time.perf_counter() - t0 < seconds:
-        sel = np.sort(rng.choice(len(w2), n, replace=False))
-        Q.qtf_slender(T, T["out_Xi0"], w2[sel], k2[sel], 0.0)
-        pairs += n * (n + 1) // 2
-    dt = time.perf_counter() - t0
-    return {"value": pairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
-            "sample": f"{pairs} pairs (24-frequency subsets of the C3 400 grid) through oracle/qtf_oracle.py, "
-                      f"{dt:.1f} s on 1 core; the reference itself takes 19-23 ms/pair/core (SURVEY.md §8(d))"}
-
-
-def bench_qtf(device, steps, warmup, world, rank, dist, cpu):
+def bench_qtf(device, steps, warmup, world, rank, dist):
     import torch
     T, f, qd, dd, X, M66, w2, k2, nkay, nwl = build_qtf(device)
     n2 = len(w2)
@@ -168,8 +189,6 @@ def bench_qtf(device, steps, warmup, world, rank, dist, cpu):
                         "frac": achieved / PEAK_FP64, "traffic": None, "kernel": "rh_qtf_slender (all launches)",
                         "kernel_ms": ms, "flops_per_pair": fpp,
                         "note": "FP64 VALU; algorithmic FLOPs from SURVEY.md §8(d); per-GPU rate"}}
-    if cpu:
-        out["cpu_baseline"] = qtf_cpu_baseline(T, w2, k2)
     return out
 
 
@@ -183,11 +202,14 @@ def main():
     ap.add_argument("--no-qtf", action="store_true")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    baselines = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        baselines = cpu_baselines()          # before this process initialises the GPU
+    import torch
+    import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -263,10 +285,11 @@ def main():
         "converged_frac": float((status == 1).mean()),
     }
     if not args.no_qtf:
-        line["qtf"] = bench_qtf(device, max(3, args.steps // 4), 1, world, rank, dist,
-                                cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(T)
+        line["qtf"] = bench_qtf(device, max(3, args.steps // 4), 1, world, rank, dist)
+    if baselines is not None:
+        line["cpu_baseline"] = baselines[0]
+        if "qtf" in line:
+            line["qtf"]["cpu_baseline"] = baselines[1]
     if rank == 0:
         print(json.dumps(line))
     if world > 1:
