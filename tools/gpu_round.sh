@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
-timeout -k 10 900 python -m pytest tests -q -m gpu > $OUT/gpu_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 $OUT/gpu_tests.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 cd /tmp && export TMPDIR=/tmp
