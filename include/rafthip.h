@@ -148,6 +148,12 @@ int rh_ctx_create(int device, rh_ctx** out);
 int rh_ctx_destroy(rh_ctx* ctx);
 int rh_version(void);
 
+/* Kernel selection for rh_solve_cases (process-wide; not part of the reference API):
+ * 0 = automatic (LDS-resident fast path when nw <= 1024 and the node tables fit in LDS,
+ * else the general kernel), 1 = always the general kernel.  Used by the parity tests to
+ * cross-check the two device paths on the same inputs. */
+int rh_set_solver(int which);
+
 /* Unit-amplitude wave kinematics and strip-theory inertial excitation per heading.
  * Replaces the node loops of FOWT.calcHydroExcitation (raft/raft_fowt.py:1098-1124)
  * and helpers.getWaveKin (raft/helpers.py:105-154):

@@ -12,6 +12,7 @@
 
 #include "rh_kernels.hip"   // single translation unit: kernels + their host launchers
 #include "rh_qtf.hip"
+#include "rh_solve.hip"
 
 struct rh_ctx {
   int device = 0;
@@ -23,6 +24,7 @@ struct rh_ctx {
 
 namespace {
 thread_local std::string g_err;
+bool g_force_v2 = false;   // rh_set_solver(1): always use k_solve_cases (parity cross-checks)
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -84,7 +86,24 @@ extern "C" {
 
 const char* rh_last_error(void) { return g_err.c_str(); }
 
-int rh_version(void) { return 1; }
+int rh_version(void) { return 2; }
+
+#ifdef RH_PROF
+extern "C" int rh_prof_read(unsigned long long* out, int reset) {
+  RH_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(rh::rh_prof), sizeof(unsigned long long) * 8));
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    RH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(rh::rh_prof), z, sizeof z));
+  }
+  return RH_OK;
+}
+#endif
+
+int rh_set_solver(int which) {
+  if (which != 0 && which != 1) return fail(RH_EINVAL, "rh_set_solver: which=%d (0 = auto, 1 = general kernel)", which);
+  g_force_v2 = which == 1;
+  return RH_OK;
+}
 
 int rh_ctx_create(int device, rh_ctx** out) {
   if (!out) return fail(RH_EINVAL, "rh_ctx_create: null out");
@@ -158,6 +177,20 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   a.designs = ctx->d_designs;
   a.c = *cases;
   a.o = *out;
+  // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case, nw <= 1024.
+  if (nw <= 2 * rh::kLT && !g_force_v2) {
+    const int nb = nw <= rh::kLT ? 1 : 2;
+    int nmmax = 0;
+    for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
+    const size_t lsm = rh::solve_lds_smem(nnmax, nmmax, nb);
+    if (lsm <= 160 * 1024) {
+      dim3 grid(cases->ncase), block(rh::kLT);
+      if (nb == 1) hipLaunchKernelGGL(rh::k_solve_lds<1>, grid, block, lsm, s, a);
+      else hipLaunchKernelGGL(rh::k_solve_lds<2>, grid, block, lsm, s, a);
+      RH_HIP(hipGetLastError());
+      return RH_OK;
+    }
+  }
   const size_t smem = sizeof(double) * (size_t)((kThreads / 64) * nnmax * 3 + nnmax * 9 + 36 + (kThreads / 64) * 6 + 108 + nnmax * 5);
   dim3 grid(cases->ncase), block(kThreads);
   switch (nb_for(nw)) {

@@ -21,6 +21,12 @@ __device__ __forceinline__ cd ld(const rh_c128* p) {
 __device__ __forceinline__ void st(rh_c128* p, cd v) {
   *reinterpret_cast<double2*>(p) = make_double2(v.r, v.i);
 }
+// non-temporal (streaming) store: write-once data that must not displace cached tables
+__device__ __forceinline__ void st_nt(rh_c128* p, cd v) {
+  double* q = reinterpret_cast<double*>(p);
+  __builtin_nontemporal_store(v.r, q);
+  __builtin_nontemporal_store(v.i, q + 1);
+}
 __device__ __forceinline__ cd add(cd a, cd b) { return cd{a.r + b.r, a.i + b.i}; }
 __device__ __forceinline__ cd sub(cd a, cd b) { return cd{a.r - b.r, a.i - b.i}; }
 __device__ __forceinline__ cd mul(cd a, cd b) { return cd{a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r}; }
@@ -88,6 +94,35 @@ __device__ __forceinline__ bool lu_solve(cd (&A)[N][N], cd (&x)[N]) {
     x[k] = cdiv(s, A[k][k]);
   }
   return ok;
+}
+
+// Raw buffer access: the 128-bit resource lives in SGPRs, each lane supplies one 32-bit byte
+// offset and the per-array / per-component part is a scalar offset.  This keeps the many
+// (array, DOF, bin) addresses of the case solve from being materialised as 64-bit VGPR pairs,
+// and bounds every access by the resource size (out-of-range loads return 0, stores drop).
+struct Buf {
+  __amdgpu_buffer_rsrc_t r;
+};
+__device__ __forceinline__ Buf mkbuf(const void* p, unsigned bytes) {
+  return Buf{__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000)};
+}
+__device__ __forceinline__ cd bld(Buf b, unsigned voff, unsigned soff) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(b.r, voff, soff, 0);
+  const double2 d = __builtin_bit_cast(double2, v);
+  return cd{d.x, d.y};
+}
+__device__ __forceinline__ void bst(Buf b, cd x, unsigned voff, unsigned soff) {
+  const double2 d = make_double2(x.r, x.i);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), b.r, voff,
+                                         soff, 0);
+}
+__device__ __forceinline__ double bld1(Buf b, unsigned voff, unsigned soff) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(b.r, voff, soff, 0);
+  return __builtin_bit_cast(double, v);
+}
+__device__ __forceinline__ void bst1(Buf b, double x, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x), b.r, voff,
+                                        soff, 0);
 }
 
 // full 64-lane butterfly sum (every lane ends with the total)

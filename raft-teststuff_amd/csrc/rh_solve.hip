@@ -1,0 +1,507 @@
+// rh_solve.hip -- k_solve_lds: the per-case drag fixed point with the relaxed iterate in LDS.
+//
+// Same algorithm and arithmetic as k_solve_cases (rh_kernels.hip; raft/raft_model.py:918-1000,
+// raft/raft_fowt.py:1152-1293), re-laid-out for latency on gfx950:
+//   * 512 threads (8 waves) per case, one case per CU; lane = bin, NB <= 2 bins per thread.
+//   * XiLast lives in LDS ([6][512 NB] complex) for the whole solve: the thread that owns a
+//     bin is the only one that reads or writes it, so no global round trip per iteration.
+//     The unrelaxed solution is streamed to HBM with non-temporal stores (it is only
+//     consumed after the loop), so it does not evict the wave tables from L2.
+//   * The projected wave table (kproj, the only per-node stream) is read through a buffer
+//     resource (one 32-bit lane offset per bin, node/projection offsets scalar) with a
+//     3-slot register ring: node n+2 is in flight while node n is reduced.
+//   * Per-node bin sums: a 6-step DPP wave reduction (VALU only, no LDS or SGPR traffic),
+//     one partial per wave, summed in wave order.  Fixed order, so results are deterministic.
+#include "rh_device.h"
+
+namespace rh {
+
+#ifdef RH_PROF
+// Phase cycle counters (s_memtime of wave 0 of every workgroup), summed over workgroups:
+// [0] prologue [1] A [2] B [3] C excitation [4] C solve [5] flags [6] epilogue [7] iterations
+__device__ unsigned long long rh_prof[8];
+#define PROF_T(v) const unsigned long long v = clock64()
+#define PROF_ADD(i, x) if (tid == 0) atomicAdd(&rh_prof[i], (unsigned long long)(x))
+#else
+#define PROF_T(v)
+#define PROF_ADD(i, x)
+#endif
+
+constexpr int kLT = 512;          // threads per case workgroup
+constexpr int kLW = kLT / 64;     // waves per case workgroup
+
+// A scalar zero the compiler cannot fold (see its use in phase C).
+__device__ __forceinline__ int opaque_zero() {
+  int z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return z;
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_mov_rows(double v) {   // rows outside ROWS receive 0
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWS, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Sum over the whole wave, complete in lane 63 only.  Call with every lane active.
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror and row_mirror give every lane
+// its 16-lane row total r_k; row_bcast:15 then adds r0 into row 1 and r2 into row 3, and
+// row_bcast:31 adds row 1 into row 3: lane 63 = (r3 + r2) + (r1 + r0).  VALU only, no
+// LDS or SGPR traffic, fixed order.
+__device__ __forceinline__ double wave_sum63(double v) {
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0x141>(v);
+  v += dpp_mov<0x140>(v);
+  v += dpp_mov_rows<0x142, 0xA>(v);
+  v += dpp_mov_rows<0x143, 0xC>(v);
+  return v;
+}
+
+// Every table the loops read is staged here: a global load inside the node loops would share
+// the vector-memory counter with the prefetched wave-table loads and force them to drain.
+__host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB) {
+  return sizeof(double) * ((size_t)12 * kLT * NB      // XiLast [6][512 NB] complex
+                           + (size_t)nn * 3 * kLW     // per-wave node sums
+                           + (size_t)nn * 36          // per-node B_drag contributions
+                           + (size_t)nn * 9           // Bmat
+                           + (size_t)nn * 5           // member-factored drag coefficients
+                           + (size_t)nn               // node axial coordinate t
+                           + (size_t)nm * 18          // member cq, c1, c2
+                           + (size_t)2 * kLT * NB     // w and zeta per (padded) bin
+                           + 36 + 108 + kLW * 6)      // B_drag, M|B|C image, std partials
+         + sizeof(int) * ((size_t)nm + 2);            // member node ranges
+}
+
+template <int NB>
+__global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  PROF_T(tp0);
+  const int slot = xcd_remap(blockIdx.x, a.c.ncase);
+  const int ic = a.c.order ? a.c.order[slot] : slot;
+  const rh_design& d = a.designs[a.c.design[ic]].d;
+  const int nw = d.nw, nn = d.nn, nm = d.nm;
+  const unsigned nw16 = (unsigned)nw * 16u;
+  const double* __restrict__ node = d.node;
+  const int head = a.c.head[ic];
+  const size_t c6 = (size_t)ic * 6 * nw;
+  const Buf bK = mkbuf(d.kproj + (size_t)head * nn * 3 * nw, (unsigned)nn * 3u * nw16);
+  const Buf bFe = mkbuf(d.finer + (size_t)head * 6 * nw, 6u * nw16);
+  const bool has_fx = a.c.fext != nullptr;
+  const Buf bFx = mkbuf(has_fx ? a.c.fext + c6 : nullptr, has_fx ? 6u * nw16 : 0u);
+
+  constexpr int NWP = kLT * NB;                    // padded bins held in LDS
+  cd* xl = reinterpret_cast<cd*>(smem);            // [6][NWP]
+  double* red = smem + 12 * NWP;                   // [nn*3][kLW]
+  double* bm = red + nn * 3 * kLW;                 // [nn][9]
+  double* al = bm + nn * 9;                        // [nn][5]
+  double* bd = al + nn * 5;                        // [36]
+  double* mbc = bd + 36;                           // [108] M, B_lin, C
+  double* sred = mbc + 108;                        // [kLW][6]
+  double* bdn = sred + kLW * 6;                    // [36][nn]
+  double* nt = bdn + 36 * nn;                      // [nn]
+  double* mbf = nt + nn;                           // [18][nm]
+  double* lw = mbf + 18 * nm;                      // [NWP] w per bin (pad bins: w[nw-1])
+  double* lz = lw + NWP;                           // [NWP] zeta per bin (pad bins: 0)
+  int* mstart = reinterpret_cast<int*>(lz + NWP);  // [nm+1]
+  load_mbc(d, mbc, tid);
+  for (int n = tid; n < nn; n += kLT) nt[n] = node[RH_NF_T * nn + n];
+  for (int e = tid; e < 18 * nm; e += kLT) mbf[e] = d.memb[e];   // RH_MF_CQ0..C20 are fields 0..17
+  for (int e = tid; e <= nm; e += kLT) mstart[e] = d.mstart[e];
+
+  // Per-bin scalars live in LDS, not in registers: nothing per-thread stays live across the
+  // phases, so the register-heavy solve of phase C does not push other values to scratch.
+  // Bin j of this thread is b = tid + 512 j; loads use the clamped bin min(b, nw-1) so no
+  // load is predicated, and pad bins (b >= nw) carry zeta = 0 and XiLast = 0.
+  auto voff = [&](int b) { return (unsigned)(b < nw ? b : nw - 1) * 16u; };
+  {
+    const int spec = a.c.spectrum[ic];
+    const double Hs = a.c.Hs[ic], Tp = a.c.Tp[ic], gam = a.c.gamma[ic];
+    const rh_c128* XI0 = a.c.Xi_init ? a.c.Xi_init + c6 : nullptr;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int b = tid + kLT * j;
+      const bool okb = b < nw;
+      const double w = d.w[okb ? b : nw - 1];
+      const double zz = sea_amplitude(spec, Hs, Tp, gam, w, d.dw);
+      lw[b] = w;
+      lz[b] = okb ? zz : 0.0;
+      if (okb && a.o.zeta) a.o.zeta[(size_t)ic * nw + b] = zz;
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+        xl[c * NWP + b] = okb ? (XI0 ? ld(XI0 + c * nw + b) : mk(a.c.XiStart, 0.0)) : mk(0.0, 0.0);
+    }
+  }
+  rh_c128* Xo = a.o.Xi + c6;
+  rh_c128* XP = a.o.Xi_prev ? a.o.Xi_prev + c6 : nullptr;
+  const double rho = d.rho;
+  const int nloop = a.c.nIter + 1;
+  const double tol = a.c.tol;
+  int status = RH_CASE_NOT_CONVERGED, iters = nloop;
+  __syncthreads();
+  PROF_T(tp1);
+  PROF_ADD(0, tp1 - tp0);
+
+  for (int it = a.c.first_iter; it < nloop; ++it) {
+    PROF_T(ta0);
+    PROF_ADD(7, 1);
+    // ---------------- A: per-node sums of squared relative-velocity components ----------
+    // Member-factored (rh_member_field): per (member, bin)
+    //   Bq = iw cq.Xi, B1 = iw c1.Xi, B2 = iw c2.Xi, E1 = iw p2.th, E2 = -iw p1.th
+    // and per node s_q = z Kq - Bq, s_1 = z K1 - (B1 + t E1), s_2 = z K2 - (B2 + t E2)
+    // (raft/raft_fowt.py:1205-1211).
+    {
+      unsigned vb[NB];
+      double bz[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        vb[j] = voff(tid + kLT * j);
+        bz[j] = lz[tid + kLT * j];
+      }
+      cd Bq[NB], B1[NB], B2[NB], E1[NB], E2[NB];
+      auto member_terms = [&](int m) {
+        double cq[6], c1[6], c2[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          cq[i] = mbf[(RH_MF_CQ0 + i) * nm + m];
+          c1[i] = mbf[(RH_MF_C10 + i) * nm + m];
+          c2[i] = mbf[(RH_MF_C20 + i) * nm + m];
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const int b = tid + kLT * j;
+          cd X[6];
+#pragma unroll
+          for (int c = 0; c < 6; ++c) X[c] = xl[c * NWP + b];
+          cd Aq = mk(0, 0), A1 = mk(0, 0), A2 = mk(0, 0);
+#pragma unroll
+          for (int c = 0; c < 6; ++c) {
+            Aq = add(Aq, scl(X[c], cq[c]));
+            A1 = add(A1, scl(X[c], c1[c]));
+            A2 = add(A2, scl(X[c], c2[c]));
+          }
+          const cd D1 = add(add(scl(X[3], c2[0]), scl(X[4], c2[1])), scl(X[5], c2[2]));   // p2 . th
+          const cd D2 = add(add(scl(X[3], c1[0]), scl(X[4], c1[1])), scl(X[5], c1[2]));   // p1 . th
+          const double w = lw[b];
+          Bq[j] = iw(w, Aq);
+          B1[j] = iw(w, A1);
+          B2[j] = iw(w, A2);
+          E1[j] = iw(w, D1);
+          E2[j] = iw(-w, D2);
+        }
+      };
+      auto load_node = [&](cd (&K)[3][NB], int n) {
+        const unsigned so = (unsigned)(n < nn ? n : nn - 1) * 3u * nw16;
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) K[p][j] = bld(bK, vb[j], so + (unsigned)p * nw16);
+      };
+      auto reduce_node = [&](const cd (&K)[3][NB], int n) {
+        const double t = nt[n];
+        double s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const double z = bz[j];
+          const cd sq = sub(scl(K[0][j], z), Bq[j]);
+          const cd sp1 = sub(scl(K[1][j], z), add(B1[j], scl(E1[j], t)));
+          const cd sp2 = sub(scl(K[2][j], z), add(B2[j], scl(E2[j], t)));
+          s0 += abs2(sq);
+          s1 += abs2(sp1);
+          s2 += abs2(sp2);
+        }
+        s0 = wave_sum63(s0);
+        s1 = wave_sum63(s1);
+        s2 = wave_sum63(s2);
+        if (lane == 63) {
+          double* R = red + (size_t)n * 3 * kLW + wv;
+          R[0] = s0;
+          R[kLW] = s1;
+          R[2 * kLW] = s2;
+        }
+      };
+      cd KA[3][NB], KB[3][NB], KC[3][NB];
+      load_node(KA, 0);
+      load_node(KB, 1);
+      int m = -1, mnext = 0;
+      auto step = [&](cd (&K)[3][NB], int n) {
+        if (n == mnext) {   // uniform: entering member m+1 (members are node-contiguous)
+          do { ++m; mnext = mstart[m + 1]; } while (mnext == n);
+          member_terms(m);
+        }
+        reduce_node(K, n);
+        load_node(K, n + 3);
+      };
+      load_node(KC, 2);
+      for (int n = 0; n < nn; n += 3) {
+        step(KA, n);
+        if (n + 1 < nn) step(KB, n + 1);
+        if (n + 2 < nn) step(KC, n + 2);
+      }
+    }
+    __syncthreads();
+    PROF_T(ta1);
+    PROF_ADD(1, ta1 - ta0);
+    // ---------------- B: node drag matrices and B_drag ----------------------------------
+    for (int n = tid; n < nn; n += kLT) {
+      double r3[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const double* R = red + (size_t)(n * 3 + c) * kLW;
+        double s = 0;
+#pragma unroll
+        for (int w = 0; w < kLW; ++w) s += R[w];
+        r3[c] = s;
+      }
+      // sum|vrel_q|^2 = sum|s_q|^2 |q|^2 ; circular: |vrel_p|^2 = |s_1|^2|p1|^2 + |s_2|^2|p2|^2
+      const double qq = nrm2(node, nn, RH_NF_QX, n), pp1 = nrm2(node, nn, RH_NF_P1X, n), pp2 = nrm2(node, nn, RH_NF_P2X, n);
+      const bool circ = nf(node, nn, RH_NF_CIRC, n) != 0.0;
+      const double sums[3] = {r3[0] * qq, circ ? r3[1] * pp1 + r3[2] * pp2 : r3[1] * pp1, r3[2] * pp2};
+      double B4[4];
+      node_bmat(node, nn, n, rho, sums, bm + 9 * n, B4);
+      const double t = nf(node, nn, RH_NF_T, n);
+      double* A = al + 5 * n;
+      A[0] = B4[0] + B4[3];     // axial: side + end   (qMat terms of Bmat, raft/raft_fowt.py:1228-1248)
+      A[1] = B4[1];
+      A[2] = B4[2];
+      A[3] = t * B4[1];
+      A[4] = t * B4[2];
+      // this node's translateMatrix3to6DOF (raft/helpers.py:455-478), summed below in node order
+      const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
+#pragma unroll
+      for (int e = 0; e < 36; ++e) bdn[e * nn + n] = t3to6(bm + 9 * n, rx, ry, rz, e / 6, e % 6);
+    }
+    __syncthreads();
+    if (tid < 36) {
+      const double* P = bdn + tid * nn;
+      double s = 0;
+      for (int n = 0; n < nn; ++n) s += P[n];
+      bd[tid] = s;
+    }
+    __syncthreads();
+    PROF_T(ta2);
+    PROF_ADD(2, ta2 - ta0 - (ta1 - ta0));
+#ifdef RH_PROF
+    unsigned long long tc_exc = 0, tc_sol = 0;
+#endif
+    // ---------------- C: excitation, Z(w), LU solve, convergence flags ------------------
+    bool my_ok = true, my_nan = false, my_sing = false;
+#pragma unroll 1
+    for (int j = 0; j < NB; ++j) {
+      // per-bin scalars picked without dynamic register indexing (the loop is not unrolled,
+      // so only one bin's LU is ever live)
+      const int bj = tid + kLT * j;
+      const unsigned vj = voff(bj);
+      const bool okj = bj < nw;
+      // drag excitation of bin j before the zeta factor, member-factored:
+      //   f_n = Bmat_n uhat_n = aq q Kq + a1 p1 K1 + a2 p2 K2,  r_n x f_n = rA x f_n + t q x f_n
+      // with q x p1 = p2, q x p2 = -p1 (raft/raft_fowt.py:1255-1259, 1283-1289).
+      PROF_T(tc0);
+      cd fe[6];   // unit inertial excitation of this bin, in flight during the node loop
+#pragma unroll
+      for (int c = 0; c < 6; ++c) fe[c] = bld(bFe, vj, c * nw16);
+      cd F[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
+      {
+        cd SQ = mk(0, 0), S1 = mk(0, 0), S2 = mk(0, 0), T1 = mk(0, 0), T2 = mk(0, 0);
+        auto load1 = [&](cd (&K)[3], int n) {
+          const unsigned so = (unsigned)(n < nn ? n : nn - 1) * 3u * nw16;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) K[p] = bld(bK, vj, so + (unsigned)p * nw16);
+        };
+        int m = 0, mnext = nn > 0 ? mstart[1] : 0;
+        auto fold = [&]() {   // close member m: F += sum of its nodes (as drag_exc_members)
+#pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            const double cq = mbf[(RH_MF_CQ0 + i) * nm + m], c1 = mbf[(RH_MF_C10 + i) * nm + m],
+                         c2 = mbf[(RH_MF_C20 + i) * nm + m];
+            F[i] = add(F[i], add(add(scl(SQ, cq), scl(S1, c1)), scl(S2, c2)));
+          }
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const double p1 = mbf[(RH_MF_C10 + i) * nm + m], p2 = mbf[(RH_MF_C20 + i) * nm + m];
+            F[3 + i] = add(F[3 + i], sub(scl(T1, p2), scl(T2, p1)));
+          }
+          SQ = S1 = S2 = T1 = T2 = mk(0, 0);
+        };
+        auto step = [&](cd (&K)[3], int n) {
+          while (n == mnext) {   // uniform: member m ended before node n
+            fold();
+            ++m;
+            mnext = mstart[m + 1];
+          }
+          const double* A = al + 5 * n;
+          const double A0 = A[0], A1 = A[1], A2 = A[2], A3 = A[3], A4 = A[4];
+          SQ = add(SQ, scl(K[0], A0));
+          S1 = add(S1, scl(K[1], A1));
+          S2 = add(S2, scl(K[2], A2));
+          T1 = add(T1, scl(K[1], A3));
+          T2 = add(T2, scl(K[2], A4));
+          load1(K, n + 3);
+        };
+        cd KA[3], KB[3], KC[3];
+        load1(KA, 0);
+        load1(KB, 1);
+        load1(KC, 2);
+        for (int n = 0; n < nn; n += 3) {
+          step(KA, n);
+          if (n + 1 < nn) step(KB, n + 1);
+          if (n + 2 < nn) step(KC, n + 2);
+        }
+        if (nn > 0) fold();
+      }
+      PROF_T(tc1);
+#ifdef RH_PROF
+      tc_exc += tc1 - tc0;
+#endif
+      if (!okj) continue;
+      const int b = tid + kLT * j;
+      const unsigned v = vj;
+      const double w = lw[b], z = lz[b];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) F[c] = add(scl(fe[c], z), scl(F[c], z));   // F_lin + F_drag
+      if (has_fx) {
+        cd fx[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) fx[c] = bld(bFx, v, c * nw16);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) F[c] = add(F[c], fx[c]);
+      }
+      cd Z[6][6];
+      {
+        // index the LDS image with a zero the compiler cannot see through, so that its 144
+        // loop-invariant reads stay here instead of being hoisted into VGPRs for the solve
+        const int zo = opaque_zero();
+        const double* zm = mbc + zo;
+        const double* zb = bd + zo;
+        const double w2 = -(w * w);
+        if (d.mb_per_bin) {
+          const double* M = d.M + (size_t)b * 36;
+          const double* B = d.B + (size_t)b * 36;
+#pragma unroll
+          for (int r = 0; r < 6; ++r) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) Z[r][c] = mk(w2 * M[6 * r + c] + zm[72 + 6 * r + c], w * (B[6 * r + c] + zb[6 * r + c]));
+            __builtin_amdgcn_sched_barrier(0);   // one row of reads in flight at a time
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 6; ++r) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+              Z[r][c] = mk(w2 * zm[6 * r + c] + zm[72 + 6 * r + c], w * (zm[36 + 6 * r + c] + zb[6 * r + c]));
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      my_sing |= !lu_solve<6>(Z, F);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const cd x = F[c];
+        const cd xlast = xl[c * NWP + b];
+        my_nan |= (x.r != x.r) || (x.i != x.i);
+        // tolCheck = |Xi - XiLast| / (|Xi| + tol) < tol  (raft/raft_model.py:961-962)
+        const double tt = cabs(sub(x, xlast)) / (cabs(x) + tol);
+        my_ok = my_ok && (tt < tol);
+        st_nt(Xo + c * nw + b, x);   // streamed: only the last iteration's value is kept
+        if (XP) st(XP + c * nw + b, xlast);
+        // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged
+        xl[c * NWP + b] = add(scl(xlast, 0.2), scl(x, 0.8));
+      }
+#ifdef RH_PROF
+      tc_sol += clock64() - tc1;
+#endif
+    }
+    PROF_ADD(3, tc_exc);
+    PROF_ADD(4, tc_sol);
+    PROF_T(ta3);
+    const int all_ok = __syncthreads_and(my_ok ? 1 : 0);
+    const int any_nan = __syncthreads_or(my_nan ? 1 : 0);
+    const int any_sing = __syncthreads_or(my_sing ? 1 : 0);
+    PROF_T(ta4);
+    PROF_ADD(5, ta4 - ta3);
+    if (any_nan) {
+      status = RH_CASE_NAN;
+      iters = it + 1;
+      break;
+    }
+    if (any_sing) {
+      status = RH_CASE_SINGULAR;
+      iters = it + 1;
+      break;
+    }
+    if (all_ok) {
+      status = RH_CASE_CONVERGED;
+      iters = it + 1;
+      break;
+    }
+  }
+
+  // ---------------- outputs ------------------------------------------------------------
+  PROF_T(te0);
+  if (tid == 0) {
+    a.o.iters[ic] = iters;
+    a.o.status[ic] = status;
+  }
+  if (a.o.B_drag && tid < 36) a.o.B_drag[(size_t)ic * 36 + tid] = bd[tid];
+  if (a.o.Bmat)
+    for (int e = tid; e < nn * 9; e += kLT) a.o.Bmat[(size_t)ic * nn * 9 + e] = bm[e];
+  if (a.o.Z) {   // final impedance fowt.Z (raft/raft_model.py:1013) from the last B_drag, streamed
+#pragma unroll 1
+    for (int j = 0; j < NB; ++j) {
+      const int b = tid + kLT * j;
+      if (b >= nw) continue;
+      const double w = lw[b], w2 = -(w * w);
+      rh_c128* Zo = a.o.Z + ((size_t)ic * nw + b) * 36;
+#pragma unroll 1
+      for (int e = 0; e < 36; ++e) {
+        const double M = d.mb_per_bin ? d.M[(size_t)b * 36 + e] : mbc[e];
+        const double B = d.mb_per_bin ? d.B[(size_t)b * 36 + e] : mbc[36 + e];
+        st(Zo + e, mk(w2 * M + mbc[72 + e], w * (B + bd[e])));
+      }
+    }
+  }
+  double ss[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int b = tid + kLT * j;
+    if (b >= nw) continue;
+    const double z = lz[b];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const cd x = ld(Xo + c * nw + b);
+      const cd xd = c >= 3 ? scl(x, kRad2Deg) : x;
+      const double m2 = abs2(xd);
+      ss[c] += m2;
+      if (a.o.psd) a.o.psd[((size_t)ic * 6 + c) * nw + b] = 0.5 * m2 / d.dw;
+      if (a.o.rao) st(a.o.rao + ((size_t)ic * 6 + c) * nw + b, fabs(z) > 1e-6 ? cd{x.r / z, x.i / z} : mk(0, 0));
+    }
+  }
+  if (a.o.std) {
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const double s = wave_sum(ss[c]);
+      if (lane == 0) sred[wv * 6 + c] = s;
+    }
+    __syncthreads();
+    if (tid < 6) {
+      double s = 0;
+      for (int w = 0; w < kLW; ++w) s += sred[w * 6 + tid];
+      a.o.std[(size_t)ic * 6 + tid] = sqrt(0.5 * s);
+    }
+  }
+  PROF_T(te1);
+  PROF_ADD(6, te1 - te0);
+}
+
+}  // namespace rh

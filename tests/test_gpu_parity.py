@@ -205,3 +205,29 @@ def test_system_solve_12dof_matches_numpy():
         Zs[6:, 6:] = Z[1, b]
         Zs += K
         np.testing.assert_allclose(X[:, b], np.linalg.solve(Zs, F[:, b]), rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("tag,design,settings,ncase", [("c2_nw1000", "VolturnUS-S_example", {"min_freq": 0.0002}, 128),
+                                                       ("c2_nw200", "VolturnUS-S_example", None, 64),
+                                                       ("c1_OC3spar", "OC3spar", None, 16)])
+def test_fast_and_general_kernels_agree(tag, design, settings, ncase):
+    """The LDS-resident fast kernel (k_solve_lds) and the general kernel (k_solve_cases) on the
+    same batch: identical iteration counts and statuses, outputs within 1e-12 (they differ only
+    in the summation order of the per-node bin reductions)."""
+    from raft import _native as N
+    T = load_golden(tag)
+    m, f = make_model(design, T, settings)
+    cases = random_cases(ncase, 99)
+    want = ("psd", "std", "zeta", "B_drag", "rao")
+    a = m.analyzeCasesBatch(cases, want=want)
+    N.check(N.lib().rh_set_solver(1), "rh_set_solver")
+    try:
+        b = m.analyzeCasesBatch(cases, want=want)
+    finally:
+        N.check(N.lib().rh_set_solver(0), "rh_set_solver")
+    np.testing.assert_array_equal(a["iters"], b["iters"])
+    np.testing.assert_array_equal(a["status"], b["status"])
+    for ic in range(ncase):
+        assert rel(a["Xi"][ic], b["Xi"][ic]) < 1e-12, ic
+        assert rel(a["B_drag"][ic], b["B_drag"][ic]) < 1e-12, ic
+    np.testing.assert_array_equal(a["zeta"], b["zeta"])

@@ -1,0 +1,48 @@
+"""Build phase-ablated copies of librafthip.so (tools/ubench/var_<name>.so) to attribute the
+case-solve time to its phases on the GPU.  The ablated libraries give wrong answers by
+construction; tools/ubench/time_solve.py only times them (per executed iteration)."""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+CSRC = os.path.join(ROOT, "raft-teststuff_amd", "csrc")
+
+EDITS = {
+    "prof": [],          # unmodified source built with -DRH_PROF (phase cycle counters)
+    "noLU": [("      my_sing |= !lu_solve<6>(Z, F);", "      F[0] = add(F[0], Z[0][0]);")],
+    "noA": [("      for (int n = 0; n < nn; n += 3) {\n        step(KA, n);\n        if (n + 1 < nn) step(KB, n + 1);",
+             "      for (int n = 0; n < 0; n += 3) {\n        step(KA, n);\n        if (n + 1 < nn) step(KB, n + 1);")],
+    "noC": [("        for (int n = 0; n < nn; n += 3) {\n          step(KA, n);",
+             "        for (int n = 0; n < 0; n += 3) {\n          step(KA, n);")],
+}
+
+
+def build(name, edits, flags=()):
+    tmp = tempfile.mkdtemp()
+    dst = os.path.join(tmp, "csrc")
+    shutil.copytree(CSRC, dst)
+    inc = os.path.join(tmp, "..", "include")
+    p = os.path.join(dst, "rh_solve.hip")
+    s = open(p).read()
+    for a, b in edits:
+        assert a in s, (name, a[:60])
+        s = s.replace(a, b)
+    open(p, "w").write(s)
+    # rh_device.h includes ../../include/rafthip.h relative to csrc
+    os.makedirs(os.path.join(tmp, "x"), exist_ok=True)
+    shutil.move(dst, os.path.join(tmp, "x", "csrc"))
+    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
+    out = os.path.join(ROOT, "tools", "ubench", f"var_{name}.so")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC",
+                    "-Wno-unused-result", *flags, "-o", out, os.path.join(tmp, "x", "csrc", "rh_abi.hip")], check=True)
+    shutil.rmtree(tmp)
+    print("built", out)
+
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(EDITS)
+    for n in names:
+        build(n, EDITS[n], ["-DRH_PROF"] if n == "prof" else [])
