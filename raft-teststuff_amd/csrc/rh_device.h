@@ -63,21 +63,30 @@ __device__ __forceinline__ bool lu_solve(cd (&A)[N][N], cd (&x)[N]) {
       if (v > best) { best = v; p = i; }
     }
     ok = ok && (best != 0.0);
+    // The row exchange is a chain of per-lane selects; skip it when no lane of the wave
+    // pivots off the diagonal at this step (the common case for these impedance matrices).
+    // Results are the same either way.
+    if (__builtin_amdgcn_ballot_w64(p != k) != 0) {
 #pragma unroll
-    for (int i = k + 1; i < N; ++i) {
-      const bool sw = (p == i);
+      for (int i = k + 1; i < N; ++i) {
+        const bool sw = (p == i);
 #pragma unroll
-      for (int j = k; j < N; ++j) {
-        const cd a = A[k][j], b = A[i][j];
-        A[k][j] = sw ? b : a;
-        A[i][j] = sw ? a : b;
+        for (int j = k; j < N; ++j) {
+          const cd a = A[k][j], b = A[i][j];
+          A[k][j] = sw ? b : a;
+          A[i][j] = sw ? a : b;
+        }
+        const cd a = x[k], b = x[i];
+        x[k] = sw ? b : a;
+        x[i] = sw ? a : b;
       }
-      const cd a = x[k], b = x[i];
-      x[k] = sw ? b : a;
-      x[i] = sw ? a : b;
     }
-    const cd piv = A[k][k];
-    const cd rinv = cdiv(mk(1.0, 0.0), best != 0.0 ? piv : mk(1.0, 0.0));
+    // 1/piv = conj(piv) / |piv|^2: one real division per pivot, reused by the back
+    // substitution (|Z| entries are far from the overflow range of |piv|^2)
+    const cd piv = best != 0.0 ? A[k][k] : mk(1.0, 0.0);
+    const double inv = 1.0 / (piv.r * piv.r + piv.i * piv.i);
+    const cd rinv = mk(piv.r * inv, -piv.i * inv);
+    A[k][k] = rinv;   // the diagonal is only needed as its reciprocal from here on
 #pragma unroll
     for (int i = k + 1; i < N; ++i) {
       const cd l = mul(A[i][k], rinv);
@@ -91,7 +100,7 @@ __device__ __forceinline__ bool lu_solve(cd (&A)[N][N], cd (&x)[N]) {
     cd s = x[k];
 #pragma unroll
     for (int j = k + 1; j < N; ++j) s = sub(s, mul(A[k][j], x[j]));
-    x[k] = cdiv(s, A[k][k]);
+    x[k] = mul(s, A[k][k]);
   }
   return ok;
 }

@@ -29,6 +29,8 @@ __device__ unsigned long long rh_prof[8];
 
 constexpr int kLT = 512;          // threads per case workgroup
 constexpr int kLW = kLT / 64;     // waves per case workgroup
+constexpr int kRingA = 3;         // wave-table prefetch depth (nodes) of phase A
+constexpr int kRingC = 6;         // ... of phase C (one bin per pass: less work per node)
 
 // A scalar zero the compiler cannot fold (see its use in phase C).
 __device__ __forceinline__ int opaque_zero() {
@@ -37,12 +39,85 @@ __device__ __forceinline__ int opaque_zero() {
   return z;
 }
 
+// The lane index, recomputed where it is used: a hoisted copy would be one more value kept
+// live across the whole solve (and spilled, and its reload would drain the prefetch ring,
+// since scratch loads share the vector-memory counter with the wave-table loads).
+__device__ __forceinline__ int lane_here() {
+  int r;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(r));
+  return r;
+}
+
 template <int CTRL>
-__device__ __forceinline__ double dpp_mov(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+__device__ __forceinline__ double dpp_mov(double v) {   // full-mask permutations: every lane valid
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
   return __hiloint2double(hi, lo);
 }
+
+// Transposing butterfly: 16 per-lane values u[k] -> lane i of EVERY row ends with the wave
+// total (all 64 lanes) of value k(i) = 8 f0 + 4 f1 + 2 f2 + f3, with the lane bits
+//   f0 = b0^b2, f1 = b1^b2, f2 = b2^b3, f3 = b3     (i = lane & 15, b = bits of i).
+// Stage s pairs lane i with i^1 (quad_perm [1,0,3,2]), i^2 (quad_perm [2,3,0,1]), i^7
+// (row_half_mirror), i^15 (row_mirror); the f_s differ across each pair and agree on the
+// values both lanes still hold, so each lane keeps one half, sends the other, and the value
+// count halves per stage: 15 exchanges for 16 values instead of 16 full reductions.  The
+// four row sums are then combined across rows (lane^16, lane^32).  Fixed order everywhere.
+__device__ __forceinline__ double tbfly16(double (&u)[16], int lane) {
+  const int i = lane & 15;
+  const bool f0 = ((i ^ (i >> 2)) & 1) != 0, f1 = (((i >> 1) ^ (i >> 2)) & 1) != 0;
+  const bool f2 = (((i >> 2) ^ (i >> 3)) & 1) != 0, f3 = ((i >> 3) & 1) != 0;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const double keep = f0 ? u[p + 8] : u[p], send = f0 ? u[p] : u[p + 8];
+    u[p] = keep + dpp_mov<0xB1>(send);
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const double keep = f1 ? u[p + 4] : u[p], send = f1 ? u[p] : u[p + 4];
+    u[p] = keep + dpp_mov<0x4E>(send);
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const double keep = f2 ? u[p + 2] : u[p], send = f2 ? u[p] : u[p + 2];
+    u[p] = keep + dpp_mov<0x141>(send);
+  }
+  {
+    const double keep = f3 ? u[1] : u[0], send = f3 ? u[0] : u[1];
+    u[0] = keep + dpp_mov<0x140>(send);
+  }
+  double t = u[0];
+  t += __shfl_xor(t, 16, 64);
+  t += __shfl_xor(t, 32, 64);
+  return t;
+}
+__device__ __forceinline__ int tbfly16_index(int lane) {
+  const int i = lane & 15;
+  return 8 * ((i ^ (i >> 2)) & 1) + 4 * (((i >> 1) ^ (i >> 2)) & 1) + 2 * (((i >> 2) ^ (i >> 3)) & 1) + ((i >> 3) & 1);
+}
+
+// Three wave sums at once.  A 2-stage transposing butterfly inside each quad (partners i^1,
+// i^2: each lane keeps one of the values {a, b, c, 0}), then the quad sums are folded over
+// the row (row_ror 4, 8) and over the rows (lane^16, lane^32).  Every lane ends with the
+// wave total of value tbfly3_index(lane) (0 = a, 1 = b, 2 = c, 3 = pad): lanes 0, 2, 1
+// hold a, b, c.  33 instructions instead of 3 x 18 for three separate reductions.
+__device__ __forceinline__ double tbfly3(double a, double b, double c, int lane) {
+  const bool f0 = (lane & 1) != 0, f1 = (lane & 2) != 0;
+  // stage 0: pairs (a, c) and (b, 0): keep the second of each pair if f0
+  const double k0 = f0 ? c : a, s0 = f0 ? a : c;
+  const double k1 = f0 ? 0.0 : b, s1 = f0 ? b : 0.0;
+  const double u0 = k0 + dpp_mov<0xB1>(s0);
+  const double u1 = k1 + dpp_mov<0xB1>(s1);
+  // stage 1: pair (u0, u1): keep u1 if f1
+  double t = (f1 ? u1 : u0) + dpp_mov<0x4E>(f1 ? u0 : u1);
+  t += dpp_mov<0x124>(t);   // row_ror:4
+  t += dpp_mov<0x128>(t);   // row_ror:8
+  t += __shfl_xor(t, 16, 64);
+  t += __shfl_xor(t, 32, 64);
+  return t;
+}
+// value held by a lane after tbfly3: 2 f0 + f1 -> lane 0: a (0), lane 1: c (2), lane 2: b (1)
+__device__ __forceinline__ int tbfly3_index(int lane) { return 2 * (lane & 1) + ((lane >> 1) & 1); }
 
 template <int CTRL, int ROWS>
 __device__ __forceinline__ double dpp_mov_rows(double v) {   // rows outside ROWS receive 0
@@ -85,6 +160,7 @@ template <int NB>
 __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wv_s = __builtin_amdgcn_readfirstlane(wv);   // wave index in an SGPR
   PROF_T(tp0);
   const int slot = xcd_remap(blockIdx.x, a.c.ncase);
   const int ic = a.c.order ? a.c.order[slot] : slot;
@@ -206,9 +282,10 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
 #pragma unroll
           for (int p = 0; p < 3; ++p) K[p][j] = bld(bK, vb[j], so + (unsigned)p * nw16);
       };
-      auto reduce_node = [&](const cd (&K)[3][NB], int n) {
+      // this lane's partial sums over its bins of |s_q|^2, |s_1|^2, |s_2|^2 for one node
+      auto node_sums = [&](const cd (&K)[3][NB], int n, double& s0, double& s1, double& s2) {
         const double t = nt[n];
-        double s0 = 0, s1 = 0, s2 = 0;
+        s0 = s1 = s2 = 0;
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
           const double z = bz[j];
@@ -219,33 +296,30 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
           s1 += abs2(sp1);
           s2 += abs2(sp2);
         }
-        s0 = wave_sum63(s0);
-        s1 = wave_sum63(s1);
-        s2 = wave_sum63(s2);
-        if (lane == 63) {
-          double* R = red + (size_t)n * 3 * kLW + wv;
-          R[0] = s0;
-          R[kLW] = s1;
-          R[2 * kLW] = s2;
-        }
       };
-      cd KA[3][NB], KB[3][NB], KC[3][NB];
-      load_node(KA, 0);
-      load_node(KB, 1);
+      // the three sums of a node are reduced over the wave together (tbfly3); lane k < 3
+      // writes sum k.  The ring slot of node n is refilled with node n + kRingA.
+      cd K[kRingA][3][NB];
+#pragma unroll
+      for (int r = 0; r < kRingA; ++r) load_node(K[r], r);
       int m = -1, mnext = 0;
-      auto step = [&](cd (&K)[3][NB], int n) {
-        if (n == mnext) {   // uniform: entering member m+1 (members are node-contiguous)
-          do { ++m; mnext = mstart[m + 1]; } while (mnext == n);
-          member_terms(m);
+      for (int n = 0; n < nn; n += kRingA) {
+#pragma unroll
+        for (int r = 0; r < kRingA; ++r) {
+          const int nr = n + r;
+          if (nr < nn) {
+            if (nr == mnext) {   // uniform: entering member m+1 (members are node-contiguous)
+              do { ++m; mnext = mstart[m + 1]; } while (mnext == nr);
+              member_terms(m);
+            }
+            double s0, s1, s2;
+            node_sums(K[r], nr, s0, s1, s2);
+            load_node(K[r], nr + kRingA);
+            const int ln = lane_here();
+            const double tot = tbfly3(s0, s1, s2, ln);
+            if (ln < 3) red[(nr * 3 + tbfly3_index(ln)) * kLW + wv_s] = tot;
+          }
         }
-        reduce_node(K, n);
-        load_node(K, n + 3);
-      };
-      load_node(KC, 2);
-      for (int n = 0; n < nn; n += 3) {
-        step(KA, n);
-        if (n + 1 < nn) step(KB, n + 1);
-        if (n + 2 < nn) step(KC, n + 2);
       }
     }
     __syncthreads();
@@ -347,16 +421,15 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
           S2 = add(S2, scl(K[2], A2));
           T1 = add(T1, scl(K[1], A3));
           T2 = add(T2, scl(K[2], A4));
-          load1(K, n + 3);
+          load1(K, n + kRingC);
         };
-        cd KA[3], KB[3], KC[3];
-        load1(KA, 0);
-        load1(KB, 1);
-        load1(KC, 2);
-        for (int n = 0; n < nn; n += 3) {
-          step(KA, n);
-          if (n + 1 < nn) step(KB, n + 1);
-          if (n + 2 < nn) step(KC, n + 2);
+        cd K[kRingC][3];
+#pragma unroll
+        for (int r = 0; r < kRingC; ++r) load1(K[r], r);
+        for (int n = 0; n < nn; n += kRingC) {
+#pragma unroll
+          for (int r = 0; r < kRingC; ++r)
+            if (n + r < nn) step(K[r], n + r);
         }
         if (nn > 0) fold();
       }
@@ -411,7 +484,8 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
         const cd xlast = xl[c * NWP + b];
         my_nan |= (x.r != x.r) || (x.i != x.i);
         // tolCheck = |Xi - XiLast| / (|Xi| + tol) < tol  (raft/raft_model.py:961-962)
-        const double tt = cabs(sub(x, xlast)) / (cabs(x) + tol);
+        // (magnitudes as sqrt(re^2 + im^2): within an ulp of np.abs's hypot, far cheaper)
+        const double tt = sqrt(abs2(sub(x, xlast))) / (sqrt(abs2(x)) + tol);
         my_ok = my_ok && (tt < tol);
         st_nt(Xo + c * nw + b, x);   // streamed: only the last iteration's value is kept
         if (XP) st(XP + c * nw + b, xlast);

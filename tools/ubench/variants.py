@@ -13,6 +13,8 @@ CSRC = os.path.join(ROOT, "raft-teststuff_amd", "csrc")
 EDITS = {
     "prof": [],          # unmodified source built with -DRH_PROF (phase cycle counters)
     "noLU": [("      my_sing |= !lu_solve<6>(Z, F);", "      F[0] = add(F[0], Z[0][0]);")],
+    "stXo": [("        st_nt(Xo + c * nw + b, x);", "        st(Xo + c * nw + b, x);")],
+    "noXo": [("        st_nt(Xo + c * nw + b, x);", "        if (x.r == 1234.5) st(Xo + c * nw + b, x);")],
     "noA": [("      for (int n = 0; n < nn; n += 3) {\n        step(KA, n);\n        if (n + 1 < nn) step(KB, n + 1);",
              "      for (int n = 0; n < 0; n += 3) {\n        step(KA, n);\n        if (n + 1 < nn) step(KB, n + 1);")],
     "noC": [("        for (int n = 0; n < nn; n += 3) {\n          step(KA, n);",
