@@ -315,7 +315,13 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   wk.node = (rh_c128*)work;
   wk.wl = wk.node + (size_t)q->nq * rh::QT_COUNT * q->n2;
   wk.freq = wk.wl + (size_t)q->nmq * rh::WT_COUNT * q->n2;
+  wk.hinv = wk.freq + (size_t)rh::FT_COUNT * q->n2;
+  wk.kayt = reinterpret_cast<double*>(wk.hinv + (size_t)q->nkr * q->n2 * 12);
   const int nb = (q->n2 + 63) / 64;
+  if (q->nkr > 0) {
+    hipLaunchKernelGGL(rh::k_qtf_kay, dim3(nb, q->nkr), dim3(64), 0, s, *q, wk);
+    RH_HIP(hipGetLastError());
+  }
   hipLaunchKernelGGL(rh::k_qtf_freq, dim3(nb), dim3(64), 0, s, *q, nw, w, Xi0, M66, wk);
   RH_HIP(hipGetLastError());
   if (q->nq > 0) {

@@ -30,10 +30,13 @@ struct QtfWork {
   rh_c128* node;   // [nq][QT_COUNT][n2]
   rh_c128* wl;     // [nmq][WT_COUNT][n2]
   rh_c128* freq;   // [FT_COUNT][n2]
+  rh_c128* hinv;   // [nkr][n2][12] reciprocals of the Hankel-derivative table q.hank
+  double* kayt;    // [nkr][n2][2] cosh(k R H), sqrt(k R H tanh(k R H)) of every KAY radius row
 };
 
-__host__ __device__ inline size_t qtf_work_elems(const rh_qtf_design& q) {
-  return (size_t)q.nq * QT_COUNT * q.n2 + (size_t)q.nmq * WT_COUNT * q.n2 + (size_t)FT_COUNT * q.n2;
+__host__ __device__ inline size_t qtf_work_elems(const rh_qtf_design& q) {   // complex elements
+  return (size_t)q.nq * QT_COUNT * q.n2 + (size_t)q.nmq * WT_COUNT * q.n2 + (size_t)FT_COUNT * q.n2 +
+         (size_t)q.nkr * q.n2 * 12 + ((size_t)q.nkr * q.n2 * 2 + 1) / 2;
 }
 
 __device__ __forceinline__ double qn(const rh_qtf_design& q, int f, int n) { return q.qnode[f * q.nq + n]; }
@@ -281,11 +284,27 @@ __device__ __forceinline__ void ld3(const rh_c128* T, int field, size_t n2, int 
   for (int i = 0; i < 3; ++i) o[i] = ld(T + (size_t)(field + i) * n2 + f);
 }
 
-// omega of raft_member.py:1102-1109 from the Hankel derivative table D_n (n = 0..11)
-__device__ __forceinline__ cd kay_omega(const rh_c128* D1, const rh_c128* D2, int n) {
-  const cd HN_ii = ld(D1 + n), HNm1_ii = ld(D1 + n + 1);
-  const cd HN_jj = cconj(ld(D2 + n)), HNm1_jj = cconj(ld(D2 + n + 1));
-  return sub(cdiv(mk(1, 0), mul(HNm1_ii, HN_jj)), cdiv(mk(1, 0), mul(HN_ii, HNm1_jj)));
+// Per (KAY radius row, frequency) factors of the Kim & Yue correction that do not depend on
+// the pair: the reciprocals R_n = 1 / D_n of the Hankel-derivative table, and the interval
+// factors cosh(k R H), sqrt(k R H tanh(k R H)) of raft_member.py:1185-1190 (H = h / R).
+__global__ __launch_bounds__(64) void k_qtf_kay(rh_qtf_design q, QtfWork wk) {
+  const int f = blockIdx.x * 64 + threadIdx.x, ir = blockIdx.y;
+  if (f >= q.n2) return;
+  const rh_c128* D = q.hank + ((size_t)ir * q.n2 + f) * 12;
+  rh_c128* R = wk.hinv + ((size_t)ir * q.n2 + f) * 12;
+#pragma unroll
+  for (int n = 0; n < 12; ++n) st(R + n, cdiv(mk(1, 0), ld(D + n)));
+  const double Rr = q.kray[RH_KR_R * q.nkr + ir];
+  const double kh = q.k2[f] * Rr * (q.depth / Rr);
+  double* t = wk.kayt + ((size_t)ir * q.n2 + f) * 2;
+  t[0] = cosh(kh);
+  t[1] = sqrt(kh * tanh(kh));
+}
+
+// omega of raft_member.py:1102-1109, 1 / (H'_{n+1}(k1R) conj H'_n(k2R)) - 1 / (H'_n(k1R) conj H'_{n+1}(k2R)),
+// from the reciprocal tables R1 = 1/D(k1 R), R2 = 1/D(k2 R): division-free
+__device__ __forceinline__ cd kay_omega(const rh_c128* R1, const rh_c128* R2, int n) {
+  return sub(mul(ld(R1 + n + 1), cconj(ld(R2 + n))), mul(ld(R1 + n), cconj(ld(R2 + n + 1))));
 }
 
 // Row k of this rank is i1 = k nrank + (k even ? rank : nrank-1-rank): a snake deal of the
@@ -572,16 +591,17 @@ __global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork
       for (int i = 0; i < 6; ++i) Fk[i] = mk(0, 0);
       for (int ir = r0; ir < r1; ++ir) {
         const double R = q.kray[RH_KR_R * q.nkr + ir];
-        const rh_c128* D1 = q.hank + ((size_t)ir * n2 + i1) * 12;
-        const rh_c128* D2 = q.hank + ((size_t)ir * n2 + i2) * 12;
+        const rh_c128* D1 = wk.hinv + ((size_t)ir * n2 + i1) * 12;
+        const rh_c128* D2 = wk.hinv + ((size_t)ir * n2 + i2) * 12;
         const double k1R = k1 * R, k2R = k2 * R;
         double sre;
         double px, py, pz;
         if (ir == r0) {       // waterline term (:1133-1149)
           const cd c0 = mk(0, -rho * g * R * 2 / M_PI / (k1R * k2R));
           cd s = mk(0, 0);
-          for (int nn = 0; nn <= 10; ++nn) s = add(s, mul(c0, kay_omega(D1, D2, nn)));
-          sre = s.r;
+#pragma unroll 1
+          for (int nn = 0; nn <= 10; ++nn) s = add(s, kay_omega(D1, D2, nn));
+          sre = mul(c0, s).r;
           px = wx;
           py = wy;
           pz = wz;
@@ -599,15 +619,16 @@ __global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork
             Im = 0.5 * (a2 - d2 - a1 + d1);
             Ip = 0.5 * (a2 + d2 - a1 - d1);
           }
-          const double ch1 = cosh(k1h), ch2 = cosh(k2h);
-          const double coef = k1h * k2h / sqrt(k1h * tanh(k1h)) / sqrt(k2h * tanh(k2h));
+          const double* t1 = wk.kayt + ((size_t)ir * n2 + i1) * 2;
+          const double* t2 = wk.kayt + ((size_t)ir * n2 + i2) * 2;
+          // coef / (cosh(k1 R H) cosh(k2 R H)) and Ip / (k1R k2R), hoisted out of the n sum
+          const double cc = k1h * k2h / (t1[1] * t2[1] * t1[0] * t2[0]);
+          const double ipr = Ip / (k1R * k2R);
           const cd c0 = mk(0, rho * g * R * 2 / M_PI / (k1R * k2R));
           cd s = mk(0, 0);
-          for (int nn = 0; nn <= 10; ++nn) {
-            const double tail = coef * (Im + Ip * nn * (nn + 1) / k1R / k2R) / ch1 / ch2;
-            s = add(s, scl(mul(c0, kay_omega(D1, D2, nn)), tail));
-          }
-          sre = s.r;
+#pragma unroll 1
+          for (int nn = 0; nn <= 10; ++nn) s = add(s, scl(kay_omega(D1, D2, nn), cc * (Im + ipr * (nn * (nn + 1)))));
+          sre = mul(c0, s).r;
           px = q.kray[RH_KR_MX * q.nkr + ir];
           py = q.kray[RH_KR_MY * q.nkr + ir];
           pz = q.kray[RH_KR_MZ * q.nkr + ir];
