@@ -24,6 +24,29 @@ sys.path.insert(0, os.path.join(ROOT, "raft-teststuff_amd"))
 
 NCASE = 512
 PEAK_FP64 = 78.6e12   # MI355X FP64 dense peak (vector = matrix rate), FLOP/s
+# HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950
+# correction of MI355X_MICROARCH.md + WRITE_SIZE), written by tools/pmc_summary.py
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v4", "pmc_summary.json")
+
+
+def pmc_traffic(kernel):
+    """HBM traffic (bytes per launch) of `kernel` from PMC_SUMMARY, or None."""
+    try:
+        with open(PMC_SUMMARY) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    for name, v in d.items():
+        if kernel in name and "hbm_read_bytes_corrected" in v and "hbm_write_bytes" in v:
+            return v["hbm_read_bytes_corrected"] + v["hbm_write_bytes"]
+    return None
+
+
+def solve_kernel_name(nw):
+    """The kernel rh_solve_cases launches for this grid (dispatch in rh_abi.hip)."""
+    if nw <= 1024:
+        return f"rh::k_solve_lds<{1 if nw <= 512 else 2}>"
+    return "rh::k_solve_cases<4>"
 
 
 def flops_per_case(n_loop, nw, nc, nr, nsub):
@@ -186,7 +209,8 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
                       "submerged_nodes": qd.nq, "kay_intervals": nkay, "waterline_members": nwl,
                       "parallelism": f"row-sharded x{world} + all-reduce"},
            "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
-                        "frac": achieved / PEAK_FP64, "traffic": None, "kernel": "rh_qtf_slender (all launches)",
+                        "frac": achieved / PEAK_FP64, "traffic": pmc_traffic("k_qtf_pairs"),
+                        "kernel": "rh_qtf_slender (all launches; traffic: k_qtf_pairs)",
                         "kernel_ms": ms, "flops_per_pair": fpp,
                         "note": "FP64 VALU; algorithmic FLOPs from SURVEY.md §8(d); per-GPU rate"}}
     return out
@@ -278,9 +302,12 @@ def main():
                    "cases_per_step_per_gpu": args.ncase, "nw": dd.nw, "submerged_nodes": dd.nn,
                    "nodes_circ_rect": [nc, nr], "nIter": int(m.nIter), "parallelism": f"case-sharded x{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_FP64, "traffic": None,
-                     "kernel": "rh::k_solve_cases<4>", "kernel_ms": kern_ms,
-                     "flops_per_launch": flops, "note": "FP64 compute bound; algorithmic FLOPs from SURVEY.md §8(d)"},
+                     "frac": achieved / PEAK_FP64, "traffic": pmc_traffic(solve_kernel_name(dd.nw).split("<")[0]),
+                     "kernel": solve_kernel_name(dd.nw), "kernel_ms": kern_ms,
+                     "flops_per_launch": flops,
+                     "note": "FP64 VALU bound (peak = MI355X FP64 vector = matrix rate); algorithmic FLOPs from "
+                             "SURVEY.md §8(d); traffic = HBM bytes per launch from "
+                             + os.path.relpath(PMC_SUMMARY, ROOT)},
         "iterations_mean": float(iters.mean()),
         "converged_frac": float((status == 1).mean()),
     }

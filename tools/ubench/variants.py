@@ -11,6 +11,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 CSRC = os.path.join(ROOT, "raft-teststuff_amd", "csrc")
 
 EDITS = {
+    "qNoKay": [("rh_qtf.hip", "    if (qm(q, RH_QM_KAY, m) != 0.0) {", "    if (qm(q, RH_QM_KAY, m) == 12345.0) {")],
+    "qNoNodes": [("rh_qtf.hip", "    for (int n = n0; n < n1; ++n) {\n      const rh_c128* T = wk.node", "    for (int n = n0; n < n0; ++n) {\n      const rh_c128* T = wk.node")],
     "prof": [],          # unmodified source built with -DRH_PROF (phase cycle counters)
     "noLU": [("      my_sing |= !lu_solve<6>(Z, F);", "      F[0] = add(F[0], Z[0][0]);")],
     "stXo": [("        st_nt(Xo + c * nw + b, x);", "        st(Xo + c * nw + b, x);")],
@@ -27,12 +29,13 @@ def build(name, edits, flags=()):
     dst = os.path.join(tmp, "csrc")
     shutil.copytree(CSRC, dst)
     inc = os.path.join(tmp, "..", "include")
-    p = os.path.join(dst, "rh_solve.hip")
-    s = open(p).read()
-    for a, b in edits:
+    for e in edits:
+        fname, a, b = e if len(e) == 3 else ("rh_solve.hip", e[0], e[1])
+        p = os.path.join(dst, fname)
+        s = open(p).read()
         assert a in s, (name, a[:60])
         s = s.replace(a, b)
-    open(p, "w").write(s)
+        open(p, "w").write(s)
     # rh_device.h includes ../../include/rafthip.h relative to csrc
     os.makedirs(os.path.join(tmp, "x"), exist_ok=True)
     shutil.move(dst, os.path.join(tmp, "x", "csrc"))
