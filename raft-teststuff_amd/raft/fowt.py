@@ -5,9 +5,10 @@ argument meaning, return values and the side-effect attributes downstream code r
 (SURVEY.md §8(b)).  The per-node / per-bin arithmetic runs in librafthip; this class owns
 the per-design preparation (members, node tables, linear matrices) and the device buffers.
 
-Not built here: statics (calcStatics needs member inertia and
-hydrostatics -- supply them with setStatics()), MoorPy mooring, rotor aerodynamics
-(CCBlade), BEM (pyHAMS) and reading external QTF files (potSecOrder=2).
+The statics (member inertia / hydrostatics / RNA) are computed on
+the host by raft/statics.py.  Not built here: MoorPy mooring (its
+stiffness C_moor is an input, FOWT.setStatics), rotor aerodynamics (CCBlade), BEM (pyHAMS)
+and reading external QTF files (potSecOrder=2).
 """
 import os
 import ctypes
@@ -17,6 +18,7 @@ import numpy as np
 from . import _native as N
 from .hydro_math import DEG2RAD, get_from_dict, wave_numbers, translate_matrix_6to6
 from .member import Member
+from .statics import RNA, fowt_statics
 from .prep import DeviceDesign
 
 STATICS_KEYS = ["M_struc", "B_struc", "C_struc", "C_hydro", "W_struc", "W_hydro"]
@@ -43,7 +45,11 @@ class FOWT:
         self.potModMaster = get_from_dict(plat, "potModMaster", dtype=int, default=0)
         dlsMax = get_from_dict(plat, "dlsMax", default=5.0)
         self.memberList = []
+        self.nplatmems = 0                 # raft/raft_fowt.py:61-67
+        self.ntowers = 0
+        self.rnaList = []                  # RNA inertia/pose per rotor (raft/statics.py)
         for mi in plat["members"]:
+            self.nplatmems += len(mi["heading"]) if "heading" in mi else 1
             mi = dict(mi)
             if self.potModMaster in [1]:
                 mi["potMod"] = False
@@ -62,12 +68,18 @@ class FOWT:
             self.nrotors = get_from_dict(turb, "nrotors", dtype=int, shape=0, default=1)
             towers = turb.get("tower")
             if towers is not None:
-                for mem in (towers if isinstance(towers, list) else [towers] * self.nrotors):
+                towers = towers if isinstance(towers, list) else [towers] * self.nrotors
+                self.ntowers = len(towers)
+                for mem in towers:
                     self.memberList.append(Member(mem, self.nw))
             nac = turb.get("nacelle")
             if nac is not None:
                 for mem in (nac if isinstance(nac, list) else [nac] * self.nrotors):
                     self.memberList.append(Member(mem, self.nw))
+            tcopy = dict(turb)
+            tcopy["nrotors"] = self.nrotors
+            if all(k in tcopy for k in ("mRNA", "IxRNA", "IrRNA", "xCG_RNA", "overhang", "shaft_tilt")):
+                self.rnaList = [RNA(tcopy, ir, get_from_dict) for ir in range(self.nrotors)]
             hhub = np.atleast_1d(get_from_dict(turb, "hHub", shape=-1, default=100.0))
             self._rotor_submerged = bool(np.any(hhub < 0))
             self._aero_mod = np.atleast_1d(get_from_dict(turb, "aeroServoMod", shape=-1, default=1))
@@ -104,18 +116,32 @@ class FOWT:
         self.Xi0 = self.r6 - np.array([self.x_ref, self.y_ref, 0, 0, 0, 0])
         for mem in self.memberList:
             mem.setPosition(r6=self.r6)
+        for rot in self.rnaList:
+            rot.setPosition(self.r6)
         self._dd = None
         self._qtf_devs = {}
 
     def setStatics(self, statics):
-        """Provide the outputs of calcStatics (M_struc, B_struc, C_struc, C_hydro, ...) and
-        optionally C_moor; the statics restatement is SURVEY.md §8(f) row 1."""
+        """Override calcStatics with given matrices (M_struc, B_struc, C_struc, C_hydro, ...)
+        and optionally C_moor -- e.g. the reference's own values for a regression run, or a
+        mooring stiffness from an external MoorPy model."""
         self._statics = {k: np.array(v, dtype=float) for k, v in statics.items()}
 
     def calcStatics(self):
+        """raft/raft_fowt.py:291-565: member inertia and hydrostatics summed about the PRP
+        (raft/statics.py).  Matrices given to setStatics() override the computed ones (a
+        full set skips the computation), and its C_moor stands in for MoorPy's stiffness."""
+        given = self._statics or {}
+        if not all(k in given for k in ("M_struc", "C_struc", "C_hydro")):
+            if self._rotor_submerged:
+                raise NotImplementedError("underwater rotors (blade-member buoyancy, raft/raft_fowt.py:386-443) "
+                                          "are outside the accelerated path")
+            if self.nrotors > 0 and len(self.rnaList) != self.nrotors:
+                raise ValueError("turbine: mRNA, IxRNA, IrRNA, xCG_RNA, overhang and shaft_tilt are required")
+            fowt_statics(self)
+        self._dd = None
         if self._statics is None:
-            raise NotImplementedError("FOWT.calcStatics (member inertia/hydrostatics, raft/raft_fowt.py:291-565) "
-                                      "is not restated yet: call setStatics() with the design's statics")
+            return
         for k in STATICS_KEYS:
             if k in self._statics:
                 setattr(self, k, self._statics[k].copy())

@@ -58,6 +58,34 @@ class Member:
         if self.MCF and self.shape != "circular":
             self.MCF = False
 
+        # shell, ballast and caps for the statics (raft/raft_member.py:99-154, used by
+        # raft/statics.py); `t` is required there, so its absence only fails calcStatics
+        self.t = get_from_dict(mi, "t", shape=n) if "t" in mi else None
+        self.rho_shell = get_from_dict(mi, "rho_shell", shape=0, default=8500.)
+        st_fill = get_from_dict(mi, "l_fill", shape=n - 1, default=0)
+        for i in range(n - 1):
+            if st_fill[i] < 0:
+                raise Exception(f"Member {self.name}: ballast level in section {i+1} is negative.")
+            if st_fill[i] > st[i + 1] - st[i]:
+                raise Exception(f"Member {self.name}: ballast level in section {i+1} exceeds section length."
+                                + f" ({st_fill[i]} > {st[i+1] - st[i]}).")
+        self.l_fill = st_fill / (st[-1] - st[0]) * self.l
+        rho_fill = get_from_dict(mi, "rho_fill", shape=-1, default=1025)
+        if np.isscalar(rho_fill):
+            self.rho_fill = np.zeros(n - 1) + rho_fill
+        elif len(rho_fill) == n - 1:
+            self.rho_fill = np.array(rho_fill)
+        else:
+            raise Exception(f"Member {self.name}: the number of provided ballast densities (rho_fill) must be 1 "
+                            "less than the number of stations.")
+        cap_st = np.atleast_1d(get_from_dict(mi, "cap_stations", shape=-1, default=[]))
+        if len(cap_st) == 0:
+            self.cap_t, self.cap_d_in, self.cap_stations = [], [], []
+        else:
+            self.cap_t = get_from_dict(mi, "cap_t", shape=cap_st.shape[0])
+            self.cap_d_in = get_from_dict(mi, "cap_d_in", shape=cap_st.shape[0])
+            self.cap_stations = (cap_st - st[0]) / (st[-1] - st[0]) * self.l
+
         self.Cd_q = get_from_dict(mi, "Cd_q", shape=n, default=0.0)
         self.Cd_p1 = get_from_dict(mi, "Cd", shape=n, default=0.6, index=0)
         self.Cd_p2 = get_from_dict(mi, "Cd", shape=n, default=0.6, index=1)

@@ -231,3 +231,26 @@ def test_fast_and_general_kernels_agree(tag, design, settings, ncase):
         assert rel(a["Xi"][ic], b["Xi"][ic]) < 1e-12, ic
         assert rel(a["B_drag"][ic], b["B_drag"][ic]) < 1e-12, ic
     np.testing.assert_array_equal(a["zeta"], b["zeta"])
+
+
+@pytest.mark.parametrize("tag,design,settings", [("c2_nw200", "VolturnUS-S_example", None), ("c1_OC3spar", "OC3spar", None)])
+def test_solve_with_native_statics(tag, design, settings):
+    """The whole per-design preparation on the host (statics from raft/statics.py, only the
+    mooring stiffness given, as MoorPy would supply it) and the device solve reproduce the
+    reference's golden runs."""
+    import raft
+    T = load_golden(tag)
+    d = load_design(design)
+    if settings:
+        d["settings"].update(settings)
+    m = raft.Model(d, statics=[{"C_moor": T["C_moor"]}])
+    f = m.fowtList[0]
+    f.setPosition(T["r6"])
+    f.calcStatics()
+    f.calcHydroConstants()
+    for k in ["M_struc", "C_struc", "C_hydro"]:
+        assert np.abs(getattr(f, k) - T[k]).max() <= 1e-12 * np.abs(T[k]).max()
+    for ic, case in enumerate(golden_cases(T)):
+        Xi = m.solveDynamics(dict(case))
+        assert f.iterations == T["out_iters"][ic]
+        assert rel(Xi, T["out_Xi"][ic]) < RTOL
