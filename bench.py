@@ -216,6 +216,82 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
     return out
 
 
+C5_DESIGNS = 250
+
+
+def bench_c5(device, steps, world, rank, dist):
+    """C5 (BASELINE.json configs[4]): 250 parametersweep-style VolturnUS-S_example variants
+    (raft/sweep.py) x 40 sea states (Hs 2..10 x Tp 6..20) = 10,000 cases at nw = 1000.
+    The design-major case list is split in contiguous blocks over the ranks; a rank prepares
+    only the designs its block touches (host members/statics/added mass + device tables),
+    solves its block in one launch and the per-case outputs (std, PSD, iterations) are
+    all-gathered over RCCL.  End-to-end time = prep + solve + gather (max over ranks);
+    solve-only = the launch alone, repeated `steps` times.  Strong scaling (fixed 10k)."""
+    import torch
+    from raft.batch import DesignBatch, sweep_cases
+    from raft.parallel import case_shard, gather_cases
+    from raft.sweep import sea_state_grid, sweep_multipliers, sweep_variant
+    with open(os.path.join(ROOT, "tests", "golden", "designs", "VolturnUS-S_example.json")) as fh:
+        base = json.load(fh)
+    base["settings"]["min_freq"] = 0.0002
+    C_moor = np.load(os.path.join(ROOT, "tests", "golden", "c2_nw1000.npz"))["C_moor"]
+    mult = sweep_multipliers(C5_DESIGNS)
+    grid = sea_state_grid()
+    idx_all, cases_all = sweep_cases(C5_DESIGNS, grid)
+    n = len(idx_all)
+    lo, hi = case_shard(n, rank, world)
+    dlo, dhi = int(idx_all[lo]), int(idx_all[hi - 1]) + 1
+    variants = [sweep_variant(base, mult[i]) for i in range(dlo, dhi)]      # inputs: not timed
+    local_idx = idx_all[lo:hi] - dlo
+    want = ("psd", "std")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    B = DesignBatch(variants, statics={"C_moor": C_moor}, device=device)
+    cs = B.case_set(local_idx, cases_all[lo:hi])
+    from raft.solver import prepare_batch
+    prep = prepare_batch(B.dds, cs)                  # device wave tables per (design, heading)
+    torch.cuda.synchronize()
+    t_prep = time.perf_counter() - t0
+    res = B.solve(None, cs, want=want, prepared=prep)
+    torch.cuda.synchronize()
+    t_solve1 = time.perf_counter() - t0 - t_prep
+    out = gather_cases({"std": res["std"], "psd": res["psd"], "iters": res["iters"]}, n)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_e2e = time.perf_counter() - t0
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        res = B.solve(None, cs, want=want, prepared=prep)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_solve = (time.perf_counter() - t1) / steps
+    ts = torch.tensor([t_e2e, t_prep, t_solve, B.host_seconds], dtype=torch.float64, device=f"cuda:{device}")
+    if world > 1:
+        dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+    t_e2e, t_prep, t_solve, t_host = (float(x) for x in ts.cpu())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    iters = out["iters"].cpu().numpy()
+    return {"metric": "sweep cases/sec end-to-end (design prep + solve + gather)", "value": n / t_e2e,
+            "unit": "cases/s", "scaling": "strong", "cases": n, "designs": C5_DESIGNS, "sea_states": len(grid),
+            "end_to_end_s": t_e2e, "prep_s": t_prep, "host_prep_s": t_host, "first_solve_s": t_solve1,
+            "solve_only_cases_per_s": n / t_solve, "solve_ms": t_solve * 1e3, "kernel_ms_rank0": kern_ms,
+            "iterations_mean": float(iters.mean()),
+            "config": {"workload": "C5: 250 VolturnUS-S_example parametersweep variants (5 variables U(0.75,1.25)) "
+                                   "x 40 sea states, nw=1000", "nw": B.nw,
+                       "parallelism": f"case-block-sharded x{world} + all-gather (std, PSD, iterations)"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -224,6 +300,7 @@ def main():
     ap.add_argument("--ncase", type=int, default=NCASE)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-qtf", action="store_true")
+    ap.add_argument("--no-c5", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -313,6 +390,8 @@ def main():
     }
     if not args.no_qtf:
         line["qtf"] = bench_qtf(device, max(3, args.steps // 4), 1, world, rank, dist)
+    if not args.no_c5:
+        line["c5"] = bench_c5(device, max(3, args.steps // 4), world, rank, dist)
     if baselines is not None:
         line["cpu_baseline"] = baselines[0]
         if "qtf" in line:

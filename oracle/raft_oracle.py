@@ -419,6 +419,34 @@ def solve_dynamics(T, case, nIter, XiStart=0.0, tol=0.01, loop=False, second_ord
                 F_iner=F_iner, F_drag=F_drag, zeta=zeta, S=S, beta=beta, iters_pair=pair, **extra)
 
 
+def solve_farm(Ts, case, nIter, K_array=None, XiStart=0.0, tol=0.01):
+    """Multi-FOWT Model.solveDynamics (raft/raft_model.py:852-1146 with nFOWT > 1): each
+    FOWT runs its own drag fixed point (:869-1013, no coupling inside the loop); then
+    Z_sys = blockdiag(fowt.Z) + array stiffness (:1021-1031), Zinv per bin (:1037-1040) and
+    Xi[ih] = Zinv F_wave with F_wave = F_BEM + F_hydro_iner + drag excitation (:1049-1065).
+    Returns dict(Xi=[nH+1,6N,nw], iters=[N], fowts=[per-FOWT solve_dynamics results])."""
+    per = [solve_dynamics(T, case, nIter, XiStart, tol) for T in Ts]
+    nf = len(Ts)
+    nw = len(Ts[0]["w"])
+    nD = 6 * nf
+    Zsys = np.zeros([nw, nD, nD], dtype=complex)
+    for i, r in enumerate(per):
+        Zsys[:, 6 * i:6 * i + 6, 6 * i:6 * i + 6] += np.moveaxis(r["Z"], 2, 0)
+    if K_array is not None:
+        Zsys += np.asarray(K_array, dtype=float)[None, :, :]
+    Zinv = np.linalg.inv(Zsys)
+    nH = len(per[-1]["beta"])                          # Q11: the last FOWT's nWaves
+    Xi = np.zeros([nH + 1, nD, nw], dtype=complex)
+    for ih in range(nH):
+        F_wave = np.zeros([nD, nw], dtype=complex)
+        for i, (T, r) in enumerate(zip(Ts, per)):
+            nodes = Nodes(T)
+            u, _, _, F_iner = hydro_excitation(T, nodes, r["beta"], r["zeta"])
+            F_wave[6 * i:6 * i + 6] = F_iner[ih] + drag_excitation(nodes, r["Bmat"], u[ih])
+        Xi[ih] = np.einsum("bij,jb->ib", Zinv, F_wave)
+    return dict(Xi=Xi, iters=[r["iters"] for r in per], converged=[r["converged"] for r in per], fowts=per)
+
+
 def _solve_bins(w, M, B, C, F):
     """Per-bin Z assembly + LAPACK zgesv (raft/raft_model.py:942-947), batched."""
     Zb = (-w[:, None, None] ** 2 * np.moveaxis(M, 2, 0) + 1j * w[:, None, None] * np.moveaxis(B, 2, 0)

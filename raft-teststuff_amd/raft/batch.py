@@ -1,0 +1,87 @@
+"""Design x sea-state batches: the C5 throughput path (BASELINE.json configs[4]).
+
+The reference evaluates a design sweep as one runRAFT per design and one solveDynamics per
+case (raft/parametersweep.py:91, raft/raft_model.py:244-388).  Here every design is
+prepared once on the host (members, statics, added mass: raft/member.py, raft/statics.py)
+and on the device (node tables, per-heading wave tables), and then ALL (design, sea state)
+cases go through one rh_solve_cases launch, one workgroup per case, sorted by
+(design, heading) so an XCD streams one design's tables out of its L2.
+
+Multi-GPU: designs are dealt to ranks in contiguous blocks (each rank prepares only its
+own designs, so the host preparation scales with the rank count too); the per-case
+outputs are all-gathered once at the end (raft/parallel.py gather_cases).
+"""
+import time
+
+import numpy as np
+
+from .model import Model
+from .solver import CaseSet, solve_batch
+
+
+class DesignBatch:
+    """Prepared single-FOWT designs sharing one frequency grid.
+
+    designs : list of design dicts (each with `settings`, `site`, `platform`, `turbine`)
+    statics : None, one dict for all designs, or one dict per design, of FOWT.setStatics
+              entries (typically just {"C_moor": K}: the mooring stiffness MoorPy would give)
+    r6      : platform pose for the linearisation (default: the reference position)
+    """
+
+    def __init__(self, designs, statics=None, r6=None, device=0):
+        t0 = time.perf_counter()
+        if isinstance(statics, dict) or statics is None:
+            statics = [statics] * len(designs)
+        if len(statics) != len(designs):
+            raise ValueError("statics: one dict for all designs or one per design")
+        self.models, self.fowts, self.dds = [], [], []
+        for d, st in zip(designs, statics):
+            m = Model(d, statics=None if st is None else [st], device=device)
+            if m.nFOWT != 1:
+                raise NotImplementedError("DesignBatch handles single-FOWT designs (use Model for arrays)")
+            f = m.fowtList[0]
+            f.setPosition(np.zeros(6) if r6 is None else np.asarray(r6, dtype=float))
+            f.calcStatics()
+            f.calcHydroConstants()
+            self.models.append(m)
+            self.fowts.append(f)
+        m0 = self.models[0]
+        for m in self.models[1:]:
+            if m.nw != m0.nw or not np.array_equal(m.w, m0.w):
+                raise ValueError("all designs of a batch must share the frequency grid")
+            if m.nIter != m0.nIter or m.XiStart != m0.XiStart:
+                raise ValueError("all designs of a batch must share nIter and XiStart")
+        self.nIter, self.XiStart, self.nw, self.w = m0.nIter, m0.XiStart, m0.nw, m0.w
+        self.host_seconds = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        self.dds = [f.device_design() for f in self.fowts]
+        self.upload_seconds = time.perf_counter() - t0
+
+    def __len__(self):
+        return len(self.models)
+
+    def case_set(self, design_idx, cases):
+        """CaseSet of (design index, case dict) pairs; one sea state per case."""
+        hd, sp, Hs, Tp, gm = [], [], [], [], []
+        for c in cases:
+            one = lambda k, dflt=None: (np.atleast_1d(c.get(k, dflt))[0] if c.get(k, dflt) is not None else None)
+            if not np.isscalar(c["wave_heading"]) and len(c["wave_heading"]) != 1:
+                raise NotImplementedError("DesignBatch: one sea state per case")
+            hd.append(float(one("wave_heading", 0)))
+            sp.append(str(one("wave_spectrum", "JONSWAP")))
+            Hs.append(float(one("wave_height")))
+            Tp.append(float(one("wave_period")))
+            gm.append(float(one("wave_gamma", 0)))
+        return CaseSet(np.asarray(design_idx, dtype=np.int32), hd, sp, Hs, Tp, gm)
+
+    def solve(self, design_idx, cases, tol=0.01, want=("psd", "std", "zeta", "B_drag"), prepared=None):
+        """Drag fixed point + response of every case in one device call.  Returns the
+        BatchResult (device tensors, stream-ordered): Xi [n,6,nw], iters, status, ..."""
+        cs = cases if isinstance(cases, CaseSet) else self.case_set(design_idx, cases)
+        return solve_batch(self.dds, cs, self.nIter, self.XiStart, tol, want=want, prepared=prepared)
+
+
+def sweep_cases(n_designs, sea_states):
+    """Every design paired with every sea state: (design index, case) lists, design-major."""
+    idx = np.repeat(np.arange(n_designs, dtype=np.int32), len(sea_states))
+    return idx, [dict(s) for _ in range(n_designs) for s in sea_states]

@@ -51,3 +51,27 @@ def statics_of(T):
 @pytest.fixture(scope="session")
 def golden():
     return load_golden
+
+
+def farm_tables(T):
+    """Per-FOWT design tables of the c4_farm fixture (keys f<i>_*)."""
+    out = []
+    i = 0
+    while f"f{i}_w" in T:
+        pre = f"f{i}_"
+        out.append({k[len(pre):]: v for k, v in T.items() if k.startswith(pre)})
+        i += 1
+    return out
+
+
+def fixture_design(tag, base_name, fi=0):
+    """(design dict, design tables T, FOWT index) behind a solve fixture: the farm fixture
+    holds per-FOWT tables (f<i>_*), the C5 sweep fixtures hold the multipliers of the
+    parametersweep variant (raft/sweep.py) of `base_name`."""
+    G = load_golden(tag)
+    d = load_design(base_name)
+    if "sweep_mult" in G:
+        from raft.sweep import sweep_variant
+        d = sweep_variant(d, G["sweep_mult"])
+    T = farm_tables(G)[fi] if "f0_w" in G else G
+    return d, T, G

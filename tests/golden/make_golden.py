@@ -144,7 +144,11 @@ def case_dict(design, row):
 
 def golden_solve(tag, yaml_path, cases, settings=None, keep_Z=False):
     settings = settings or {}
-    design = load_design(yaml_path, **settings)
+    if isinstance(yaml_path, dict):          # an in-memory design (C5 sweep variants)
+        design = yaml_path
+        design["settings"].update(settings)
+    else:
+        design = load_design(yaml_path, **settings)
     model = raft.Model(design)
     fowt = model.fowtList[0]
     out = {}
@@ -355,9 +359,90 @@ def golden_qtf():
     print("wrote c3_qtf.npz", file=sys.stderr)
 
 
+# Stand-in array-level (shared-line) stiffness for the 2-FOWT farm: both bodies anchored
+# by C_MOOR at the FOWT level plus a shared surge/sway line between them.
+K_SHARED = np.diag([3.0e4, 1.0e4, 0.0, 0.0, 0.0, 0.0])
+K_ARRAY = np.block([[K_SHARED, -K_SHARED], [-K_SHARED, K_SHARED]])
+
+
+def golden_farm():
+    """C4: tests/test_data/VolturnUS-S_farm.yaml (2 FOWTs, x = 0 / 1600 m, heading_adjust
+    180 / 0, nw = 240, nIter = 10).  Array coupling enters Z_sys through
+    ms.getCoupledStiffnessA (raft/raft_model.py:1030-1031), here the K_ARRAY fixture."""
+    design = load_design(os.path.join(REF, "tests", "test_data", "VolturnUS-S_farm.yaml"))
+    model = raft.Model(design)
+    model.ms.getCoupledStiffnessA = lambda *a, **kw: K_ARRAY.copy()
+    cases = seeded_cases(3, 20241018)
+    out = {"K_array": K_ARRAY, "nIter": np.int64(model.nIter), "XiStart": np.float64(model.XiStart)}
+    res = {k: [] for k in ["Xi", "iters", "B_drag", "zeta", "seconds"]}
+    for c in cases:
+        case = dict(c)
+        for i, fowt in enumerate(model.fowtList):
+            prepare_fowt(fowt, case)
+            if f"f{i}_w" not in out:
+                out.update({f"f{i}_{k}": v for k, v in design_tables(fowt).items()})
+        buf = io.StringIO()
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(buf):
+            Xi = model.solveDynamics(case, display=2)
+        dt = time.perf_counter() - t0
+        # one "Iteration k, converged" line per FOWT drag loop, in FOWT order
+        its = [int(m) + 1 for m in re.findall(r"Iteration (\d+), converged", buf.getvalue())]
+        assert len(its) == len(model.fowtList), its
+        res["Xi"].append(np.array(Xi))
+        res["iters"].append(its)
+        res["B_drag"].append([f.B_hydro_drag.copy() for f in model.fowtList])
+        res["zeta"].append(model.fowtList[0].zeta.copy())
+        res["seconds"].append(dt)
+        print(f"  farm: case {c} iters={its} t={dt:.1f}s", file=sys.stderr)
+    for k, v in res.items():
+        out["out_" + k] = np.array(v)
+    keys = ["wave_spectrum", "wave_period", "wave_height", "wave_heading", "wave_gamma"]
+    out["cases_json"] = np.array(json.dumps([{k: np.atleast_1d(c[k]).tolist() for k in keys} for c in cases]))
+    np.savez_compressed(os.path.join(HERE, "c4_farm.npz"), **out)
+    print("wrote c4_farm.npz", file=sys.stderr)
+
+
+def load_sweep_module():
+    """raft-teststuff_amd/raft/sweep.py by file path (numpy only; the name `raft` is the
+    reference package here)."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(os.path.dirname(HERE)), "raft-teststuff_amd", "raft", "sweep.py")
+    spec = importlib.util.spec_from_file_location("rh_sweep", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def golden_sweep():
+    """C5: three parametersweep-style VolturnUS-S_example variants (raft/parametersweep.py
+    variables, U(0.75,1.25) draws) at nw = 1000, two sea states each, statics computed by
+    the reference for each variant, mooring stiffness C_MOOR."""
+    sw = load_sweep_module()
+    with open(os.path.join(REF, "examples", "VolturnUS-S_example.yaml")) as f:
+        base = yaml.load(f, Loader=yaml.FullLoader)
+    mult = sw.sweep_multipliers(3, seed=20241016)
+    grid = sw.sea_state_grid()
+    rng = np.random.default_rng(20241019)
+    for i, m in enumerate(mult):
+        d = sw.sweep_variant(base, m)
+        pick = rng.choice(len(grid), 2, replace=False)
+        cases = [dict(grid[j], wind_speed=0, wind_heading=0, turbulence=0, turbine_status="operating", yaw_misalign=0)
+                 for j in pick]
+        golden_solve(f"c5_sweep{i}", d, cases, settings=dict(min_freq=0.0002))
+        T = dict(np.load(os.path.join(HERE, f"c5_sweep{i}.npz")))
+        T.pop("node_Imat_MCF", None)
+        T["sweep_mult"] = m
+        np.savez_compressed(os.path.join(HERE, f"c5_sweep{i}.npz"), **T)
+
+
 def main(which):
     if "qtf" in which:
         golden_qtf()
+    if "farm" in which:
+        golden_farm()
+    if "sweep" in which:
+        golden_sweep()
     if "designs" in which:
         export_designs()
     ex = os.path.join(REF, "examples", "VolturnUS-S_example.yaml")

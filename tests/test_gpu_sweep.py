@@ -1,0 +1,141 @@
+"""GPU parity for the multi-design (C5) and multi-FOWT (C4) paths, against reference runs.
+
+* C5: three parametersweep variants of VolturnUS-S_example (raft/sweep.py restating
+  raft/parametersweep.py:56-88) at nw = 1000.  The reference computed the statics of each
+  variant itself (tests/golden/make_golden.py golden_sweep); here the product does the whole
+  per-design preparation (members, statics, added mass) and solves every case of every
+  design in ONE rh_solve_cases launch.
+* C4: tests/test_data/VolturnUS-S_farm.yaml, two FOWTs 1600 m apart, coupled through the
+  array stiffness fixture (raft/raft_model.py:1021-1065).
+
+Tolerance (north_star): 1e-9 relative (normwise per case), identical iteration counts.
+"""
+import numpy as np
+import pytest
+
+from conftest import farm_tables, fixture_design, golden_cases, load_design, load_golden, statics_of
+from oracle import raft_oracle as O
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-9
+SWEEP_TAGS = ["c5_sweep0", "c5_sweep1", "c5_sweep2"]
+
+
+def rel(a, b):
+    nb = np.linalg.norm(b)
+    return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
+
+
+def _sweep_inputs():
+    designs, cmoor, idx, cases, refs = [], [], [], [], []
+    for i, tag in enumerate(SWEEP_TAGS):
+        d, T, _ = fixture_design(tag, "VolturnUS-S_example")
+        d["settings"]["min_freq"] = 0.0002
+        designs.append(d)
+        cmoor.append({"C_moor": T["C_moor"]})
+        for ic, c in enumerate(golden_cases(T)):
+            idx.append(i)
+            cases.append(c)
+            refs.append((T, ic))
+    return designs, cmoor, idx, cases, refs
+
+
+def _check_case(res, j, T, ic):
+    assert res["iters"][j] == T["out_iters"][ic], (j, res["iters"][j], T["out_iters"][ic])
+    assert res["status"][j] == T["out_conv"][ic]
+    assert rel(res["Xi"][j], T["out_Xi"][ic][0]) < RTOL, rel(res["Xi"][j], T["out_Xi"][ic][0])
+    assert rel(res["B_drag"][j], T["out_B_drag"][ic]) < RTOL
+    dofs = ["surge", "sway", "heave", "roll", "pitch", "yaw"]
+    smax = max(T[f"out_{d}_std"][ic] for d in dofs)
+    for i, dof in enumerate(dofs):
+        np.testing.assert_allclose(res["std"][j, i], T[f"out_{dof}_std"][ic], rtol=RTOL, atol=RTOL * smax)
+
+
+def test_sweep_variants_one_launch_match_reference():
+    """Native per-design preparation + one launch over 3 designs x 2 sea states."""
+    from raft.batch import DesignBatch
+    designs, cmoor, idx, cases, refs = _sweep_inputs()
+    B = DesignBatch(designs, statics=cmoor)
+    for f, (T, _) in zip(B.fowts, [refs[0], refs[2], refs[4]]):
+        for k in ["M_struc", "C_struc", "C_hydro"]:
+            assert np.abs(getattr(f, k) - T[k]).max() <= 1e-12 * np.abs(T[k]).max(), k
+    res = B.solve(idx, cases).host()
+    for j, (T, ic) in enumerate(refs):
+        _check_case(res, j, T, ic)
+
+
+def test_full_size_c5_sweep_properties():
+    """C5 at full size: 250 designs x 40 sea states = 10,000 cases, nw = 1000, one launch.
+    The three reference-run variants are designs 0-2 of the batch and their golden cases
+    are embedded in the case list; the rest is checked by size-independent properties:
+    a 64-case sub-batch reproduces its cases bit for bit, every case finishes with a
+    finite response and a consistent status/iteration count."""
+    import torch
+    from raft.batch import DesignBatch, sweep_cases
+    from raft.sweep import sea_state_grid, sweep_multipliers, sweep_variant
+    designs, cmoor, gidx, gcases, refs = _sweep_inputs()
+    base = load_design("VolturnUS-S_example")
+    base["settings"]["min_freq"] = 0.0002
+    mult = sweep_multipliers(250)
+    designs = designs + [sweep_variant(base, m) for m in mult[3:]]
+    B = DesignBatch(designs, statics={"C_moor": refs[0][0]["C_moor"]})
+    idx, cases = sweep_cases(len(designs), sea_state_grid())
+    idx = np.concatenate([idx, np.asarray(gidx, dtype=np.int32)])
+    cases = cases + gcases
+    assert len(idx) == 10000 + len(gcases)
+    res = B.solve(idx, cases, want=("std", "B_drag"))
+    torch.cuda.synchronize()
+    h = res.host()
+    n0 = 10000
+    for j, (T, ic) in enumerate(refs):
+        _check_case(h, n0 + j, T, ic)
+    assert np.all(np.isfinite(h["Xi"]))
+    assert set(np.unique(h["status"])) <= {0, 1}
+    assert np.all(h["iters"][h["status"] == 0] == B.nIter + 1)
+    assert np.all((h["iters"] >= 1) & (h["iters"] <= B.nIter + 1))
+    sub = np.sort(np.random.default_rng(9).choice(n0, 64, replace=False))
+    s = B.solve(idx[sub], [cases[i] for i in sub], want=("std", "B_drag")).host()
+    np.testing.assert_array_equal(s["Xi"], h["Xi"][sub])
+    np.testing.assert_array_equal(s["iters"], h["iters"][sub])
+
+
+def _farm_model(T, native_statics=False):
+    import raft
+    Ts = farm_tables(T)
+    m = raft.Model(load_design("VolturnUS-S_farm"),
+                   statics=[{"C_moor": t["C_moor"]} if native_statics else statics_of(t) for t in Ts])
+    m.K_array = T["K_array"]
+    for f, t in zip(m.fowtList, Ts):
+        f.setPosition(t["r6"])
+        f.calcStatics()
+        f.calcHydroConstants()
+    return m, Ts
+
+
+@pytest.mark.parametrize("native_statics", [False, True])
+def test_farm_matches_reference(native_statics):
+    """C4: 2 coupled FOWTs, 12-DOF system; per-FOWT drag loops and iteration counts."""
+    T = load_golden("c4_farm")
+    m, Ts = _farm_model(T, native_statics)
+    for ic, case in enumerate(golden_cases(T)):
+        Xi = m.solveDynamics(dict(case))
+        assert [f.iterations for f in m.fowtList] == list(T["out_iters"][ic])
+        assert Xi.shape == T["out_Xi"][ic].shape
+        assert rel(Xi, T["out_Xi"][ic]) < RTOL, rel(Xi, T["out_Xi"][ic])
+        for i, f in enumerate(m.fowtList):
+            assert rel(f.B_hydro_drag, T["out_B_drag"][ic][i]) < RTOL
+            assert rel(f.Xi, T["out_Xi"][ic][:, 6 * i:6 * i + 6]) < RTOL
+
+
+def test_farm_seeded_cases_match_oracle():
+    """Seeded sea states (other headings, gamma) beyond the golden set, vs the oracle."""
+    T = load_golden("c4_farm")
+    m, Ts = _farm_model(T)
+    rng = np.random.default_rng(44)
+    for _ in range(3):
+        case = dict(wave_spectrum="JONSWAP", wave_period=float(rng.uniform(6, 18)), wave_height=float(rng.uniform(1, 10)),
+                    wave_heading=float(rng.choice([0, 45, 135, 270])), wave_gamma=float(rng.choice([0.0, 2.0])))
+        Xi = m.solveDynamics(dict(case))
+        r = O.solve_farm(Ts, dict(case), int(T["nIter"]), T["K_array"], float(T["XiStart"]))
+        assert [f.iterations for f in m.fowtList] == r["iters"]
+        assert rel(Xi, r["Xi"]) < RTOL

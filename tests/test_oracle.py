@@ -7,10 +7,10 @@ values of the reference's tests/test_helpers.py (numbers only).
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden
+from conftest import farm_tables, golden_cases, load_golden
 from oracle import raft_oracle as O
 
-SOLVE_TAGS = ["c1_OC3spar", "c2_nw200", "multi_heading", "c2_nw1000"]
+SOLVE_TAGS = ["c1_OC3spar", "c2_nw200", "multi_heading", "c2_nw1000", "c5_sweep0", "c5_sweep1", "c5_sweep2"]
 
 
 @pytest.mark.parametrize("tag", SOLVE_TAGS)
@@ -30,6 +30,24 @@ def test_oracle_solve_dynamics_matches_reference(tag):
         for dof in dofs:
             np.testing.assert_allclose(mo[dof + "_std"], T[f"out_{dof}_std"][ic], rtol=1e-12, atol=1e-12 * smax)
             np.testing.assert_allclose(mo[dof + "_PSD"], T[f"out_{dof}_PSD"][ic], rtol=1e-11, atol=1e-12 * pmax)
+
+
+def test_oracle_farm_matches_reference():
+    """C4: two coupled FOWTs (tests/test_data/VolturnUS-S_farm.yaml) with the array
+    stiffness fixture: per-FOWT iteration counts, the 12-DOF system response, B_drag."""
+    T = load_golden("c4_farm")
+    Ts = farm_tables(T)
+    assert len(Ts) == 2
+    for ic, case in enumerate(golden_cases(T)):
+        r = O.solve_farm(Ts, dict(case), int(T["nIter"]), T["K_array"], float(T["XiStart"]))
+        assert r["iters"] == list(T["out_iters"][ic])
+        ref = T["out_Xi"][ic]
+        assert np.linalg.norm(r["Xi"] - ref) <= 1e-12 * np.linalg.norm(ref)
+        for i, f in enumerate(r["fowts"]):
+            Bref = T["out_B_drag"][ic][i]
+            np.testing.assert_allclose(f["B_drag"], Bref, rtol=1e-12, atol=1e-12 * np.abs(Bref).max())
+        # the shared line couples the bodies: FOWT 1 moves under FOWT 0's excitation alone
+        assert np.abs(ref[0, 6:]).max() > 0
 
 
 @pytest.mark.parametrize("tag", ["fowt_VolturnUS-S", "fowt_OC3spar"])

@@ -3,39 +3,44 @@ constants, node tables) reproduces the reference's tables exactly."""
 import numpy as np
 import pytest
 
-from conftest import load_design, load_golden
+from conftest import fixture_design, load_golden
 
-CASES = [("fowt_VolturnUS-S", "VolturnUS-S_test", {}), ("fowt_OC3spar", "OC3spar_test", {}),
-         ("c2_nw200", "VolturnUS-S_example", {}), ("c1_OC3spar", "OC3spar", {}),
-         ("c2_nw1000", "VolturnUS-S_example", {"min_freq": 0.0002})]
+# (fixture, design, settings, FOWT index); c4_farm: the two FOWTs of the farm (x = 0 and
+# 1600 m, heading_adjust 180 and 0), c5_sweep*: parametersweep variants (raft/sweep.py)
+CASES = [("fowt_VolturnUS-S", "VolturnUS-S_test", {}, 0), ("fowt_OC3spar", "OC3spar_test", {}, 0),
+         ("c2_nw200", "VolturnUS-S_example", {}, 0), ("c1_OC3spar", "OC3spar", {}, 0),
+         ("c2_nw1000", "VolturnUS-S_example", {"min_freq": 0.0002}, 0),
+         ("c4_farm", "VolturnUS-S_farm", {}, 0), ("c4_farm", "VolturnUS-S_farm", {}, 1),
+         ("c5_sweep0", "VolturnUS-S_example", {"min_freq": 0.0002}, 0),
+         ("c5_sweep1", "VolturnUS-S_example", {"min_freq": 0.0002}, 0),
+         ("c5_sweep2", "VolturnUS-S_example", {"min_freq": 0.0002}, 0)]
+ARGS = "tag,design,settings,fi"
 
 
-def _model(design_name, settings, T):
+def _model(tag, design_name, settings, fi):
     import raft
-    d = load_design(design_name)
+    d, T, _ = fixture_design(tag, design_name, fi)
     d["settings"].update(settings)
     m = raft.Model(d)
-    f = m.fowtList[0]
+    f = m.fowtList[fi]
     f.setPosition(T["r6"])
     f.calcHydroConstants()
-    return m, f
+    return m, f, T
 
 
-@pytest.mark.parametrize("tag,design,settings", CASES)
-def test_grid_and_wave_numbers(tag, design, settings):
-    T = load_golden(tag)
-    m, f = _model(design, settings, T)
+@pytest.mark.parametrize(ARGS, CASES)
+def test_grid_and_wave_numbers(tag, design, settings, fi):
+    m, f, T = _model(tag, design, settings, fi)
     np.testing.assert_array_equal(m.w, T["w"])
     np.testing.assert_array_equal(f.k, T["k"])          # vectorised waveNumber is bit-identical
     assert f.dw == T["dw"]
 
 
-@pytest.mark.parametrize("tag,design,settings", CASES)
-def test_node_tables_match_reference(tag, design, settings):
+@pytest.mark.parametrize(ARGS, CASES)
+def test_node_tables_match_reference(tag, design, settings, fi):
     from raft import _native as N
     from raft.prep import node_table
-    T = load_golden(tag)
-    m, f = _model(design, settings, T)
+    m, f, T = _model(tag, design, settings, fi)
     assert sum(mm.ns for mm in f.memberList) == len(T["node_sub"])
     tab, imat, _, _ = node_table(f)
     sub = T["node_sub"].astype(bool)
@@ -52,10 +57,9 @@ def test_node_tables_match_reference(tag, design, settings):
     np.testing.assert_array_equal(tab[N.NF["I00"]:N.NF["I22"] + 1], T["node_Imat"][sub].reshape(-1, 9).T)
 
 
-@pytest.mark.parametrize("tag,design,settings", CASES)
-def test_added_mass_matches_reference(tag, design, settings):
-    T = load_golden(tag)
-    m, f = _model(design, settings, T)
+@pytest.mark.parametrize(ARGS, CASES)
+def test_added_mass_matches_reference(tag, design, settings, fi):
+    m, f, T = _model(tag, design, settings, fi)
     np.testing.assert_array_equal(f.A_hydro_morison, T["A_hydro_morison"])
 
 
@@ -63,8 +67,7 @@ def test_drag_areas_follow_reference_formulas():
     """Rectangular axial area uses ds[0] twice; end areas are |.|."""
     from raft import _native as N
     from raft.prep import node_table
-    T = load_golden("c2_nw200")
-    m, f = _model("VolturnUS-S_example", {}, T)
+    m, f, T = _model("c2_nw200", "VolturnUS-S_example", {}, 0)
     tab, _, _, _ = node_table(f)
     sub = T["node_sub"].astype(bool)
     ds, dls, drs, circ = T["node_ds"][sub], T["node_dls"][sub], T["node_drs"][sub], T["node_circ"][sub].astype(bool)

@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 from numpy.testing import assert_allclose
 
-from conftest import load_design, load_golden
+from conftest import fixture_design, load_design, load_golden
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REF = np.load(os.path.join(HERE, "golden", "statics_ref.npz"))
@@ -80,6 +80,24 @@ def test_fowt_statics_match_golden_fixture_runs(tag, design):
         if k in T:
             ref = T[k]
             assert np.abs(getattr(f, k) - ref).max() <= 1e-12 * max(np.abs(ref).max(), 1.0), k
+
+
+@pytest.mark.parametrize("tag,design,fi", [("c4_farm", "VolturnUS-S_farm", 0), ("c4_farm", "VolturnUS-S_farm", 1),
+                                           ("c5_sweep0", "VolturnUS-S_example", 0),
+                                           ("c5_sweep1", "VolturnUS-S_example", 0),
+                                           ("c5_sweep2", "VolturnUS-S_example", 0)])
+def test_statics_of_farm_and_sweep_variants(tag, design, fi):
+    """Each FOWT of the farm (positioned at x = 0 / 1600 m, rotated 180 / 0 deg) and each
+    C5 parametersweep variant: the statics the reference computed for those runs, to 1e-12."""
+    import raft
+    d, T, _ = fixture_design(tag, design, fi)
+    m = raft.Model(d)
+    f = m.fowtList[fi]
+    f.setPosition(T["r6"])
+    f.calcStatics()
+    for k in ["M_struc", "C_struc", "C_hydro", "W_struc", "W_hydro"]:
+        ref = T[k]
+        assert np.abs(getattr(f, k) - ref).max() <= 1e-12 * max(np.abs(ref).max(), 1.0), k
 
 
 def test_member_without_shell_thickness_fails_only_in_statics():
