@@ -26,7 +26,7 @@ NCASE = 512
 PEAK_FP64 = 78.6e12   # MI355X FP64 dense peak (vector = matrix rate), FLOP/s
 # HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950
 # correction of MI355X_MICROARCH.md + WRITE_SIZE), written by tools/pmc_summary.py
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v4", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v5", "pmc_summary.json")
 
 
 def pmc_traffic(kernel):
@@ -228,8 +228,8 @@ def bench_c5(device, steps, world, rank, dist):
     all-gathered over RCCL.  End-to-end time = prep + solve + gather (max over ranks);
     solve-only = the launch alone, repeated `steps` times.  Strong scaling (fixed 10k)."""
     import torch
-    from raft.batch import DesignBatch, sweep_cases
-    from raft.parallel import case_shard, gather_cases
+    from raft.batch import DesignBatch, sweep_cases, sweep_shard
+    from raft.parallel import gather_cases
     from raft.sweep import sea_state_grid, sweep_multipliers, sweep_variant
     with open(os.path.join(ROOT, "tests", "golden", "designs", "VolturnUS-S_example.json")) as fh:
         base = json.load(fh)
@@ -239,8 +239,7 @@ def bench_c5(device, steps, world, rank, dist):
     grid = sea_state_grid()
     idx_all, cases_all = sweep_cases(C5_DESIGNS, grid)
     n = len(idx_all)
-    lo, hi = case_shard(n, rank, world)
-    dlo, dhi = int(idx_all[lo]), int(idx_all[hi - 1]) + 1
+    lo, hi, dlo, dhi = sweep_shard(idx_all, rank, world)
     variants = [sweep_variant(base, mult[i]) for i in range(dlo, dhi)]      # inputs: not timed
     local_idx = idx_all[lo:hi] - dlo
     want = ("psd", "std")

@@ -154,6 +154,12 @@ int rh_version(void);
  * cross-check the two device paths on the same inputs. */
 int rh_set_solver(int which);
 
+/* Waves per 64 (w1, w2) pairs in the QTF pair kernel (process-wide; not part of the
+ * reference API): 1, 2 or 4 (default).  The per-pair terms are split over the waves and
+ * summed in a fixed order, so the result differs between settings only by rounding.
+ * Used by the tests and the kernel-tuning scripts. */
+int rh_set_qtf_waves(int waves);
+
 /* Unit-amplitude wave kinematics and strip-theory inertial excitation per heading.
  * Replaces the node loops of FOWT.calcHydroExcitation (raft/raft_fowt.py:1098-1124)
  * and helpers.getWaveKin (raft/helpers.py:105-154):

@@ -25,6 +25,7 @@ struct rh_ctx {
 namespace {
 thread_local std::string g_err;
 bool g_force_v2 = false;   // rh_set_solver(1): always use k_solve_cases (parity cross-checks)
+int g_qtf_waves = 4;       // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -102,6 +103,12 @@ extern "C" int rh_prof_read(unsigned long long* out, int reset) {
 int rh_set_solver(int which) {
   if (which != 0 && which != 1) return fail(RH_EINVAL, "rh_set_solver: which=%d (0 = auto, 1 = general kernel)", which);
   g_force_v2 = which == 1;
+  return RH_OK;
+}
+
+int rh_set_qtf_waves(int waves) {
+  if (waves != 1 && waves != 2 && waves != 4) return fail(RH_EINVAL, "rh_set_qtf_waves: waves=%d (1, 2 or 4)", waves);
+  g_qtf_waves = waves;
   return RH_OK;
 }
 
@@ -334,8 +341,17 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   }
   const int rows = (q->n2 + nrank - 1) / nrank;     // snake rounds (k_qtf_pairs skips i1 >= n2)
   if (rows > 0) {
-    hipLaunchKernelGGL(rh::k_qtf_pairs, dim3((q->n2 + rh::kQtfTile - 1) / rh::kQtfTile, rows), dim3(rh::kQtfTile), 0,
-                       s, *q, wk, qtf, rank, nrank, mirror);
+    const dim3 grid((q->n2 + rh::kQtfTile - 1) / rh::kQtfTile, rows);
+    switch (g_qtf_waves) {        // waves per 64 pairs (rh_set_qtf_waves; default 4)
+      case 1:
+        hipLaunchKernelGGL(rh::k_qtf_pairs<1>, grid, dim3(rh::kQtfTile), 0, s, *q, wk, qtf, rank, nrank, mirror);
+        break;
+      case 2:
+        hipLaunchKernelGGL(rh::k_qtf_pairs<2>, grid, dim3(2 * rh::kQtfTile), 0, s, *q, wk, qtf, rank, nrank, mirror);
+        break;
+      default:
+        hipLaunchKernelGGL(rh::k_qtf_pairs<4>, grid, dim3(4 * rh::kQtfTile), 0, s, *q, wk, qtf, rank, nrank, mirror);
+    }
     RH_HIP(hipGetLastError());
   }
   return RH_OK;

@@ -39,8 +39,23 @@ __host__ __device__ inline size_t qtf_work_elems(const rh_qtf_design& q) {   // 
          (size_t)q.nkr * q.n2 * 12 + ((size_t)q.nkr * q.n2 * 2 + 1) / 2;
 }
 
-__device__ __forceinline__ double qn(const rh_qtf_design& q, int f, int n) { return q.qnode[f * q.nq + n]; }
-__device__ __forceinline__ double qm(const rh_qtf_design& q, int f, int m) { return q.qmemb[f * q.nmq + m]; }
+// Loads of wave-uniform table entries through the constant address space: the backend
+// then issues scalar loads into SGPRs instead of 64 identical vector loads into VGPRs (the
+// tables are written by earlier launches only, so they are invariant inside a kernel)
+typedef const double __attribute__((address_space(4)))* f64_kp;
+typedef const int __attribute__((address_space(4)))* i32_kp;
+__device__ __forceinline__ cd lds(const rh_c128* p) {
+  const f64_kp d = (f64_kp)(p);
+  return cd{d[0], d[1]};
+}
+__device__ __forceinline__ double ldsd(const double* p) { return *(f64_kp)(p); }
+__device__ __forceinline__ int ldsi(const int* p) { return *(i32_kp)(p); }
+__device__ __forceinline__ double qn(const rh_qtf_design& q, int f, int n) { return ldsd(q.qnode + f * q.nq + n); }
+__device__ __forceinline__ double qm(const rh_qtf_design& q, int f, int m) { return ldsd(q.qmemb + f * q.nmq + m); }
+__device__ __forceinline__ void ldm9(const rh_qtf_design& q, int f, int n, double* M) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) M[i] = qn(q, f + i, n);
+}
 
 // cross products with a real vector (np.cross order)
 __device__ __forceinline__ void cross_cc(const cd* a, const cd* b, cd* o) {
@@ -283,6 +298,10 @@ __device__ __forceinline__ void ld3(const rh_c128* T, int field, size_t n2, int 
 #pragma unroll
   for (int i = 0; i < 3; ++i) o[i] = ld(T + (size_t)(field + i) * n2 + f);
 }
+__device__ __forceinline__ void ld3s(const rh_c128* T, int field, size_t n2, int f, cd* o) {   // f wave-uniform
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o[i] = lds(T + (size_t)(field + i) * n2 + f);
+}
 
 // Per (KAY radius row, frequency) factors of the Kim & Yue correction that do not depend on
 // the pair: the reciprocals R_n = 1 / D_n of the Hankel-derivative table, and the interval
@@ -303,35 +322,59 @@ __global__ __launch_bounds__(64) void k_qtf_kay(rh_qtf_design q, QtfWork wk) {
 
 // omega of raft_member.py:1102-1109, 1 / (H'_{n+1}(k1R) conj H'_n(k2R)) - 1 / (H'_n(k1R) conj H'_{n+1}(k2R)),
 // from the reciprocal tables R1 = 1/D(k1 R), R2 = 1/D(k2 R): division-free
-__device__ __forceinline__ cd kay_omega(const rh_c128* R1, const rh_c128* R2, int n) {
-  return sub(mul(ld(R1 + n + 1), cconj(ld(R2 + n))), mul(ld(R1 + n), cconj(ld(R2 + n + 1))));
+__device__ __forceinline__ cd kay_omega(const rh_c128* R1, const rh_c128* R2, int n) {   // R1 wave-uniform
+  return sub(mul(lds(R1 + n + 1), cconj(ld(R2 + n))), mul(lds(R1 + n), cconj(ld(R2 + n + 1))));
 }
 
 // Row k of this rank is i1 = k nrank + (k even ? rank : nrank-1-rank): a snake deal of the
 // upper-triangle rows (longest first), so every rank gets the same pair count to within one
 // row.  mirror = write the Hermitian lower triangle too (single device); sharded runs
 // mirror after the exchange (k_qtf_fill).
-__global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf,
-                                                        int rank, int nrank, int mirror) {
+//
+// A workgroup is NWV (W) waves on the SAME 64 pairs (one w1 row, 64 consecutive w2).  The terms
+// of a pair are split over the waves: wave w takes nodes w, w+W, ..., the waterline terms
+// of members w, w+W, ... and the Kim & Yue radius rows W-1-w, 2W-1-w, ... (reversed, so the
+// waves with one node fewer get the extra row), wave 0 also the Pinkster IV term.  The W
+// partial sums meet in LDS and wave 0 adds them in wave order (deterministic).  With one
+// wave per 64 pairs a row-sharded grid (80k pairs / 8 GPUs) is ~0.2 waves per SIMD; W waves
+// multiply the resident waves by W (on one GPU, 1 to 4 waves are within 1 %).
+//
+// Occupancy: left alone the compiler spends 256 VGPRs + AGPRs (1 wave per SIMD).  Asking
+// for 2 waves per SIMD costs ~40 spilled VGPRs (the wave-uniform w1 side and the node and
+// member tables come through scalar loads, so SGPRs carry them); C3 QTF 0.71 -> 0.50 ms.
+// 3 or 4 waves per SIMD spill 100-300 VGPRs and are slower (tools/ubench/run_qtf_variants.sh).
+#if !defined(RH_QTF_WPE)
+#define RH_QTF_WPE 2
+#endif
+#define RH_QTF_ATTR __attribute__((amdgpu_waves_per_eu(RH_QTF_WPE)))
+template <int NWV>
+__global__ __launch_bounds__(kQtfTile * NWV) RH_QTF_ATTR void k_qtf_pairs(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf,
+                                                            int rank, int nrank, int mirror) {
+  __shared__ double red[(NWV > 1 ? NWV - 1 : 1) * 12 * kQtfTile];
   const int kr = (int)blockIdx.y;
   const int i1 = kr * nrank + ((kr & 1) ? nrank - 1 - rank : rank);
-  const int i2 = blockIdx.x * kQtfTile + threadIdx.x;
+  const int lane = (int)threadIdx.x & (kQtfTile - 1);
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kQtfTile);
+  const int i2 = blockIdx.x * kQtfTile + lane;
   const int n2 = q.n2;
-  if (i1 >= n2 || i2 >= n2 || i2 < i1) return;
-  const double w1 = q.w2[i1], w2 = q.w2[i2], k1 = q.k2[i1], k2 = q.k2[i2];
-  if (w2 < w1) return;
+  if (i1 >= n2 || (int)blockIdx.x * kQtfTile + kQtfTile - 1 < i1) return;     // block-uniform
+  const bool active = i2 < n2 && i2 >= i1 && q.w2[i2] >= q.w2[i1];
+  const int i2s = active ? i2 : i1;         // inactive lanes compute a harmless valid pair
+  const double w1 = ldsd(q.w2 + i1), w2 = q.w2[i2s], k1 = ldsd(q.k2 + i1), k2 = q.k2[i2s];
   const double h = q.depth, rho = q.rho, g = q.g, beta = q.beta;
   cd Q[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) Q[i] = mk(0, 0);
   // ---- Pinkster IV: rotation of the first-order force (:1449-1456)
-  {
+  if (wv == 0) {
     cd th1[3], th2c[3], F1a[3], F1b[3], F2c[3], tmp1[3], tmp2[3];
-    ld3(wk.freq, FT_XI + 3, n2, i1, th1);
-    ld3(wk.freq, FT_XI + 3, n2, i2, th2c);
+    ld3s(wk.freq, FT_XI + 3, n2, i1, th1);
+    ld3(wk.freq, FT_XI + 3, n2, i2s, th2c);
 #pragma unroll
     for (int i = 0; i < 3; ++i) th2c[i] = cconj(th2c[i]);
     for (int part = 0; part < 2; ++part) {
-      ld3(wk.freq, FT_F1 + 3 * part, n2, i2, F2c);
-      ld3(wk.freq, FT_F1 + 3 * part, n2, i1, F1a);
+      ld3(wk.freq, FT_F1 + 3 * part, n2, i2s, F2c);
+      ld3s(wk.freq, FT_F1 + 3 * part, n2, i1, F1a);
 #pragma unroll
       for (int i = 0; i < 3; ++i) F2c[i] = cconj(F2c[i]);
       cross_cc(th1, F2c, tmp1);
@@ -362,87 +405,77 @@ __global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork
     aux2 = scl(add(g21, cconj(g12)), 0.5);
   }
   cd om1[3], om2[3];
-  ld3(wk.freq, FT_OM, n2, i1, om1);
-  ld3(wk.freq, FT_OM, n2, i2, om2);
+  ld3s(wk.freq, FT_OM, n2, i1, om1);
+  ld3(wk.freq, FT_OM, n2, i2s, om2);
   // OMEGA = -getH(i w th):  -H = [[0,-v2,v1],[v2,0,-v0],[-v1,v0,0]]
   const cd O1[9] = {mk(0, 0), scl(om1[2], -1), om1[1], om1[2], mk(0, 0), scl(om1[0], -1), scl(om1[1], -1), om1[0], mk(0, 0)};
   const cd O2[9] = {mk(0, 0), scl(om2[2], -1), om2[1], om2[2], mk(0, 0), scl(om2[0], -1), scl(om2[1], -1), om2[0], mk(0, 0)};
 
-  for (int m = 0; m < q.nmq; ++m) {
-    const int n0 = q.qmstart[m], n1 = q.qmstart[m + 1];
-    for (int n = n0; n < n1; ++n) {
-      const rh_c128* T = wk.node + (size_t)n * QT_COUNT * n2;
-      const double rx = qn(q, RH_QN_RX, n), ry = qn(q, RH_QN_RY, n), rz = qn(q, RH_QN_RZ, n);
-      const double qv[3] = {qn(q, RH_QN_QX, n), qn(q, RH_QN_QY, n), qn(q, RH_QN_QZ, n)};
-      double CM[9], CA[9], P12[9], QM[9];
-#pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        CM[i] = qn(q, RH_QN_CM + i, n);
-        CA[i] = qn(q, RH_QN_CA + i, n);
-        P12[i] = qn(q, RH_QN_P12 + i, n);
-        QM[i] = qn(q, RH_QN_QM + i, n);
-      }
-      const double rv = rho * qn(q, RH_QN_VI, n);
-      const double rve = rho * qn(q, RH_QN_VE, n) * qn(q, RH_QN_CAE, n);
-      const double ai = qn(q, RH_QN_AI, n);
-      // second-order potential acceleration and pressure at the node
-      cd acc2[3] = {mk(0, 0), mk(0, 0), mk(0, 0)}, p2 = mk(0, 0);
-      if (pot_on && rz <= 0) {
-        const double kxy = cosh(nk * (rz + h)) / cnh, kz = sinh(nk * (rz + h)) / cnh;
-        const double th = kx * rx + ky * ry + 0 * rz;
-        const cd ph = mk(cos(th), -sin(th));
-        const cd base = mul(scl(aux2, kxy), ph);
-        acc2[0] = scl(base, (w1 - w2) * kx);
-        acc2[1] = scl(base, (w1 - w2) * ky);
-        acc2[2] = mul(mul(scl(aux2, kz), ph), mk(0, (w1 - w2) * nk));
-        p2 = mul(base, mk(0, -rho * (w1 - w2)));
-      }
-      cd u1[3], u2[3], vp1[3], vp2[3], dr1[3], dr2[3], gp1[3], gp2[3], G1[9], G2[9];
-      ld3(T, QT_U, n2, i1, u1);
-      ld3(T, QT_U, n2, i2, u2);
-      ld3(T, QT_VP, n2, i1, vp1);
-      ld3(T, QT_VP, n2, i2, vp2);
-      ld3(T, QT_DR, n2, i1, dr1);
-      ld3(T, QT_DR, n2, i2, dr2);
-      ld3(T, QT_GP, n2, i1, gp1);
-      ld3(T, QT_GP, n2, i2, gp2);
-#pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        G1[i] = ld(T + (size_t)(QT_GU + i) * n2 + i1);
-        G2[i] = ld(T + (size_t)(QT_GU + i) * n2 + i2);
-      }
-      const cd va1 = ld(T + (size_t)QT_VA * n2 + i1), va2 = ld(T + (size_t)QT_VA * n2 + i2);
-      const cd dz1 = ld(T + (size_t)QT_DWDZ * n2 + i1), dz2 = ld(T + (size_t)QT_DWDZ * n2 + i2);
-      cd G2c[9];
-#pragma unroll
-      for (int i = 0; i < 9; ++i) G2c[i] = cconj(G2[i]);
-      cd f[3], t3[3], t4[3], t5[3];
-      // f_2ndPot (:1541-1542) + pressure and axial parts (:1587-1588)
+  // Node terms, one block per term group; each block names the tables it reads (the
+  // compiler merges the repeated loads).  Fencing the blocks apart to shorten live ranges
+  // was measured slower: loads can then no longer be issued ahead of the previous block.
+#pragma unroll 1
+  for (int n = wv; n < q.nq; n += NWV) {
+    const rh_c128* T = wk.node + (size_t)n * QT_COUNT * n2;
+    const double rx = qn(q, RH_QN_RX, n), ry = qn(q, RH_QN_RY, n), rz = qn(q, RH_QN_RZ, n);
+    const double qv[3] = {qn(q, RH_QN_QX, n), qn(q, RH_QN_QY, n), qn(q, RH_QN_QZ, n)};
+    const double rv = rho * qn(q, RH_QN_VI, n);
+    const double rve = rho * qn(q, RH_QN_VE, n) * qn(q, RH_QN_CAE, n);
+    const double ai = qn(q, RH_QN_AI, n);
+    // (1) second-order potential acceleration and pressure (f_2ndPot :1541-1542, :1587-1588)
+    if (pot_on && rz <= 0) {
+      cd acc2[3], p2;
+      const double kxy = cosh(nk * (rz + h)) / cnh, kz = sinh(nk * (rz + h)) / cnh;
+      const double th = kx * rx + ky * ry + 0 * rz;
+      const cd ph = mk(cos(th), -sin(th));
+      const cd base = mul(scl(aux2, kxy), ph);
+      acc2[0] = scl(base, (w1 - w2) * kx);
+      acc2[1] = scl(base, (w1 - w2) * ky);
+      acc2[2] = mul(mul(scl(aux2, kz), ph), mk(0, (w1 - w2) * nk));
+      p2 = mul(base, mk(0, -rho * (w1 - w2)));
+      double CM[9], QM[9];
+      ldm9(q, RH_QN_CM, n, CM);
+      ldm9(q, RH_QN_QM, n, QM);
+      cd f[3], t3[3], t4[3];
       rmv(CM, acc2, t3);
       rmv(QM, acc2, t4);
 #pragma unroll
       for (int i = 0; i < 3; ++i) f[i] = add(add(scl(t3[i], rv), scl(p2, ai * qv[i])), scl(t4[i], rve));
       acc6(Q, f, rx, ry, rz);
-      // convective acceleration (:1545-1546, 1589) and Bernoulli pressure drop (:1593-1594)
-      cd c1v[3], c2v[3], conv[3];
-      {
-        cd u2c[3] = {cconj(u2[0]), cconj(u2[1]), cconj(u2[2])};
-        cmv(G1, u2c, c1v);
-        cmv(G2c, u1, c2v);
+    }
+    // (2) convective acceleration (:1545-1546, 1589) and Bernoulli pressure drop (:1593-1594)
+    {
+      cd u1[3], u2c[3], vp1[3], vp2[3], G1[9], G2c[9], c1v[3], c2v[3], conv[3], t3[3], t4[3], t5[3], cu2[3], f[3];
+      ld3s(T, QT_U, n2, i1, u1);
+      ld3(T, QT_U, n2, i2s, u2c);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) conv[i] = scl(add(c1v[i], c2v[i]), 0.25);
+      for (int i = 0; i < 3; ++i) u2c[i] = cconj(u2c[i]);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        G1[i] = lds(T + (size_t)(QT_GU + i) * n2 + i1);
+        G2c[i] = cconj(ld(T + (size_t)(QT_GU + i) * n2 + i2s));
       }
-      rmv(CM, conv, t3);
-      rmv(QM, conv, t4);
+      cmv(G1, u2c, c1v);
+      cmv(G2c, u1, c2v);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) conv[i] = scl(add(c1v[i], c2v[i]), 0.25);
+      double M9[9];
+      ldm9(q, RH_QN_CM, n, M9);
+      rmv(M9, conv, t3);
+      ldm9(q, RH_QN_QM, n, M9);
+      rmv(M9, conv, t4);
+      ld3s(T, QT_VP, n2, i1, vp1);
+      ld3(T, QT_VP, n2, i2s, vp2);
       cd ur1[3], ur2[3];
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         ur1[i] = sub(u1[i], vp1[i]);
-        ur2[i] = sub(u2[i], vp2[i]);
+        ur2[i] = sub(cconj(u2c[i]), vp2[i]);
       }
-      rmv(P12, ur1, t5);
-      cd cu2[3];
-      rmv(CA, ur2, cu2);
+      ldm9(q, RH_QN_P12, n, M9);
+      rmv(M9, ur1, t5);
+      ldm9(q, RH_QN_CA, n, M9);
+      rmv(M9, ur2, cu2);
       cd pd = mk(0, 0);
 #pragma unroll
       for (int i = 0; i < 3; ++i) pd = add(pd, mul(t5[i], cconj(cu2[i])));
@@ -450,111 +483,152 @@ __global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork
 #pragma unroll
       for (int i = 0; i < 3; ++i) f[i] = add(add(scl(t3[i], rv), scl(t4[i], rve)), scl(pd, ai * qv[i]));
       acc6(Q, f, rx, ry, rz);
-      // Rainey axial divergence (raft/helpers.py:228-251)
-      {
-        cd up1[3], up2[3];
-        const cd s1 = add(add(scl(u1[0], qv[0]), scl(u1[1], qv[1])), scl(u1[2], qv[2]));
-        const cd s2 = add(add(scl(u2[0], qv[0]), scl(u2[1], qv[1])), scl(u2[2], qv[2]));
-        cd a[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          up1[i] = sub(u1[i], scl(s1, qv[i]));
-          up2[i] = sub(u2[i], scl(s2, qv[i]));
-          a[i] = scl(add(mul(dz1, cconj(sub(up2[i], vp2[i]))), mul(cconj(dz2), sub(up1[i], vp1[i]))), 0.25);
-        }
-        const cd aq = add(add(scl(a[0], qv[0]), scl(a[1], qv[1])), scl(a[2], qv[2]));
-#pragma unroll
-        for (int i = 0; i < 3; ++i) a[i] = sub(a[i], scl(aq, qv[i]));
-        rmv(CA, a, t3);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) f[i] = scl(t3[i], rv);
-        acc6(Q, f, rx, ry, rz);
-      }
-      // body motion in the first-order field (:1552-1553, 1590-1592)
-      {
-        cd d2c[3] = {cconj(dr2[0]), cconj(dr2[1]), cconj(dr2[2])};
-        cd a1[3], a2[3], an[3];
-        cmv(G1, d2c, a1);
-        cmv(G2c, dr1, a2);
-        // grad du/dt = i w grad u: 0.25 (i w1 G1) conj(dr2) + 0.25 conj(i w2 G2) dr1
-#pragma unroll
-        for (int i = 0; i < 3; ++i) an[i] = add(scl(iw(w1, a1[i]), 0.25), scl(iw(-w2, a2[i]), 0.25));
-        rmv(CM, an, t3);
-        rmv(QM, an, t4);
-        cd pn = mk(0, 0), pm = mk(0, 0);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          pn = add(pn, mul(gp1[i], cconj(dr2[i])));
-          pm = add(pm, mul(cconj(gp2[i]), dr1[i]));
-        }
-        const cd pnab = add(scl(pn, 0.25), scl(pm, 0.25));
-#pragma unroll
-        for (int i = 0; i < 3; ++i) f[i] = add(add(scl(t3[i], rv), scl(t4[i], rve)), scl(pnab, ai * qv[i]));
-        acc6(Q, f, rx, ry, rz);
-      }
-      // Rainey body-rotation terms (:1556-1575)
-      {
-        cd x1[3], x2[3], y1[3], y2[3], s[3];
-        cd va2q[3] = {cconj(scl(va2, qv[0])), cconj(scl(va2, qv[1])), cconj(scl(va2, qv[2]))};
-        cd va1q[3] = {scl(va1, qv[0]), scl(va1, qv[1]), scl(va1, qv[2])};
-        cd O2c[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) O2c[i] = cconj(O2[i]);
-        cmv(O1, va2q, x1);
-        cmv(O2c, va1q, x2);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) s[i] = add(x1[i], x2[i]);
-        rmv(CA, s, t3);
-        cd fr[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) fr[i] = scl(scl(t3[i], -0.25 * 2), rv);
-        cd V1[9], V2c[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-          V1[i] = add(G1[i], O1[i]);
-          V2c[i] = cconj(add(G2[i], O2[i]));
-        }
-        // aux = 0.25 (V1 conj(CaM u2a) + conj(V2) CaM u1a); aux -= qMat aux
-        cd cu1[3];
-        rmv(CA, ur1, cu1);
-        cd cu2c[3] = {cconj(cu2[0]), cconj(cu2[1]), cconj(cu2[2])};
-        cmv(V1, cu2c, x1);
-        cmv(V2c, cu1, x2);
-        cd ax[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) ax[i] = scl(add(x1[i], x2[i]), 0.25);
-        rmv(QM, ax, t4);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) fr[i] = add(fr[i], scl(sub(ax[i], t4[i]), rv));
-        // u_aux -= qMat u_aux ; aux = 0.25 (CaM V1 conj(u2a) + CaM conj(V2) u1a)
-        cd w1a[3], w2a[3];
-        rmv(QM, ur1, t4);
-        rmv(QM, ur2, t5);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          w1a[i] = sub(ur1[i], t4[i]);
-          w2a[i] = cconj(sub(ur2[i], t5[i]));
-        }
-        cmv(V1, w2a, x1);
-        cmv(V2c, w1a, x2);
-        rmv(CA, x1, y1);
-        rmv(CA, x2, y2);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) fr[i] = add(fr[i], scl(scl(add(y1[i], y2[i]), 0.25), -rv));
-        acc6(Q, fr, rx, ry, rz);
-      }
     }
-    // ---- waterline relative-elevation force (:1602-1630)
+    // (3) Rainey axial divergence (raft/helpers.py:228-251)
+    {
+      cd u1[3], u2[3], vp1[3], vp2[3], up1[3], up2[3], a[3], t3[3], f[3];
+      ld3s(T, QT_U, n2, i1, u1);
+      ld3(T, QT_U, n2, i2s, u2);
+      ld3s(T, QT_VP, n2, i1, vp1);
+      ld3(T, QT_VP, n2, i2s, vp2);
+      const cd dz1 = lds(T + (size_t)QT_DWDZ * n2 + i1), dz2 = ld(T + (size_t)QT_DWDZ * n2 + i2s);
+      const cd s1 = add(add(scl(u1[0], qv[0]), scl(u1[1], qv[1])), scl(u1[2], qv[2]));
+      const cd s2 = add(add(scl(u2[0], qv[0]), scl(u2[1], qv[1])), scl(u2[2], qv[2]));
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        up1[i] = sub(u1[i], scl(s1, qv[i]));
+        up2[i] = sub(u2[i], scl(s2, qv[i]));
+        a[i] = scl(add(mul(dz1, cconj(sub(up2[i], vp2[i]))), mul(cconj(dz2), sub(up1[i], vp1[i]))), 0.25);
+      }
+      const cd aq = add(add(scl(a[0], qv[0]), scl(a[1], qv[1])), scl(a[2], qv[2]));
+#pragma unroll
+      for (int i = 0; i < 3; ++i) a[i] = sub(a[i], scl(aq, qv[i]));
+      double CA[9];
+      ldm9(q, RH_QN_CA, n, CA);
+      rmv(CA, a, t3);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) f[i] = scl(t3[i], rv);
+      acc6(Q, f, rx, ry, rz);
+    }
+    // (4) body motion in the first-order field (:1552-1553, 1590-1592)
+    {
+      cd dr1[3], d2c[3], G1[9], G2c[9], a1[3], a2[3], an[3], t3[3], t4[3], f[3];
+      ld3s(T, QT_DR, n2, i1, dr1);
+      ld3(T, QT_DR, n2, i2s, d2c);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) d2c[i] = cconj(d2c[i]);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        G1[i] = lds(T + (size_t)(QT_GU + i) * n2 + i1);
+        G2c[i] = cconj(ld(T + (size_t)(QT_GU + i) * n2 + i2s));
+      }
+      cmv(G1, d2c, a1);
+      cmv(G2c, dr1, a2);
+      // grad du/dt = i w grad u: 0.25 (i w1 G1) conj(dr2) + 0.25 conj(i w2 G2) dr1
+#pragma unroll
+      for (int i = 0; i < 3; ++i) an[i] = add(scl(iw(w1, a1[i]), 0.25), scl(iw(-w2, a2[i]), 0.25));
+      double M9[9];
+      ldm9(q, RH_QN_CM, n, M9);
+      rmv(M9, an, t3);
+      ldm9(q, RH_QN_QM, n, M9);
+      rmv(M9, an, t4);
+      cd gp1[3], gp2[3];
+      ld3s(T, QT_GP, n2, i1, gp1);
+      ld3(T, QT_GP, n2, i2s, gp2);
+      cd pn = mk(0, 0), pm = mk(0, 0);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        pn = add(pn, mul(gp1[i], d2c[i]));
+        pm = add(pm, mul(cconj(gp2[i]), dr1[i]));
+      }
+      const cd pnab = add(scl(pn, 0.25), scl(pm, 0.25));
+#pragma unroll
+      for (int i = 0; i < 3; ++i) f[i] = add(add(scl(t3[i], rv), scl(t4[i], rve)), scl(pnab, ai * qv[i]));
+      acc6(Q, f, rx, ry, rz);
+    }
+    // (5) Rainey body-rotation terms (:1556-1575)
+    {
+      cd x1[3], x2[3], y1[3], y2[3], s[3], t3[3], t4[3], t5[3], fr[3];
+      const cd va1 = lds(T + (size_t)QT_VA * n2 + i1), va2 = ld(T + (size_t)QT_VA * n2 + i2s);
+      cd va2q[3] = {cconj(scl(va2, qv[0])), cconj(scl(va2, qv[1])), cconj(scl(va2, qv[2]))};
+      cd va1q[3] = {scl(va1, qv[0]), scl(va1, qv[1]), scl(va1, qv[2])};
+      cd O2c[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) O2c[i] = cconj(O2[i]);
+      cmv(O1, va2q, x1);
+      cmv(O2c, va1q, x2);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) s[i] = add(x1[i], x2[i]);
+      double CA[9], QM[9];
+      ldm9(q, RH_QN_CA, n, CA);
+      rmv(CA, s, t3);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) fr[i] = scl(scl(t3[i], -0.25 * 2), rv);
+      cd V1[9], V2c[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        V1[i] = add(lds(T + (size_t)(QT_GU + i) * n2 + i1), O1[i]);
+        V2c[i] = cconj(add(ld(T + (size_t)(QT_GU + i) * n2 + i2s), O2[i]));
+      }
+      cd ur1[3], ur2[3];
+      {
+        cd u1[3], u2[3], vp1[3], vp2[3];
+        ld3s(T, QT_U, n2, i1, u1);
+        ld3(T, QT_U, n2, i2s, u2);
+        ld3s(T, QT_VP, n2, i1, vp1);
+        ld3(T, QT_VP, n2, i2s, vp2);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          ur1[i] = sub(u1[i], vp1[i]);
+          ur2[i] = sub(u2[i], vp2[i]);
+        }
+      }
+      // aux = 0.25 (V1 conj(CaM u2a) + conj(V2) CaM u1a); aux -= qMat aux
+      cd cu1[3], cu2c[3];
+      rmv(CA, ur1, cu1);
+      rmv(CA, ur2, cu2c);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) cu2c[i] = cconj(cu2c[i]);
+      cmv(V1, cu2c, x1);
+      cmv(V2c, cu1, x2);
+      cd ax[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) ax[i] = scl(add(x1[i], x2[i]), 0.25);
+      ldm9(q, RH_QN_QM, n, QM);
+      rmv(QM, ax, t4);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) fr[i] = add(fr[i], scl(sub(ax[i], t4[i]), rv));
+      // u_aux -= qMat u_aux ; aux = 0.25 (CaM V1 conj(u2a) + CaM conj(V2) u1a)
+      cd w1a[3], w2a[3];
+      rmv(QM, ur1, t4);
+      rmv(QM, ur2, t5);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        w1a[i] = sub(ur1[i], t4[i]);
+        w2a[i] = cconj(sub(ur2[i], t5[i]));
+      }
+      cmv(V1, w2a, x1);
+      cmv(V2c, w1a, x2);
+      rmv(CA, x1, y1);
+      rmv(CA, x2, y2);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) fr[i] = add(fr[i], scl(scl(add(y1[i], y2[i]), 0.25), -rv));
+      acc6(Q, fr, rx, ry, rz);
+    }
+  }
+  // ---- waterline relative-elevation force (:1602-1630)
+#pragma unroll 1
+  for (int m = wv; m < q.nmq; m += NWV) {
     if (qm(q, RH_QM_WL, m) != 0.0) {
       const rh_c128* W = wk.wl + (size_t)m * WT_COUNT * n2;
-      const cd e1 = ld(W + (size_t)WT_ETAR * n2 + i1), e2c = cconj(ld(W + (size_t)WT_ETAR * n2 + i2));
+      const cd e1 = lds(W + (size_t)WT_ETAR * n2 + i1), e2c = cconj(ld(W + (size_t)WT_ETAR * n2 + i2s));
       cd ud1[3], ud2[3], a1[3], a2[3], ge1[3], ge2[3];
-      ld3(W, WT_UD, n2, i1, ud1);
-      ld3(W, WT_UD, n2, i2, ud2);
-      ld3(W, WT_A, n2, i1, a1);
-      ld3(W, WT_A, n2, i2, a2);
-      ld3(W, WT_GE, n2, i1, ge1);
-      ld3(W, WT_GE, n2, i2, ge2);
+      ld3s(W, WT_UD, n2, i1, ud1);
+      ld3(W, WT_UD, n2, i2s, ud2);
+      ld3s(W, WT_A, n2, i1, a1);
+      ld3(W, WT_A, n2, i2s, a2);
+      ld3s(W, WT_GE, n2, i1, ge1);
+      ld3(W, WT_GE, n2, i2s, ge2);
       double CM[9], CA[9];
 #pragma unroll
       for (int i = 0; i < 9; ++i) {
@@ -577,71 +651,95 @@ __global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork
       }
       acc6(Q, fo, qm(q, RH_QM_RIX, m), qm(q, RH_QM_RIY, m), qm(q, RH_QM_RIZ, m));
     }
-    // ---- Kim & Yue second-order diffraction (raft/raft_member.py:1090-1205)
-    if (qm(q, RH_QM_KAY, m) != 0.0) {
-      const int r0 = q.kstart[m], r1 = q.kstart[m + 1];
-      const double cb = cos(beta), sb = sin(beta);
-      const double kkx = k1 * cb - k2 * cb, kky = k1 * sb - k2 * sb;
+  }
+  // ---- Kim & Yue second-order diffraction (raft/raft_member.py:1090-1205), one radius row
+  // at a time; conj(F) when k1 < k2 is applied per row (conj is exact and
+  // linear, so it equals conj of the member sum)
+  {
+    const bool cj = k1 < k2;
+    const double cb = cos(beta), sb = sin(beta);
+    const double kkx = k1 * cb - k2 * cb, kky = k1 * sb - k2 * sb;
+    int m = 0;
+#pragma unroll 1
+    for (int ir = NWV - 1 - wv; ir < q.nkr; ir += NWV) {
+      while (ldsi(q.kstart + m + 1) <= ir) ++m;          // member of row ir (rows ascend)
+      const int r0 = ldsi(q.kstart + m);
       const double wx = qm(q, RH_QM_WLX, m), wy = qm(q, RH_QM_WLY, m), wz = qm(q, RH_QM_WLZ, m);
       const double thp = kkx * wx + kky * wy + 0 * wz;
       const cd ph = mk(cos(thp), -sin(thp));
       const double pf[3] = {qm(q, RH_QM_PFX, m), qm(q, RH_QM_PFY, m), qm(q, RH_QM_PFZ, m)};
-      cd Fk[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) Fk[i] = mk(0, 0);
-      for (int ir = r0; ir < r1; ++ir) {
-        const double R = q.kray[RH_KR_R * q.nkr + ir];
-        const rh_c128* D1 = wk.hinv + ((size_t)ir * n2 + i1) * 12;
-        const rh_c128* D2 = wk.hinv + ((size_t)ir * n2 + i2) * 12;
-        const double k1R = k1 * R, k2R = k2 * R;
-        double sre;
-        double px, py, pz;
-        if (ir == r0) {       // waterline term (:1133-1149)
-          const cd c0 = mk(0, -rho * g * R * 2 / M_PI / (k1R * k2R));
-          cd s = mk(0, 0);
+      const double R = ldsd(q.kray + RH_KR_R * q.nkr + ir);
+      const rh_c128* D1 = wk.hinv + ((size_t)ir * n2 + i1) * 12;
+      const rh_c128* D2 = wk.hinv + ((size_t)ir * n2 + i2s) * 12;
+      const double k1R = k1 * R, k2R = k2 * R;
+      double sre;
+      double px, py, pz;
+      if (ir == r0) {       // waterline term (:1133-1149)
+        const cd c0 = mk(0, -rho * g * R * 2 / M_PI / (k1R * k2R));
+        cd s = mk(0, 0);
 #pragma unroll 1
-          for (int nn = 0; nn <= 10; ++nn) s = add(s, kay_omega(D1, D2, nn));
-          sre = mul(c0, s).r;
-          px = wx;
-          py = wy;
-          pz = wz;
-        } else {              // node-interval Bernoulli term (:1155-1200)
-          const double z1 = q.kray[RH_KR_Z1 * q.nkr + ir], z2 = q.kray[RH_KR_Z2 * q.nkr + ir];
-          const double H = h / R;
-          const double k1h = k1R * H, k2h = k2R * H;
-          double Im, Ip;
-          const double a2 = sinh((k1 + k2) * (z2 + h)) / (k1h + k2h), a1 = sinh((k1 + k2) * (z1 + h)) / (k1h + k2h);
-          if (w1 == w2) {
-            Im = 0.5 * (a2 - (z2 + h) / h - a1 + (z1 + h) / h);
-            Ip = 0.5 * (a2 + (z2 + h) / h - a1 - (z1 + h) / h);
-          } else {
-            const double d2 = sinh((k1 - k2) * (z2 + h)) / (k1h - k2h), d1 = sinh((k1 - k2) * (z1 + h)) / (k1h - k2h);
-            Im = 0.5 * (a2 - d2 - a1 + d1);
-            Ip = 0.5 * (a2 + d2 - a1 - d1);
-          }
-          const double* t1 = wk.kayt + ((size_t)ir * n2 + i1) * 2;
-          const double* t2 = wk.kayt + ((size_t)ir * n2 + i2) * 2;
-          // coef / (cosh(k1 R H) cosh(k2 R H)) and Ip / (k1R k2R), hoisted out of the n sum
-          const double cc = k1h * k2h / (t1[1] * t2[1] * t1[0] * t2[0]);
-          const double ipr = Ip / (k1R * k2R);
-          const cd c0 = mk(0, rho * g * R * 2 / M_PI / (k1R * k2R));
-          cd s = mk(0, 0);
-#pragma unroll 1
-          for (int nn = 0; nn <= 10; ++nn) s = add(s, scl(kay_omega(D1, D2, nn), cc * (Im + ipr * (nn * (nn + 1)))));
-          sre = mul(c0, s).r;
-          px = q.kray[RH_KR_MX * q.nkr + ir];
-          py = q.kray[RH_KR_MY * q.nkr + ir];
-          pz = q.kray[RH_KR_MZ * q.nkr + ir];
+        for (int nn = 0; nn <= 10; ++nn) s = add(s, kay_omega(D1, D2, nn));
+        sre = mul(c0, s).r;
+        px = wx;
+        py = wy;
+        pz = wz;
+      } else {              // node-interval Bernoulli term (:1155-1200)
+        const double z1 = ldsd(q.kray + RH_KR_Z1 * q.nkr + ir), z2 = ldsd(q.kray + RH_KR_Z2 * q.nkr + ir);
+        const double H = h / R;
+        const double k1h = k1R * H, k2h = k2R * H;
+        double Im, Ip;
+        const double a2 = sinh((k1 + k2) * (z2 + h)) / (k1h + k2h), a1 = sinh((k1 + k2) * (z1 + h)) / (k1h + k2h);
+        if (w1 == w2) {
+          Im = 0.5 * (a2 - (z2 + h) / h - a1 + (z1 + h) / h);
+          Ip = 0.5 * (a2 + (z2 + h) / h - a1 - (z1 + h) / h);
+        } else {
+          const double d2 = sinh((k1 - k2) * (z2 + h)) / (k1h - k2h), d1 = sinh((k1 - k2) * (z1 + h)) / (k1h - k2h);
+          Im = 0.5 * (a2 - d2 - a1 + d1);
+          Ip = 0.5 * (a2 + d2 - a1 - d1);
         }
-        const cd Fs = scl(ph, sre);    // real part times the phase of the waterline point
-        cd fv[3] = {scl(Fs, pf[0]), scl(Fs, pf[1]), scl(Fs, pf[2])};
-        acc6(Fk, fv, px, py, pz);
+        const double* t1 = wk.kayt + ((size_t)ir * n2 + i1) * 2;
+        const double* t2 = wk.kayt + ((size_t)ir * n2 + i2s) * 2;
+        // coef / (cosh(k1 R H) cosh(k2 R H)) and Ip / (k1R k2R), hoisted out of the n sum
+        const double cc = k1h * k2h / (ldsd(t1 + 1) * t2[1] * ldsd(t1) * t2[0]);
+        const double ipr = Ip / (k1R * k2R);
+        const cd c0 = mk(0, rho * g * R * 2 / M_PI / (k1R * k2R));
+        cd s = mk(0, 0);
+#pragma unroll 1
+        for (int nn = 0; nn <= 10; ++nn) s = add(s, scl(kay_omega(D1, D2, nn), cc * (Im + ipr * (nn * (nn + 1)))));
+        sre = mul(c0, s).r;
+        px = ldsd(q.kray + RH_KR_MX * q.nkr + ir);
+        py = ldsd(q.kray + RH_KR_MY * q.nkr + ir);
+        pz = ldsd(q.kray + RH_KR_MZ * q.nkr + ir);
       }
-      const bool cj = k1 < k2;
+      const cd Fs = scl(ph, sre);    // real part times the phase of the waterline point
+      cd fv[3] = {scl(Fs, pf[0]), scl(Fs, pf[1]), scl(Fs, pf[2])};
+      if (cj) {
 #pragma unroll
-      for (int i = 0; i < 6; ++i) Q[i] = add(Q[i], cj ? cconj(Fk[i]) : Fk[i]);
+        for (int i = 0; i < 3; ++i) fv[i] = cconj(fv[i]);
+      }
+      acc6(Q, fv, px, py, pz);
     }
   }
+  // ---- the NWV partial sums meet in LDS; wave 0 adds them in wave order
+  if (NWV > 1) {
+    if (wv > 0) {
+      double* r = red + (size_t)(wv - 1) * 12 * kQtfTile;
+#pragma unroll
+      for (int d = 0; d < 6; ++d) {
+        r[(2 * d) * kQtfTile + lane] = Q[d].r;
+        r[(2 * d + 1) * kQtfTile + lane] = Q[d].i;
+      }
+    }
+    __syncthreads();
+    if (wv > 0) return;
+#pragma unroll 1
+    for (int v = 0; v < NWV - 1; ++v) {
+      const double* r = red + (size_t)v * 12 * kQtfTile;
+#pragma unroll
+      for (int d = 0; d < 6; ++d) Q[d] = add(Q[d], mk(r[(2 * d) * kQtfTile + lane], r[(2 * d + 1) * kQtfTile + lane]));
+    }
+  }
+  if (!active) return;
   // Hermitian fill (:1639-1640): qtf + conj(qtf).T - diag(conj(diag(qtf)))
   rh_c128* up = qtf + ((size_t)i1 * n2 + i2) * 6;
   if (!mirror) {
@@ -659,6 +757,10 @@ __global__ __launch_bounds__(kQtfTile) void k_qtf_pairs(rh_qtf_design q, QtfWork
     }
   }
 }
+
+template __global__ void k_qtf_pairs<1>(rh_qtf_design, QtfWork, rh_c128*, int, int, int);
+template __global__ void k_qtf_pairs<2>(rh_qtf_design, QtfWork, rh_c128*, int, int, int);
+template __global__ void k_qtf_pairs<4>(rh_qtf_design, QtfWork, rh_c128*, int, int, int);
 
 // Hermitian fill of a row-sharded QTF after the exchange: lower[i2][i1] = conj(upper[i1][i2]);
 // the diagonal keeps q + conj(q) - conj(q) == q exactly (raft/raft_fowt.py:1639-1640)

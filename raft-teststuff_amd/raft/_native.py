@@ -94,6 +94,7 @@ def lib():
                                         ctypes.c_int, _p, _p, ctypes.c_longlong, _p],
                 "rh_qtf_hermitian_fill": [_p, ctypes.c_int, _p, _p],
                 "rh_set_solver": [ctypes.c_int],
+                "rh_set_qtf_waves": [ctypes.c_int],
                 "rh_force_2nd": [_p, ctypes.c_int, _p, _p, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p],
             }.items():
                 fn = getattr(L, name)

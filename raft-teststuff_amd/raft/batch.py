@@ -81,6 +81,16 @@ class DesignBatch:
         return solve_batch(self.dds, cs, self.nIter, self.XiStart, tol, want=want, prepared=prepared)
 
 
+def sweep_shard(design_idx, rank, world):
+    """This rank's contiguous block [lo, hi) of a design-major case list and the design
+    range [dlo, dhi) it touches (a design cut by a block boundary is prepared by both ranks)."""
+    from .parallel import case_shard
+    lo, hi = case_shard(len(design_idx), rank, world)
+    if hi <= lo:
+        return lo, hi, 0, 0
+    return lo, hi, int(design_idx[lo]), int(design_idx[hi - 1]) + 1
+
+
 def sweep_cases(n_designs, sea_states):
     """Every design paired with every sea state: (design index, case) lists, design-major."""
     idx = np.repeat(np.arange(n_designs, dtype=np.int32), len(sea_states))

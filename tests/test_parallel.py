@@ -54,6 +54,50 @@ def test_case_shard_partitions_every_case_once():
             assert max(pairs) - min(pairs) <= n2                 # snake deal: within one row
 
 
+def test_sweep_shard_covers_every_case_and_its_design():
+    """C5 sharding (bench.py bench_c5): contiguous blocks of the design-major case list; a
+    rank's design range holds every design its cases reference, designs cut by a block
+    boundary are prepared by both neighbours and by no other rank."""
+    from raft.batch import sweep_cases, sweep_shard
+    from raft.sweep import sea_state_grid
+    for nd, ns in [(250, 40), (3, 2), (7, 5)]:
+        idx, cases = sweep_cases(nd, sea_state_grid()[:ns])
+        assert len(cases) == nd * ns and np.all(np.diff(idx) >= 0)
+        for world in [1, 2, 3, 8]:
+            seen = np.zeros(len(idx), dtype=int)
+            prepared = np.zeros(nd, dtype=int)
+            for r in range(world):
+                lo, hi, dlo, dhi = sweep_shard(idx, r, world)
+                seen[lo:hi] += 1
+                prepared[dlo:dhi] += 1
+                if hi > lo:
+                    assert dlo <= idx[lo:hi].min() and idx[lo:hi].max() < dhi
+            assert np.all(seen == 1)
+            assert prepared.min() >= 1 and prepared.max() <= 2
+
+
+def test_sweep_variant_restates_parametersweep():
+    """The five variables land where raft/parametersweep.py:56-88 puts them; multipliers of 1
+    leave the design unchanged."""
+    import json
+    import os
+    from raft.sweep import sweep_baseline, sweep_variant
+    with open(os.path.join(os.path.dirname(__file__), "golden", "designs", "VolturnUS-S_example.json")) as fh:
+        base = json.load(fh)
+    same = sweep_variant(base, [1, 1, 1, 1, 1])
+    for a, b in zip(same["platform"]["members"], base["platform"]["members"]):
+        assert np.allclose(np.asarray(a["rA"], float), np.asarray(b["rA"], float))
+        assert np.allclose(np.asarray(a["rB"], float), np.asarray(b["rB"], float))
+        assert np.allclose(np.asarray(a["d"], float), np.asarray(b["d"], float))
+    v = sweep_variant(base, [1.1, 0.9, 1.2, 0.8, 1.05])
+    b0, b1 = sweep_baseline(base), sweep_baseline(v)
+    for k, f in zip(["ccD", "ocD", "T", "ocR", "pH"], [1.1, 0.9, 1.2, 0.8, 1.05]):
+        assert np.isclose(b1[k], b0[k] * f), k
+    m = v["platform"]["members"]
+    assert np.isclose(m[2]["rB"][0], m[1]["rA"][0] - m[1]["d"] / 2)     # pontoon meets the outer column
+    assert base["platform"]["members"][0]["d"] == b0["ccD"]            # the base design is not mutated
+
+
 def _gather_check(rank, world):
     from raft.parallel import case_shard, gather_cases
     n = 11

@@ -14,7 +14,7 @@ timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout
 rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/gpu_tests.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-c5 > $OUT/bench_prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"
 if [ $rc -ne 0 ]; then tail -5 $OUT/bench_prof.log; exit $rc; fi
 for wl in solve qtf; do

@@ -12,17 +12,26 @@ sys.path.insert(0, os.path.join(ROOT, "raft-teststuff_amd"))
 def main(tag):
     import torch
     import bench
+    from raft import _native as N
     T, f, qd, dd, X, M66, w2, k2, nkay, nwl = bench.build_qtf(0)
-    for _ in range(2):
-        qd.qtf(dd.w, X, M66)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        qd.qtf(dd.w, X, M66)
-    e1.record()
-    torch.cuda.synchronize()
-    print(f"{tag:10s} QTF {e0.elapsed_time(e1) / 10:8.3f} ms", flush=True)
+    ref = None
+    for waves in ((4,) if tag == "pmc" else (1, 2, 4)):     # PMC passes: the default kernel only
+        N.check(N.lib().rh_set_qtf_waves(waves), "rh_set_qtf_waves")
+        for _ in range(2):
+            q = qd.qtf(dd.w, X, M66)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            q = qd.qtf(dd.w, X, M66)
+        e1.record()
+        torch.cuda.synchronize()
+        qh = q.cpu().numpy()
+        if ref is None:
+            ref = qh
+        d = np.abs(qh - ref).max() / np.abs(ref).max()
+        print(f"{tag:10s} waves={waves} QTF {e0.elapsed_time(e1) / 10:8.3f} ms  maxrel vs waves=1 {d:.2e}", flush=True)
+    N.check(N.lib().rh_set_qtf_waves(4), "rh_set_qtf_waves")
 
 
 if __name__ == "__main__":
