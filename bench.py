@@ -42,6 +42,27 @@ def pmc_traffic(kernel):
     return None
 
 
+L2_PEAK = 34.5e12     # MI355X aggregate L2 bandwidth, B/s (MI355X_MICROARCH.md, L2 per XCD)
+
+
+def pmc_l2(kernel, kernel_ms):
+    """L2 request traffic of `kernel` per launch from PMC_SUMMARY: (TCC_HIT + TCC_MISS) x 128 B
+    and its rate over the measured launch time, or None."""
+    try:
+        with open(PMC_SUMMARY) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    for name, v in d.items():
+        c = v.get("counters", {})
+        if kernel in name and "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+            b = 128.0 * (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+            rate = b / (kernel_ms * 1e-3)
+            return {"bytes": b, "TB_per_s": rate / 1e12, "peak_TB_per_s": L2_PEAK / 1e12, "frac": rate / L2_PEAK,
+                    "hit_rate": c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])}
+    return None
+
+
 def solve_kernel_name(nw):
     """The kernel rh_solve_cases launches for this grid (dispatch in rh_abi.hip)."""
     if nw <= 1024:
@@ -379,6 +400,7 @@ def main():
                    "nodes_circ_rect": [nc, nr], "nIter": int(m.nIter), "parallelism": f"case-sharded x{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP64, "traffic": pmc_traffic(solve_kernel_name(dd.nw).split("<")[0]),
+                     "l2": pmc_l2(solve_kernel_name(dd.nw).split("<")[0], kern_ms),
                      "kernel": solve_kernel_name(dd.nw), "kernel_ms": kern_ms,
                      "flops_per_launch": flops,
                      "note": "FP64 VALU bound (peak = MI355X FP64 vector = matrix rate); algorithmic FLOPs from "
