@@ -240,7 +240,26 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
 C5_DESIGNS = 250
 
 
-def bench_c5(device, steps, world, rank, dist):
+def c5_base():
+    """The C5 baseline design (VolturnUS-S_example at nw=1000) and its mooring stiffness."""
+    with open(os.path.join(ROOT, "tests", "golden", "designs", "VolturnUS-S_example.json")) as fh:
+        base = json.load(fh)
+    base["settings"]["min_freq"] = 0.0002
+    return base, np.load(os.path.join(ROOT, "tests", "golden", "c2_nw1000.npz"))["C_moor"]
+
+
+def c5_pool(world):
+    """Host workers for the C5 design preparation, started before the GPU is initialised:
+    min(16, this rank's share of the cores).  Each memoises the site's dispersion solution
+    (the per-site cost; the single-process path has it warm from the C2 leg)."""
+    from raft import Model
+    from raft.batch import host_pool
+    base, _ = c5_base()
+    P = max(1, min(16, len(os.sched_getaffinity(0)) // max(1, world)))
+    return host_pool(P, grids=[(Model.frequency_grid(base), float(base["site"]["water_depth"]))]), P
+
+
+def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
     """C5 (BASELINE.json configs[4]): 250 parametersweep-style VolturnUS-S_example variants
     (raft/sweep.py) x 40 sea states (Hs 2..10 x Tp 6..20) = 10,000 cases at nw = 1000.
     The design-major case list is split in contiguous blocks over the ranks; a rank prepares
@@ -252,10 +271,7 @@ def bench_c5(device, steps, world, rank, dist):
     from raft.batch import DesignBatch, sweep_cases, sweep_shard
     from raft.parallel import gather_cases
     from raft.sweep import sea_state_grid, sweep_multipliers, sweep_variant
-    with open(os.path.join(ROOT, "tests", "golden", "designs", "VolturnUS-S_example.json")) as fh:
-        base = json.load(fh)
-    base["settings"]["min_freq"] = 0.0002
-    C_moor = np.load(os.path.join(ROOT, "tests", "golden", "c2_nw1000.npz"))["C_moor"]
+    base, C_moor = c5_base()
     mult = sweep_multipliers(C5_DESIGNS)
     grid = sea_state_grid()
     idx_all, cases_all = sweep_cases(C5_DESIGNS, grid)
@@ -268,7 +284,7 @@ def bench_c5(device, steps, world, rank, dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    B = DesignBatch(variants, statics={"C_moor": C_moor}, device=device)
+    B = DesignBatch(variants, statics={"C_moor": C_moor}, device=device, pool=pool)
     cs = B.case_set(local_idx, cases_all[lo:hi])
     from raft.solver import prepare_batch
     prep = prepare_batch(B.dds, cs)                  # device wave tables per (design, heading)
@@ -309,7 +325,8 @@ def bench_c5(device, steps, world, rank, dist):
             "iterations_mean": float(iters.mean()),
             "config": {"workload": "C5: 250 VolturnUS-S_example parametersweep variants (5 variables U(0.75,1.25)) "
                                    "x 40 sea states, nw=1000", "nw": B.nw,
-                       "parallelism": f"case-block-sharded x{world} + all-gather (std, PSD, iterations)"}}
+                       "parallelism": f"case-block-sharded x{world} + all-gather (std, PSD, iterations)",
+                       "host_prep_workers_per_rank": nproc}}
 
 
 def main():
@@ -329,6 +346,7 @@ def main():
     baselines = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         baselines = cpu_baselines()          # before this process initialises the GPU
+    pool, nproc = c5_pool(world) if not args.no_c5 else (None, 1)   # likewise
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -412,7 +430,10 @@ def main():
     if not args.no_qtf:
         line["qtf"] = bench_qtf(device, max(3, args.steps // 4), 1, world, rank, dist)
     if not args.no_c5:
-        line["c5"] = bench_c5(device, max(3, args.steps // 4), world, rank, dist)
+        line["c5"] = bench_c5(device, max(3, args.steps // 4), world, rank, dist, pool, nproc)
+    if pool is not None:
+        pool.close()
+        pool.join()
     if baselines is not None:
         line["cpu_baseline"] = baselines[0]
         if "qtf" in line:

@@ -124,6 +124,12 @@ typedef struct {
   const rh_c128* Xi_init; /* [ncase][6][nw] initial XiLast instead of XiStart, or NULL          */
   int first_iter;         /* initial value of the iteration counter (1 for the second pass of
                              potSecOrder=1, raft/raft_model.py:973-1000), normally 0         */
+  const int* group_start; /* optional [ngroup+1] device array of offsets into `order`: group g
+                             is order[group_start[g] .. group_start[g+1]), 1..rh_group_cases()
+                             cases that share design AND heading index, solved in lock-step by
+                             one workgroup (one wave-table load serves the group).  NULL ->
+                             one case per workgroup.  The caller guarantees the sharing.     */
+  int ngroup;
 } rh_cases;
 
 /* Outputs of rh_solve_cases (device buffers; NULL = not wanted). */
@@ -149,10 +155,14 @@ int rh_ctx_destroy(rh_ctx* ctx);
 int rh_version(void);
 
 /* Kernel selection for rh_solve_cases (process-wide; not part of the reference API):
- * 0 = automatic (LDS-resident fast path when nw <= 1024 and the node tables fit in LDS,
- * else the general kernel), 1 = always the general kernel.  Used by the parity tests to
+ * 0 = automatic (the grouped kernel when group_start is given; else the LDS-resident fast
+ * path when nw <= 1024 and the node tables fit in LDS; else the general kernel),
+ * 1 = always the general kernel, 2 = never the grouped kernel (one case per workgroup).  Used by the parity tests to
  * cross-check the two device paths on the same inputs. */
 int rh_set_solver(int which);
+
+/* Maximum cases per group of rh_cases.group_start (the compiled lock-step width). */
+int rh_group_cases(void);
 
 /* Waves per 64 (w1, w2) pairs in the QTF pair kernel (process-wide; not part of the
  * reference API): 1, 2 or 4 (default).  The per-pair terms are split over the waves and

@@ -13,6 +13,7 @@
 #include "rh_kernels.hip"   // single translation unit: kernels + their host launchers
 #include "rh_qtf.hip"
 #include "rh_solve.hip"
+#include "rh_solve_grp.hip"
 
 struct rh_ctx {
   int device = 0;
@@ -25,6 +26,8 @@ struct rh_ctx {
 namespace {
 thread_local std::string g_err;
 bool g_force_v2 = false;   // rh_set_solver(1): always use k_solve_cases (parity cross-checks)
+bool g_no_group = false;   // rh_set_solver(2): ignore group_start (one case per workgroup)
+constexpr int kGroupCases = 2;   // lock-step width of k_solve_grp
 int g_qtf_waves = 4;       // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs
 
 int fail(int code, const char* fmt, ...) {
@@ -87,7 +90,7 @@ extern "C" {
 
 const char* rh_last_error(void) { return g_err.c_str(); }
 
-int rh_version(void) { return 2; }
+int rh_version(void) { return 3; }
 
 #ifdef RH_PROF
 extern "C" int rh_prof_read(unsigned long long* out, int reset) {
@@ -101,10 +104,14 @@ extern "C" int rh_prof_read(unsigned long long* out, int reset) {
 #endif
 
 int rh_set_solver(int which) {
-  if (which != 0 && which != 1) return fail(RH_EINVAL, "rh_set_solver: which=%d (0 = auto, 1 = general kernel)", which);
+  if (which < 0 || which > 2)
+    return fail(RH_EINVAL, "rh_set_solver: which=%d (0 = auto, 1 = general kernel, 2 = ungrouped)", which);
   g_force_v2 = which == 1;
+  g_no_group = which == 2;
   return RH_OK;
 }
+
+int rh_group_cases(void) { return kGroupCases; }
 
 int rh_set_qtf_waves(int waves) {
   if (waves != 1 && waves != 2 && waves != 4) return fail(RH_EINVAL, "rh_set_qtf_waves: waves=%d (1, 2 or 4)", waves);
@@ -184,6 +191,20 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   a.designs = ctx->d_designs;
   a.c = *cases;
   a.o = *out;
+  // Grouped path (rh_solve_grp.hip): kGroupCases cases of one (design, heading) per workgroup.
+  if (cases->group_start && cases->ngroup > 0 && !g_force_v2 && !g_no_group) {
+    if (cases->ngroup > cases->ncase) return fail(RH_EINVAL, "rh_solve_cases: ngroup=%d > ncase", cases->ngroup);
+    int nmmax = 0;
+    for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
+    const int npass = (nw + rh::kGT - 1) / rh::kGT;
+    const size_t lsm = rh::solve_grp_smem(nnmax, nmmax, npass, kGroupCases);
+    if (lsm <= 160 * 1024) {
+      hipLaunchKernelGGL(rh::k_solve_grp<kGroupCases>, dim3(cases->ngroup), dim3(rh::kGT), lsm, s, a,
+                         cases->group_start, cases->ngroup);
+      RH_HIP(hipGetLastError());
+      return RH_OK;
+    }
+  }
   // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case, nw <= 1024.
   if (nw <= 2 * rh::kLT && !g_force_v2) {
     const int nb = nw <= rh::kLT ? 1 : 2;

@@ -42,7 +42,7 @@ class RhCases(ctypes.Structure):
     _fields_ = [("ncase", ctypes.c_int), ("design", _p), ("head", _p), ("spectrum", _p),
                 ("Hs", _p), ("Tp", _p), ("gamma", _p), ("nIter", ctypes.c_int),
                 ("XiStart", ctypes.c_double), ("tol", ctypes.c_double), ("fext", _p), ("order", _p),
-                ("Xi_init", _p), ("first_iter", ctypes.c_int)]
+                ("Xi_init", _p), ("first_iter", ctypes.c_int), ("group_start", _p), ("ngroup", ctypes.c_int)]
 
 
 class RhSolveOut(ctypes.Structure):
@@ -101,6 +101,8 @@ def lib():
                 fn.argtypes = args
                 fn.restype = ctypes.c_int
             L.rh_version.restype = ctypes.c_int
+            L.rh_group_cases.argtypes = []
+            L.rh_group_cases.restype = ctypes.c_int
             L.rh_qtf_workspace_bytes.argtypes = [ctypes.POINTER(RhQtfDesign)]
             L.rh_qtf_workspace_bytes.restype = ctypes.c_longlong
             _lib = L

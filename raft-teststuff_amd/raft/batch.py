@@ -28,23 +28,20 @@ class DesignBatch:
     r6      : platform pose for the linearisation (default: the reference position)
     """
 
-    def __init__(self, designs, statics=None, r6=None, device=0):
+    def __init__(self, designs, statics=None, r6=None, device=0, pool=None):
+        """pool: optional multiprocessing pool (see host_pool) that prepares the designs on
+        the host in parallel; results are identical to the serial path."""
         t0 = time.perf_counter()
         if isinstance(statics, dict) or statics is None:
             statics = [statics] * len(designs)
         if len(statics) != len(designs):
             raise ValueError("statics: one dict for all designs or one per design")
-        self.models, self.fowts, self.dds = [], [], []
-        for d, st in zip(designs, statics):
-            m = Model(d, statics=None if st is None else [st], device=device)
-            if m.nFOWT != 1:
-                raise NotImplementedError("DesignBatch handles single-FOWT designs (use Model for arrays)")
-            f = m.fowtList[0]
-            f.setPosition(np.zeros(6) if r6 is None else np.asarray(r6, dtype=float))
-            f.calcStatics()
-            f.calcHydroConstants()
-            self.models.append(m)
-            self.fowts.append(f)
+        jobs = [(d, st, r6, device) for d, st in zip(designs, statics)]
+        if pool is not None and len(jobs) > 1:
+            self.models = pool.map(prepare_design, jobs, chunksize=max(1, len(jobs) // (4 * pool._processes)))
+        else:
+            self.models = [prepare_design(j) for j in jobs]
+        self.fowts = [m.fowtList[0] for m in self.models]
         m0 = self.models[0]
         for m in self.models[1:]:
             if m.nw != m0.nw or not np.array_equal(m.w, m0.w):
@@ -79,6 +76,38 @@ class DesignBatch:
         BatchResult (device tensors, stream-ordered): Xi [n,6,nw], iters, status, ..."""
         cs = cases if isinstance(cases, CaseSet) else self.case_set(design_idx, cases)
         return solve_batch(self.dds, cs, self.nIter, self.XiStart, tol, want=want, prepared=prepared)
+
+
+def prepare_design(job):
+    """Host preparation of one single-FOWT design (members, statics, added mass and
+    excitation coefficients at pose r6): the per-design part of runRAFT before the case loop
+    (raft/raft_model.py:30-170, raft/raft_fowt.py:291-565, 848-880).  Pure NumPy, so it can
+    run in a worker process; the device tables are built later by the caller."""
+    d, st, r6, device = job
+    m = Model(d, statics=None if st is None else [st], device=device)
+    if m.nFOWT != 1:
+        raise NotImplementedError("DesignBatch handles single-FOWT designs (use Model for arrays)")
+    f = m.fowtList[0]
+    f.setPosition(np.zeros(6) if r6 is None else np.asarray(r6, dtype=float))
+    f.calcStatics()
+    f.calcHydroConstants()
+    f.host_tables()            # the device-table layout, built here too (travels with the FOWT)
+    return m
+
+
+def _warm_worker(grids):
+    from .hydro_math import wave_numbers
+    for w, depth in grids:
+        wave_numbers(w, depth)
+
+
+def host_pool(processes, grids=()):
+    """A pool of `processes` host workers for DesignBatch.  Create it BEFORE this process
+    initialises the GPU (workers are started with 'spawn' and never touch the device).
+    grids: (w, depth) pairs whose dispersion solutions each worker memoises up front (the
+    per-site cost a sweep pays once, hydro_math.wave_numbers)."""
+    import multiprocessing as mp
+    return mp.get_context("spawn").Pool(processes, initializer=_warm_worker, initargs=(list(grids),))
 
 
 def sweep_shard(design_idx, rank, world):

@@ -24,7 +24,26 @@ from .prep import DeviceDesign
 STATICS_KEYS = ["M_struc", "B_struc", "C_struc", "C_hydro", "W_struc", "W_hydro"]
 
 
+class _Zeros:
+    """Pickle stand-in for a large all-zero array (the per-bin aero/BEM matrices of a design
+    without them): host preparation in worker processes ships ~70 KB per design, not ~1.4 MB."""
+
+    def __init__(self, a):
+        self.shape, self.dtype = a.shape, a.dtype
+
+
 class FOWT:
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st["_dd"] = None          # device buffers never travel (host tables do)
+        for k, v in st.items():
+            if isinstance(v, np.ndarray) and v.size > 4096 and not v.any():
+                st[k] = _Zeros(v)
+        return st
+
+    def __setstate__(self, st):
+        self.__dict__.update({k: np.zeros(v.shape, v.dtype) if isinstance(v, _Zeros) else v for k, v in st.items()})
+
     def __init__(self, design, w, mpb=None, depth=600, x_ref=0, y_ref=0, heading_adjust=0, device=0):
         self.nDOF = 6
         self.w = np.array(w, dtype=float)
@@ -106,6 +125,7 @@ class FOWT:
         for k in ("M_struc", "B_struc", "C_struc", "C_hydro"):
             setattr(self, k, np.zeros([6, 6]))   # filled by calcStatics
         self._dd = None            # DeviceDesign (built lazily, invalidated on setPosition)
+        self._host = None          # its host-side tables (prep.host_tables), same lifetime
         self._qtf_devs = {}        # QtfDevice per heading (same lifetime as _dd)
         self.nWaves = 1
 
@@ -118,7 +138,7 @@ class FOWT:
             mem.setPosition(r6=self.r6)
         for rot in self.rnaList:
             rot.setPosition(self.r6)
-        self._dd = None
+        self._dd = self._host = None
         self._qtf_devs = {}
 
     def setStatics(self, statics):
@@ -139,7 +159,7 @@ class FOWT:
             if self.nrotors > 0 and len(self.rnaList) != self.nrotors:
                 raise ValueError("turbine: mRNA, IxRNA, IrRNA, xCG_RNA, overhang and shaft_tilt are required")
             fowt_statics(self)
-        self._dd = None
+        self._dd = self._host = None
         if self._statics is None:
             return
         for k in STATICS_KEYS:
@@ -149,7 +169,7 @@ class FOWT:
             self.B_struc = np.zeros([6, 6])
         if "C_moor" in self._statics:
             self.C_moor = self._statics["C_moor"].copy()
-        self._dd = None
+        self._dd = self._host = None
 
     def calcTurbineConstants(self, case, ptfm_pitch=0):
         """raft/raft_fowt.py:773-845 restricted to what the accelerated path supports: rotor
@@ -173,8 +193,16 @@ class FOWT:
             k_array = self.k if mem.MCF else None
             self.A_hydro_morison += mem.calcHydroConstants(r_ref=self.r6[:3], rho=self.rho_water, g=self.g,
                                                            k_array=k_array)
-        self._dd = None
+        self._dd = self._host = None
         self._qtf_devs = {}
+
+    def host_tables(self):
+        """Host-side node/member tables and linear matrices of the current pose and
+        coefficients (prep.host_tables; cached, and carried along when the FOWT is pickled)."""
+        if self._host is None:
+            from .prep import host_tables
+            self._host = host_tables(self)
+        return self._host
 
     def device_design(self):
         """The DeviceDesign of the current pose and coefficients (built on first use)."""

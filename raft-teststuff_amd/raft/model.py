@@ -34,7 +34,7 @@ class Model:
         max_freq = get_from_dict(st, "max_freq", default=1.00, dtype=float)
         self.XiStart = get_from_dict(st, "XiStart", default=0.1, dtype=float)
         self.nIter = get_from_dict(st, "nIter", default=15, dtype=int)
-        self.w = np.arange(min_freq, max_freq + 0.5 * min_freq, min_freq) * 2 * np.pi   # :55
+        self.w = self.frequency_grid(design)   # :55
         self.nw = len(self.w)
         self.depth = get_from_dict(design["site"], "water_depth", dtype=float)
         self.k = wave_numbers(self.w, self.depth)
@@ -70,6 +70,14 @@ class Model:
                 f.setStatics(s)
         self.design = design
         self.results = {}
+
+    @staticmethod
+    def frequency_grid(design):
+        """The first-order frequency grid [rad/s] of a design's settings (raft/raft_model.py:55)."""
+        st = design.get("settings", {})
+        min_freq = get_from_dict(st, "min_freq", default=0.01, dtype=float)
+        max_freq = get_from_dict(st, "max_freq", default=1.00, dtype=float)
+        return np.arange(min_freq, max_freq + 0.5 * min_freq, min_freq) * 2 * np.pi
 
     # --------------------------------------------------------------------- dynamics
     def solveDynamics(self, case, tol=0.01, conv_plot=0, RAO_plot=0, display=0):

@@ -98,6 +98,24 @@ def linear_matrices(fowt):
     return M, B, C, False
 
 
+def host_tables(fowt):
+    """Everything DeviceDesign uploads, computed on the host (NumPy only, so it can run in
+    a host worker next to the rest of the per-design preparation): the real-valued tables
+    packed into ONE float64 array (one host->device copy per design) plus their layout."""
+    table, imat, members, mstart = node_table(fowt)
+    nn, nm = table.shape[1], members.shape[1]
+    M, B, C, per_bin = linear_matrices(fowt)
+    parts = [("w", np.asarray(fowt.w, dtype=float)), ("k", np.asarray(fowt.k, dtype=float)),
+             ("node", table if nn else np.zeros([N.NF_COUNT, 1])), ("memb", members if nm else np.zeros([N.MF_COUNT, 1])),
+             ("M", np.asarray(M, dtype=float)), ("B", np.asarray(B, dtype=float)), ("C", np.asarray(C, dtype=float))]
+    layout, off = {}, 0
+    for name, a in parts:
+        layout[name] = (off, a.shape)
+        off += a.size
+    packed = np.concatenate([np.ascontiguousarray(a).ravel() for _, a in parts])
+    return dict(packed=packed, layout=layout, imat=imat, mstart=mstart, nn=nn, nm=nm, per_bin=per_bin)
+
+
 class DeviceDesign:
     """Device-resident tables of one FOWT design (caller-owned torch buffers)."""
 
@@ -107,21 +125,14 @@ class DeviceDesign:
         self.device = torch.device("cuda", device)
         self.dev_index = device
         self.nw = fowt.nw
-        table, imat, members, mstart = node_table(fowt)
-        self.nn = table.shape[1]
-        self.nm = members.shape[1]
-        f64 = dict(dtype=torch.float64, device=self.device)
-        self.w = torch.tensor(fowt.w, **f64)
-        self.k = torch.tensor(fowt.k, **f64)
-        self.node = torch.tensor(table if self.nn else np.zeros([N.NF_COUNT, 1]), **f64).contiguous()
+        h = fowt.host_tables() if hasattr(fowt, "host_tables") else host_tables(fowt)
+        self.nn, self.nm, self.per_bin = h["nn"], h["nm"], h["per_bin"]
+        self._packed = torch.tensor(h["packed"], dtype=torch.float64, device=self.device)
+        for name, (off, shape) in h["layout"].items():   # contiguous views of the one upload
+            setattr(self, name, self._packed[off:off + int(np.prod(shape))].view(*shape))
+        imat = h["imat"]
         self.imat = torch.tensor(imat, dtype=torch.complex128, device=self.device) if imat is not None else None
-        self.memb = torch.tensor(members if self.nm else np.zeros([N.MF_COUNT, 1]), **f64).contiguous()
-        self.mstart = torch.tensor(mstart, dtype=torch.int32, device=self.device)
-        M, B, C, per_bin = linear_matrices(fowt)
-        self.per_bin = per_bin
-        self.M = torch.tensor(M, **f64).contiguous()
-        self.B = torch.tensor(B, **f64).contiguous()
-        self.C = torch.tensor(C, **f64).contiguous()
+        self.mstart = torch.tensor(h["mstart"], dtype=torch.int32, device=self.device)
         self.dw, self.depth, self.rho, self.g = float(fowt.dw), float(fowt.depth), float(fowt.rho_water), float(fowt.g)
         self.headings = None           # tuple of tabulated headings (rad)
         self.uhat = None

@@ -7,6 +7,7 @@ case, one workgroup per case; cases are launched sorted by (design, heading) so 
 blocks an XCD receives stream the same wave tables out of its L2.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -94,6 +95,7 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     cs.fext = N.ptr(fext)
     cs.order = N.ptr(prep["order"])
     cs.Xi_init, cs.first_iter = N.ptr(Xi_init), int(first_iter)
+    cs.group_start, cs.ngroup = N.ptr(prep["group_start"]), int(prep["ngroup"])
     o = N.RhSolveOut()
     o.Xi, o.Xi_last, o.iters, o.status = N.ptr(out["Xi"]), N.ptr(xl), N.ptr(out["iters"]), N.ptr(out["status"])
     for k in ["zeta", "B_drag", "Bmat", "psd", "std", "rao", "Z", "Xi_prev"]:
@@ -120,10 +122,33 @@ def prepare_batch(designs, cases):
         head[sel] = d.ensure_headings(betas)
     if cases.design_idx.min() < 0 or cases.design_idx.max() >= len(designs):
         raise ValueError("design index out of range")
-    order = np.lexsort((head, cases.design_idx)).astype(np.int32)
+    # design-major, then heading; within a (design, heading) run by sea state, so that the
+    # cases solved in lock-step by one workgroup tend to need the same number of iterations
+    order = np.lexsort((cases.Tp, cases.Hs, head, cases.design_idx)).astype(np.int32)
+    # Lock-step groups (k_solve_grp) are opt-in: RAFT_GROUP_WIDTH=2.  Measured on the C2
+    # batch they halve the wave-table stream but not the time per case, and
+    # one case per workgroup (k_solve_lds) schedules better at 512 cases per GPU.
+    width = min(N.lib().rh_group_cases(), int(os.environ.get("RAFT_GROUP_WIDTH", "1") or 1))
+    gstart = case_groups(cases.design_idx[order], head[order], width) if width > 1 else None
     i32 = dict(dtype=torch.int32, device=dev)
     f64 = dict(dtype=torch.float64, device=dev)
     return dict(design=torch.tensor(cases.design_idx, **i32), head=torch.tensor(head, **i32),
                 spectrum=torch.tensor(cases.spectrum, **i32), Hs=torch.tensor(cases.Hs, **f64),
                 Tp=torch.tensor(cases.Tp, **f64), gamma=torch.tensor(cases.gamma, **f64),
-                order=torch.tensor(order, **i32), head_host=head)
+                order=torch.tensor(order, **i32), head_host=head,
+                group_start=None if gstart is None else torch.tensor(gstart, **i32),
+                ngroup=0 if gstart is None else len(gstart) - 1)
+
+
+def case_groups(design, head, width):
+    """Offsets of the lock-step groups of rh_cases.group_start: consecutive (already sorted)
+    cases with equal design and heading index, at most `width` per group."""
+    n = len(design)
+    if n == 0:
+        return np.zeros(1, dtype=np.int32)
+    starts = [0]
+    for i in range(1, n):
+        if design[i] != design[i - 1] or head[i] != head[i - 1] or i - starts[-1] >= width:
+            starts.append(i)
+    starts.append(n)
+    return np.asarray(starts, dtype=np.int32)

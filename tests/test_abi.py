@@ -43,7 +43,9 @@ def test_library_exports_every_declared_symbol(libpath):
 def test_library_loads_and_binds(libpath):
     from raft import _native as N
     L = N.lib()
-    assert L.rh_version() == 2
+    assert L.rh_version() == 3
+    assert L.rh_group_cases() >= 1
+    assert L.rh_set_solver(2) == N.RH_OK and L.rh_set_solver(0) == N.RH_OK
     assert L.rh_set_solver(7) == N.RH_EINVAL and L.rh_set_solver(0) == N.RH_OK
     for f in declared_functions():
         assert hasattr(L, f)

@@ -207,20 +207,27 @@ def test_system_solve_12dof_matches_numpy():
         np.testing.assert_allclose(X[:, b], np.linalg.solve(Zs, F[:, b]), rtol=1e-10, atol=1e-12)
 
 
+@pytest.mark.parametrize("other", [1, 2], ids=["general", "grouped"])
 @pytest.mark.parametrize("tag,design,settings,ncase", [("c2_nw1000", "VolturnUS-S_example", {"min_freq": 0.0002}, 128),
                                                        ("c2_nw200", "VolturnUS-S_example", None, 64),
-                                                       ("c1_OC3spar", "OC3spar", None, 16)])
-def test_fast_and_general_kernels_agree(tag, design, settings, ncase):
-    """The LDS-resident fast kernel (k_solve_lds) and the general kernel (k_solve_cases) on the
-    same batch: identical iteration counts and statuses, outputs within 1e-12 (they differ only
-    in the summation order of the per-node bin reductions)."""
+                                                       ("c1_OC3spar", "OC3spar", None, 17)])
+def test_fast_and_general_kernels_agree(tag, design, settings, ncase, other, monkeypatch):
+    """The default path (k_solve_lds: one case per workgroup, XiLast in LDS) against the
+    general kernel (k_solve_cases, other=1) and against the lock-step grouped kernel
+    (k_solve_grp, two cases of one design and heading per workgroup, other=2) on the same
+    batch: identical iteration counts and statuses, outputs within 1e-12 (they differ only in
+    the summation order of the per-node bin reductions).  An odd case count leaves a
+    half-empty group."""
     from raft import _native as N
     T = load_golden(tag)
     m, f = make_model(design, T, settings)
     cases = random_cases(ncase, 99)
     want = ("psd", "std", "zeta", "B_drag", "rao")
     a = m.analyzeCasesBatch(cases, want=want)
-    N.check(N.lib().rh_set_solver(1), "rh_set_solver")
+    if other == 2:
+        monkeypatch.setenv("RAFT_GROUP_WIDTH", "2")
+    else:
+        N.check(N.lib().rh_set_solver(other), "rh_set_solver")
     try:
         b = m.analyzeCasesBatch(cases, want=want)
     finally:
