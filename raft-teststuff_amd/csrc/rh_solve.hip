@@ -55,6 +55,24 @@ __device__ __forceinline__ double dpp_mov(double v) {   // full-mask permutation
   return __hiloint2double(hi, lo);
 }
 
+// t + t(lane ^ 32) and t + t(lane ^ 16) with the gfx950 row-swap instructions
+// (v_permlane32_swap / v_permlane16_swap: VALU, no LDS round trip as with ds_bpermute).
+// Called with both operands equal, the swap leaves {x_i, x_partner} split over its two
+// results in lane-dependent order, and their sum is the pair sum (bitwise the same as
+// t + __shfl_xor(t, 32 | 16): FP addition commutes).  Call with every lane active.
+__device__ __forceinline__ double xsum32(double t) {
+  const int lo = __double2loint(t), hi = __double2hiint(t);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+__device__ __forceinline__ double xsum16(double t) {
+  const int lo = __double2loint(t), hi = __double2hiint(t);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+
 // Transposing butterfly: 16 per-lane values u[k] -> lane i of EVERY row ends with the wave
 // total (all 64 lanes) of value k(i) = 8 f0 + 4 f1 + 2 f2 + f3, with the lane bits
 //   f0 = b0^b2, f1 = b1^b2, f2 = b2^b3, f3 = b3     (i = lane & 15, b = bits of i).
@@ -86,10 +104,7 @@ __device__ __forceinline__ double tbfly16(double (&u)[16], int lane) {
     const double keep = f3 ? u[1] : u[0], send = f3 ? u[0] : u[1];
     u[0] = keep + dpp_mov<0x140>(send);
   }
-  double t = u[0];
-  t += __shfl_xor(t, 16, 64);
-  t += __shfl_xor(t, 32, 64);
-  return t;
+  return xsum32(xsum16(u[0]));
 }
 __device__ __forceinline__ int tbfly16_index(int lane) {
   const int i = lane & 15;
@@ -112,9 +127,7 @@ __device__ __forceinline__ double tbfly3(double a, double b, double c, int lane)
   double t = (f1 ? u1 : u0) + dpp_mov<0x4E>(f1 ? u0 : u1);
   t += dpp_mov<0x124>(t);   // row_ror:4
   t += dpp_mov<0x128>(t);   // row_ror:8
-  t += __shfl_xor(t, 16, 64);
-  t += __shfl_xor(t, 32, 64);
-  return t;
+  return xsum32(xsum16(t));
 }
 // value held by a lane after tbfly3: 2 f0 + f1 -> lane 0: a (0), lane 1: c (2), lane 2: b (1)
 __device__ __forceinline__ int tbfly3_index(int lane) { return 2 * (lane & 1) + ((lane >> 1) & 1); }

@@ -50,9 +50,7 @@ __device__ __forceinline__ double tbfly8(double (&u)[8], int lane) {
   }
   double t = u[0];
   t += dpp_mov<0x128>(t);   // row_ror:8
-  t += __shfl_xor(t, 16, 64);
-  t += __shfl_xor(t, 32, 64);
-  return t;
+  return xsum32(xsum16(t));
 }
 __device__ __forceinline__ int tbfly8_index(int lane) {
   const int i = lane & 15;
