@@ -8,7 +8,8 @@ the per-design preparation (members, node tables, linear matrices) and the devic
 The statics (member inertia / hydrostatics / RNA) are computed on
 the host by raft/statics.py.  Not built here: MoorPy mooring (its
 stiffness C_moor is an input, FOWT.setStatics), rotor aerodynamics (CCBlade), BEM (pyHAMS)
-and reading external QTF files (potSecOrder=2).
+and BEM coefficient files (potFirstOrder=1).  External .12d QTFs (potSecOrder=2) are read on
+the host (qtf_io.read_qtf12d) and applied on the device (rh_force_2nd).
 """
 import os
 import ctypes
@@ -110,8 +111,11 @@ class FOWT:
             self.w2_2nd = self.w1_2nd.copy()
             self.k1_2nd = wave_numbers(self.w1_2nd, self.depth)
             self.k2_2nd = self.k1_2nd.copy()
-        elif self.potSecOrder == 2:
-            raise NotImplementedError("potSecOrder=2 (external .12d QTF file) is outside the accelerated path")
+        elif self.potSecOrder == 2:                                       # raft/raft_fowt.py:248-252
+            if "hydroPath" not in plat:
+                raise Exception("If potSecOrder==2, then hydroPath must be specified in the platform input.")
+            self.qtfPath = plat["hydroPath"] + ".12d"
+            self.readQTF(self.qtfPath)
         self.outFolderQTF = plat.get("outFolderQTF")
         self.C_moor = np.zeros([6, 6])
         self.F_moor0 = np.zeros(6)
@@ -362,6 +366,39 @@ class FOWT:
             write_rao4(rao_path, self.w1_2nd, beta, Xi_2nd)
             self.writeQTF(self.qtf, qtf_path)
 
+    def readQTF(self, flPath, ULEN=1):
+        """WAMIT .12d reader (raft/raft_fowt.py:1651-1697): sets heads_2nd [rad], w1_2nd,
+        w2_2nd and qtf [n1, n2, nheads, 6]."""
+        from .qtf_io import read_qtf12d
+        self.heads_2nd, self.w1_2nd, self.w2_2nd, self.qtf = read_qtf12d(flPath, self.rho_water, self.g, ULEN,
+                                                                          self.nDOF)
+        self._qtf_file_dev = {}     # device copies per heading (calcHydroForce_2ndOrd)
+
+    def _file_qtf_device(self, beta):
+        """The file QTF at heading beta as the device operands of rh_force_2nd.  Heading
+        interpolation as raft/raft_fowt.py:1752-1757 does it, fill values included."""
+        import torch
+        from types import SimpleNamespace
+        key = float(beta)
+        if key not in self._qtf_file_dev:
+            h2 = np.asarray(self.heads_2nd, dtype=float)
+            if len(h2) == 1:
+                qb = self.qtf[:, :, 0, :]
+            else:
+                from scipy.interpolate import interp1d
+                q = self.qtf
+                re = interp1d(h2, q, assume_sorted=True, axis=2, bounds_error=False,
+                              fill_value=(q[:, :, 0, :], q[:, :, -1, :].real))(beta)
+                im = interp1d(h2, q, assume_sorted=True, axis=2, bounds_error=False,
+                              fill_value=(q[:, :, 0, :], q[:, :, -1, :].imag))(beta)
+                qb = re + 1j * im
+            dev = torch.device("cuda", self.device_index)
+            w2 = torch.tensor(np.asarray(self.w1_2nd, dtype=float), dtype=torch.float64, device=dev)
+            qd = SimpleNamespace(torch=torch, dev=dev, dev_index=self.device_index, n2=len(self.w1_2nd), w2=w2)
+            qt = torch.tensor(np.ascontiguousarray(qb, dtype=complex), dtype=torch.complex128, device=dev).contiguous()
+            self._qtf_file_dev[key] = (qd, qt)
+        return self._qtf_file_dev[key]
+
     def writeQTF(self, qtfIn, outPath, w=None):
         """WAMIT .12d writer (raft/raft_fowt.py:1700-1726)."""
         from .qtf_io import write_qtf12d
@@ -377,8 +414,9 @@ class FOWT:
             raise NotImplementedError("calcHydroForce_2ndOrd: only interpMode='qtf' (the reference default) is "
                                       "accelerated")
         h2 = getattr(self, "heads_2nd", None)
-        if h2 is None or getattr(self, "_qtf_dev", None) is None:
-            raise RuntimeError("calcHydroForce_2ndOrd needs a QTF (call calcQTF_slenderBody first)")
+        from_file = self.potSecOrder == 2
+        if h2 is None or (not from_file and getattr(self, "_qtf_dev", None) is None):
+            raise RuntimeError("calcHydroForce_2ndOrd needs a QTF (calcQTF_slenderBody or a .12d file)")
         if beta < h2[0]:
             print(f"Warning in calcHydroForce_2ndOrd: angle {beta} is less than the minimum incidence angle in the "
                   f"QTF. An incidence of {h2[0]} will be considered for 2nd order loads.")
@@ -387,10 +425,10 @@ class FOWT:
                   f"QTF. An incidence of {h2[-1]} will be considered for 2nd order loads.")
         from .qtf import force_2nd
         dd = self.device_design()
-        qd = self._qtf_qd
+        qd, qt = self._file_qtf_device(beta) if from_file else (self._qtf_qd, self._qtf_dev)
         S = S0 if isinstance(S0, torch.Tensor) else torch.tensor(np.asarray(S0, dtype=float), dtype=torch.float64,
                                                                   device=dd.device)
-        fm, f = force_2nd(qd, self._qtf_dev, dd.w, self.dw, S.to(dd.device).contiguous())
+        fm, f = force_2nd(qd, qt, dd.w, self.dw, S.to(dd.device).contiguous())
         self._f2nd_dev = f
         f_mean, f_h = fm.cpu().numpy(), f.cpu().numpy()
         if self.outFolderQTF is not None:

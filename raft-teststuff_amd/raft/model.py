@@ -102,7 +102,13 @@ class Model:
                 print("Solving for system response to wave excitation in primary wave direction")
             second = fowt.potSecOrder == 1
             want = ("zeta", "B_drag", "Bmat", "Z") + (("rao", "Xi_prev") if second else ())
-            res = solve_batch([dd], cs, self.nIter, self.XiStart, tol, want=want)
+            fext = None
+            if fowt.potSecOrder == 2:   # external QTF: second-order load inside the drag loop (:903-904)
+                fm, f = fowt.calcHydroForce_2ndOrd(fowt.beta[0], fowt._S_dev[0], iCase=iCase, iWT=i)
+                fowt.Fhydro_2nd_mean[0], fowt.Fhydro_2nd[0] = fm, f
+                fext = fowt._f2nd_dev.to(torch.complex128)[None].contiguous()
+                fowt._f2nd_w[0] = fext[0]
+            res = solve_batch([dd], cs, self.nIter, self.XiStart, tol, want=want, fext=fext)
             status, iters = self._check_pass(res, tol, display)
             fowt.iterations_pair = [iters]
             if second and status == N.RH_CASE_CONVERGED:
@@ -130,6 +136,10 @@ class Model:
             Fw = []
             for ih in range(nW):
                 Fd = torch.tensor(fowt.calcDragExcitation(ih), dtype=torch.complex128, device=dev)
+                if fowt.potSecOrder == 2 and ih > 0:                   # :1059-1060
+                    fm, f = fowt.calcHydroForce_2ndOrd(fowt.beta[ih], fowt._S_dev[ih])
+                    fowt.Fhydro_2nd_mean[ih], fowt.Fhydro_2nd[ih] = fm, f
+                    fowt._f2nd_w[ih] = fowt._f2nd_dev.to(torch.complex128)
                 F = dd.finer[fowt._heads[ih]] * fowt._zeta_dev[ih][None, :] + Fd
                 if fowt._f2nd_w[ih] is not None:
                     F = F + fowt._f2nd_w[ih]

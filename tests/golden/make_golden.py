@@ -436,7 +436,62 @@ def golden_sweep():
         np.savez_compressed(os.path.join(HERE, f"c5_sweep{i}.npz"), **T)
 
 
+def golden_qtf12d():
+    """potSecOrder=2: an external WAMIT .12d QTF (the reference's own
+    examples/OC4semi-WAMIT_Coefs/marin_semi.12d) read by FOWT.readQTF
+    (raft/raft_fowt.py:1651-1697) and applied through calcHydroForce_2ndOrd before the drag
+    loop and for the other sea states (raft/raft_model.py:903-904, :1059-1061).  Design:
+    OC4semi-RAFT_QTF with strip-theory first order (potFirstOrder 0) at nw = 100.
+    Stored: the file's numeric table (the test rewrites an equivalent .12d from it), the
+    parsed QTF, and per case Xi, iterations, the second-order force and mean drift."""
+    import raft.raft_fowt as rf
+    rf.interp2d = bilinear_interp2d
+    path = os.path.join(REF, "examples", "OC4semi-WAMIT_Coefs", "marin_semi")
+    design = load_design(os.path.join(REF, "examples", "OC4semi-RAFT_QTF.yaml"), min_freq=0.0025)
+    plat = design["platform"]
+    for k in ("outFolderQTF", "min_freq2nd", "max_freq2nd", "df_freq2nd"):
+        plat.pop(k, None)
+    plat["potSecOrder"] = 2
+    plat["hydroPath"] = path
+    cases = [dict(wind_speed=0, wind_heading=0, turbulence=0, turbine_status="operating", yaw_misalign=0,
+                  wave_spectrum="JONSWAP", wave_period=12.0, wave_height=6.0, wave_heading=0.0, current_speed=0,
+                  wave_gamma=0.0),
+             dict(wind_speed=0, wind_heading=0, turbulence=0, turbine_status="operating", yaw_misalign=0,
+                  wave_spectrum="JONSWAP", wave_period=9.0, wave_height=3.5, wave_heading=0.0, current_speed=0,
+                  wave_gamma=2.0),
+             dict(wind_speed=0, wind_heading=0, turbulence=0, turbine_status="operating", yaw_misalign=0,
+                  wave_spectrum=["JONSWAP", "JONSWAP"], wave_period=[12.0, 7.0], wave_height=[6.0, 2.0],
+                  wave_heading=[0.0, 30.0], current_speed=0, wave_gamma=[0.0, 0.0])]
+    out = dict(table12d=np.loadtxt(path + ".12d"))
+    res = {k: [] for k in ["Xi", "iters", "Fhydro_2nd", "Fhydro_2nd_mean", "B_drag", "zeta", "S"]}
+    for ic, case in enumerate(cases):
+        model = raft.Model(json.loads(json.dumps(design)))
+        fowt = model.fowtList[0]
+        prepare_fowt(fowt, case)
+        if ic == 0:
+            out.update(design_tables(fowt))
+            out.update(qtf=fowt.qtf.copy(), heads_2nd=np.array(fowt.heads_2nd, dtype=float), w1_2nd=fowt.w1_2nd.copy())
+        Xi, iters, conv, dt = run_solve(model, dict(case))
+        nW = fowt.nWaves
+        pad = lambda a, n: np.concatenate([a, np.zeros((n - len(a),) + a.shape[1:], dtype=a.dtype)])
+        res["Xi"].append(pad(np.array(Xi), 3))
+        res["iters"].append(iters)
+        res["Fhydro_2nd"].append(pad(fowt.Fhydro_2nd.copy(), 2))
+        res["Fhydro_2nd_mean"].append(pad(fowt.Fhydro_2nd_mean.copy(), 2))
+        res["B_drag"].append(fowt.B_hydro_drag.copy())
+        res["zeta"].append(pad(fowt.zeta.copy(), 2))
+        res["S"].append(pad(fowt.S.copy(), 2))
+        print(f"  qtf12d case {ic}: nWaves {nW}, iters {iters}, {dt:.1f}s", file=sys.stderr)
+    out.update({"out_" + k: np.array(v) for k, v in res.items()})
+    out.update(nIter=np.int64(design["settings"]["nIter"]), XiStart=np.float64(design["settings"]["XiStart"]),
+               cases_json=np.array(json.dumps(cases)))
+    np.savez_compressed(os.path.join(HERE, "qtf12d.npz"), **out)
+    print("wrote qtf12d.npz", file=sys.stderr)
+
+
 def main(which):
+    if "qtf12d" in which:
+        golden_qtf12d()
     if "qtf" in which:
         golden_qtf()
     if "farm" in which:
