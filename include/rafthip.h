@@ -204,6 +204,25 @@ int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int 
 int rh_linearize(rh_ctx* ctx, const rh_design* d, int head, const rh_c128* Xi, const double* zeta,
                  double* B_drag, double* Bmat, rh_c128* F_drag, rh_stream stream);
 
+/* Bin-sharded drag fixed point of ONE case, bins split over ranks.
+ * The only coupling across bins is the per-node RMS sum (raft/raft_fowt.py:1214-1220) and
+ * the all-bins convergence test (raft/raft_model.py:962).  One iteration on each rank:
+ *  1. rh_lin_partial_sums: per-node sums of |vrel|^2 over this rank's bins [bin_lo, bin_hi)
+ *     of Xi_last [6][nw] -> sums [nn][3] (q, p or p1, p2);
+ *  2. the caller all-reduces (sums) the sums over ranks;
+ *  3. rh_bin_step: Bmat [nn][9] and B_drag [36] from the global sums (raft/raft_fowt.py:
+ *     1223-1250), then for bins [bin_lo, bin_hi): F_lin + F_drag (+ fext [6][nw], or NULL),
+ *     Z(w) and its LU solve -> Xi, tolCheck against Xi_last and the 0.2/0.8 relaxation of
+ *     Xi_last in place (raft/raft_model.py:942-991).  flags: device int[3], zeroed by the
+ *     caller, set to 1 if some bin is [0] not converged, [1] NaN, [2] singular;
+ *  4. the caller all-reduces (max) the flags.
+ * Host driver: raft/parallel.py solve_bins_sharded. */
+int rh_lin_partial_sums(rh_ctx* ctx, const rh_design* d, int head, const rh_c128* Xi_last, const double* zeta,
+                        int bin_lo, int bin_hi, double* sums, rh_stream stream);
+int rh_bin_step(rh_ctx* ctx, const rh_design* d, int head, const double* zeta, const rh_c128* fext,
+                const double* sums, double tol, int bin_lo, int bin_hi, double* Bmat, double* B_drag,
+                rh_c128* Xi, rh_c128* Xi_last, int* flags, rh_stream stream);
+
 /* Drag excitation for given node matrices (FOWT.calcDragExcitation, raft/raft_fowt.py:1270-1293). */
 int rh_drag_excitation(rh_ctx* ctx, const rh_design* d, int head, const double* zeta,
                        const double* Bmat, rh_c128* F_drag, rh_stream stream);

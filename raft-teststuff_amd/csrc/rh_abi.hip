@@ -270,6 +270,40 @@ int rh_linearize(rh_ctx* ctx, const rh_design* d, int head, const rh_c128* Xi, c
   return RH_OK;
 }
 
+int rh_lin_partial_sums(rh_ctx* ctx, const rh_design* d, int head, const rh_c128* Xi_last, const double* zeta,
+                        int bin_lo, int bin_hi, double* sums, rh_stream stream) {
+  if (!ctx || !d || !Xi_last || !zeta || !sums) return fail(RH_EINVAL, "rh_lin_partial_sums: null argument");
+  if (int r = check_design(*d, true)) return r;
+  if (head < 0 || head >= d->nhead) return fail(RH_EINVAL, "rh_lin_partial_sums: head %d out of range", head);
+  if (bin_lo < 0 || bin_hi > d->nw || bin_lo > bin_hi)
+    return fail(RH_EINVAL, "rh_lin_partial_sums: bins [%d, %d) outside [0, %d)", bin_lo, bin_hi, d->nw);
+  RH_HIP(hipSetDevice(ctx->device));
+  if (d->nn > 0)
+    hipLaunchKernelGGL(rh::k_lin_partial, dim3(d->nn), dim3(kThreads), 0, (hipStream_t)stream, *d, head, Xi_last, zeta,
+                       bin_lo, bin_hi, sums);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
+int rh_bin_step(rh_ctx* ctx, const rh_design* d, int head, const double* zeta, const rh_c128* fext, const double* sums,
+                double tol, int bin_lo, int bin_hi, double* Bmat, double* B_drag, rh_c128* Xi, rh_c128* Xi_last,
+                int* flags, rh_stream stream) {
+  if (!ctx || !d || !zeta || !sums || !Bmat || !B_drag || !Xi || !Xi_last || !flags)
+    return fail(RH_EINVAL, "rh_bin_step: null argument");
+  if (int r = check_design(*d, true)) return r;
+  if (head < 0 || head >= d->nhead) return fail(RH_EINVAL, "rh_bin_step: head %d out of range", head);
+  if (bin_lo < 0 || bin_hi > d->nw || bin_lo > bin_hi)
+    return fail(RH_EINVAL, "rh_bin_step: bins [%d, %d) outside [0, %d)", bin_lo, bin_hi, d->nw);
+  RH_HIP(hipSetDevice(ctx->device));
+  const int n = bin_hi - bin_lo;
+  const size_t smem = sizeof(double) * (size_t)(9 * d->nn + 36 + 108);
+  hipLaunchKernelGGL(rh::k_bin_step, dim3(n > 0 ? (n + kThreads - 1) / kThreads : 1), dim3(kThreads), smem,
+                     (hipStream_t)stream, *d, head, zeta, fext, sums, tol, bin_lo, bin_hi, Bmat, B_drag, Xi, Xi_last,
+                     flags);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
 int rh_drag_excitation(rh_ctx* ctx, const rh_design* d, int head, const double* zeta, const double* Bmat,
                        rh_c128* F_drag, rh_stream stream) {
   if (!ctx || !d || !zeta || !Bmat || !F_drag) return fail(RH_EINVAL, "rh_drag_excitation: null argument");

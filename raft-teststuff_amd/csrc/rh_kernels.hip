@@ -604,10 +604,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_heading_resp(HeadArgs a) {
 // stand-alone linearisation (FOWT.calcHydroLinearization for a given Xi)
 // ----------------------------------------------------------------------------------------
 // pass 1: block per node, reduce over bins
-__global__ __launch_bounds__(kThreads) void k_lin_sums(rh_design d, int head, const rh_c128* __restrict__ Xi,
-                                                       const double* __restrict__ zeta, double* __restrict__ Bmat) {
-  __shared__ double red[kWaves][3];
-  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+// Block-wide per-node sums of |vrel_q|^2, |vrel_p|^2 (or |vrel_p1|^2, |vrel_p2|^2) over the
+// bins [lo, hi) of Xi (raft/raft_fowt.py:1205-1220), bins strided over the block; returns
+// the three sums in thread 0.  Fixed order (per-thread bins, butterflies, waves in order).
+__device__ __forceinline__ void lin_node_sums(const rh_design& d, int head, const rh_c128* __restrict__ Xi,
+                                              const double* __restrict__ zeta, int n, int lo, int hi,
+                                              double (&red)[kWaves][3], double (&out)[3]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nw = d.nw, nn = d.nn;
   const double* node = d.node;
   const rh_c128* U = d.uhat + ((size_t)head * nn + n) * 3 * nw;
@@ -617,7 +620,7 @@ __global__ __launch_bounds__(kThreads) void k_lin_sums(rh_design d, int head, co
   const double b0 = nf(node, nn, RH_NF_P2X, n), b1 = nf(node, nn, RH_NF_P2Y, n), b2 = nf(node, nn, RH_NF_P2Z, n);
   const bool circ = nf(node, nn, RH_NF_CIRC, n) != 0.0;
   double s0 = 0, s1 = 0, s2 = 0;
-  for (int b = tid; b < nw; b += kThreads) {
+  for (int b = lo + tid; b < hi; b += kThreads) {
     const double w = d.w[b], z = zeta[b];
     const cd u0 = scl(ld(U + b), z), u1 = scl(ld(U + nw + b), z), u2 = scl(ld(U + 2 * nw + b), z);
     cd X[6];
@@ -649,14 +652,103 @@ __global__ __launch_bounds__(kThreads) void k_lin_sums(rh_design d, int head, co
   }
   __syncthreads();
   if (tid == 0) {
-    double sums[3];
     for (int c = 0; c < 3; ++c) {
       double s = 0;
       for (int w = 0; w < kWaves; ++w) s += red[w][c];
-      sums[c] = s;
+      out[c] = s;
     }
-    node_bmat(node, nn, n, d.rho, sums, Bmat + 9 * n);
   }
+}
+
+__global__ __launch_bounds__(kThreads) void k_lin_sums(rh_design d, int head, const rh_c128* __restrict__ Xi,
+                                                       const double* __restrict__ zeta, double* __restrict__ Bmat) {
+  __shared__ double red[kWaves][3];
+  double sums[3];
+  const int n = blockIdx.x;
+  lin_node_sums(d, head, Xi, zeta, n, 0, d.nw, red, sums);
+  if (threadIdx.x == 0) node_bmat(d.node, d.nn, n, d.rho, sums, Bmat + 9 * n);
+}
+
+// ----------------------------------------------------------------------------------------
+// bin-sharded drag fixed point: one case, bins split over ranks
+// ----------------------------------------------------------------------------------------
+// step 1: this rank's partial node sums over bins [lo, hi), block per node
+__global__ __launch_bounds__(kThreads) void k_lin_partial(rh_design d, int head, const rh_c128* __restrict__ Xi,
+                                                          const double* __restrict__ zeta, int lo, int hi,
+                                                          double* __restrict__ sums) {
+  __shared__ double red[kWaves][3];
+  double s[3];
+  const int n = blockIdx.x;
+  lin_node_sums(d, head, Xi, zeta, n, lo, hi, red, s);
+  if (threadIdx.x == 0)
+    for (int c = 0; c < 3; ++c) sums[3 * n + c] = s[c];
+}
+
+// step 2 (after the caller's all-reduce of the sums): node drag matrices and B_drag from the
+// global sums (every block, into LDS; block 0 also writes them out), then thread per bin of
+// [lo, hi): drag + inertial excitation (+ fext), Z(w), LU, tolCheck and relaxation of XiLast
+// (raft/raft_model.py:942-991, the arithmetic of k_heading_resp / k_solve_cases).
+// flags (caller-zeroed): [0] some bin not converged, [1] NaN, [2] singular.
+__global__ __launch_bounds__(kThreads) void k_bin_step(rh_design d, int head, const double* __restrict__ zeta,
+                                                       const rh_c128* __restrict__ fext, const double* __restrict__ sums,
+                                                       double tol, int lo, int hi, double* __restrict__ Bmat_out,
+                                                       double* __restrict__ Bd_out, rh_c128* __restrict__ Xi,
+                                                       rh_c128* __restrict__ XL, int* __restrict__ flags) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nw = d.nw, nn = d.nn, tid = threadIdx.x;
+  double* bm = smem;            // [nn][9]
+  double* bd = bm + 9 * nn;     // [36]
+  double* mbc = bd + 36;        // [108]
+  load_mbc(d, mbc, tid);
+  for (int n = tid; n < nn; n += blockDim.x) {
+    const double s3[3] = {sums[3 * n], sums[3 * n + 1], sums[3 * n + 2]};
+    node_bmat(d.node, nn, n, d.rho, s3, bm + 9 * n);
+  }
+  __syncthreads();
+  if (tid < 36) {
+    double s = 0;
+    for (int n = 0; n < nn; ++n)
+      s += t3to6(bm + 9 * n, nf(d.node, nn, RH_NF_XX, n), nf(d.node, nn, RH_NF_XY, n), nf(d.node, nn, RH_NF_XZ, n),
+                 tid / 6, tid % 6);
+    bd[tid] = s;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    for (int e = tid; e < 9 * nn; e += blockDim.x) Bmat_out[e] = bm[e];
+    if (tid < 36) Bd_out[tid] = bd[tid];
+  }
+  const int b = lo + blockIdx.x * blockDim.x + tid;
+  int bad = 0;
+  if (b < hi) {
+    const rh_c128* Uh = d.uhat + (size_t)head * nn * 3 * nw;
+    const rh_c128* Fe = d.finer + (size_t)head * 6 * nw;
+    const double z = zeta[b];
+    cd F[6];
+    drag_exc_bin(d.node, nn, bm, Uh, nw, b, F);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) F[c] = add(scl(ld(Fe + c * nw + b), z), scl(F[c], z));
+    if (fext) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) F[c] = add(F[c], ld(fext + c * nw + b));
+    }
+    cd Z[6][6];
+    assemble_z(d, mbc, b, d.w[b], bd, Z);
+    if (!lu_solve<6>(Z, F)) bad |= 4;
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const cd x = F[c], xl = ld(XL + c * nw + b);
+      if ((x.r != x.r) || (x.i != x.i)) bad |= 2;
+      const double tt = sqrt(abs2(sub(x, xl))) / (sqrt(abs2(x)) + tol);   // raft/raft_model.py:961-962
+      ok = ok && (tt < tol);
+      st(Xi + c * nw + b, x);
+      st(XL + c * nw + b, add(scl(xl, 0.2), scl(x, 0.8)));                 // :991
+    }
+    if (!ok) bad |= 1;
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    if (__builtin_amdgcn_ballot_w64((bad >> q) & 1) != 0 && (tid & 63) == 0) atomicMax(flags + q, 1);
 }
 
 // pass 2: B_drag (36 threads) -- sequential node order like the reference's running sum

@@ -85,6 +85,10 @@ def lib():
                                         _p, _p, _p],
                 "rh_linearize": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, _p, _p, _p, _p, _p, _p],
                 "rh_drag_excitation": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, _p, _p, _p, _p],
+                "rh_lin_partial_sums": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, _p, _p, ctypes.c_int, ctypes.c_int,
+                                        _p, _p],
+                "rh_bin_step": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, _p, _p, _p, ctypes.c_double, ctypes.c_int,
+                                ctypes.c_int, _p, _p, _p, _p, _p, _p],
                 "rh_sea_state": [_p, ctypes.c_int, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p, _p, _p, _p],
                 "rh_motion_stats": [_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, _p, _p, _p, _p],
                 "rh_system_solve": [_p, ctypes.c_int, ctypes.c_int, _p, _p, _p, _p, _p],

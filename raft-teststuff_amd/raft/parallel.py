@@ -106,3 +106,107 @@ def solve_cases_sharded(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd
     if res is None:
         raise ValueError("every rank needs at least one case")
     return gather_cases(dict(res), cases.n, group), (0, cases.n)
+
+
+# ------------------------------------------------------------------------------------------
+# bin sharding of ONE case (SURVEY.md §8(e) row 2)
+# ------------------------------------------------------------------------------------------
+def bin_shard(nw, rank, world):
+    """[lo, hi) of rank's contiguous block of frequency bins."""
+    return case_shard(nw, rank, world)
+
+
+def _all_reduce(t, op, group):
+    dist = _dist()
+    if t.is_cuda and dist.get_backend(group) == "gloo":     # gloo reduces host tensors
+        c = t.cpu()
+        dist.all_reduce(c, op=op, group=group)
+        t.copy_(c)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+
+
+def bin_fixed_point(partial, step, nn, nIter, nw, device=None, group=None, shards=None):
+    """The collective skeleton of the bin-sharded drag fixed point (raft/raft_model.py:918-1000).
+    Per iteration: partial(lo, hi, out) writes this rank's per-node |vrel|^2 sums [3 nn] for
+    each of its bin shards (summed in shard order), one all-reduce(sum) of 3 nn doubles,
+    step(sums, lo, hi, flags) solves its bins and raises flags [not converged, NaN,
+    singular], one all-reduce(max) of the flags.  `shards` overrides this rank's bin ranges
+    (several per process, e.g. to exercise the split on one device).
+    Returns (iterations, status) with status an RH_CASE_* code."""
+    import torch
+    from . import _native as N
+    dist = _dist()
+    rank, world = world_of(group)
+    mine = shards if shards is not None else [bin_shard(nw, rank, world)]
+    sums = torch.zeros(3 * nn, dtype=torch.float64, device=device)
+    part = torch.empty_like(sums)
+    flags = torch.zeros(3, dtype=torch.int32, device=device)
+    for it in range(nIter + 1):                      # the loop runs nIter+1 times (:861)
+        sums.zero_()
+        for lo, hi in mine:
+            partial(lo, hi, part)
+            sums += part
+        if world > 1:
+            _all_reduce(sums, dist.ReduceOp.SUM, group)
+        flags.zero_()
+        for lo, hi in mine:
+            step(sums, lo, hi, flags)
+        if world > 1:
+            _all_reduce(flags, dist.ReduceOp.MAX, group)
+        f = flags.tolist()
+        if f[1]:
+            return it + 1, N.RH_CASE_NAN
+        if f[2]:
+            return it + 1, N.RH_CASE_SINGULAR
+        if not f[0]:
+            return it + 1, N.RH_CASE_CONVERGED
+    return nIter + 1, N.RH_CASE_NOT_CONVERGED
+
+
+def solve_bins_sharded(fowt, case, nIter, XiStart=0.0, tol=0.01, group=None, shards=None):
+    """Model.solveDynamics' drag fixed point for one single-FOWT case with the frequency bins
+    split over the ranks of `group` (rh_lin_partial_sums / rh_bin_step, include/rafthip.h).
+    Every rank ends with the full response: the bin slices are exchanged with one
+    all-reduce(sum) of zero-padded [6, nw] arrays (exact: x + 0 == x).
+    Returns (Xi [6, nw] complex, iterations, status, B_drag [6, 6])."""
+    import ctypes
+
+    import numpy as np
+    import torch
+    from . import _native as N
+    dist = _dist()
+    case = dict(case)
+    fowt.calcHydroExcitation(case, memberList=fowt.memberList)
+    if fowt.nWaves != 1:
+        raise NotImplementedError("solve_bins_sharded: one sea state per case")
+    dd = fowt.device_design()
+    nw, nn, dev = dd.nw, dd.nn, dd.device
+    zeta = fowt._zeta_dev[0].contiguous()
+    head = int(fowt._heads[0])
+    XL = torch.full([6, nw], complex(XiStart, 0.0), dtype=torch.complex128, device=dev)
+    Xi = torch.zeros([6, nw], dtype=torch.complex128, device=dev)
+    Bmat = torch.empty([max(nn, 1) * 9], dtype=torch.float64, device=dev)
+    Bd = torch.empty([36], dtype=torch.float64, device=dev)
+    d = dd.struct()
+    ctx = N.context(dd.dev_index)
+    s = N.stream_handle(torch, dev)
+    L = N.lib()
+
+    def partial(lo, hi, out):
+        N.check(L.rh_lin_partial_sums(ctx, ctypes.byref(d), head, N.ptr(XL), N.ptr(zeta), lo, hi, N.ptr(out), s),
+                "rh_lin_partial_sums")
+
+    def step(sums, lo, hi, flags):
+        N.check(L.rh_bin_step(ctx, ctypes.byref(d), head, N.ptr(zeta), None, N.ptr(sums), float(tol), lo, hi,
+                              N.ptr(Bmat), N.ptr(Bd), N.ptr(Xi), N.ptr(XL), N.ptr(flags), s), "rh_bin_step")
+
+    iters, status = bin_fixed_point(partial, step, nn, nIter, nw, device=dev, group=group, shards=shards)
+    rank, world = world_of(group)
+    if world > 1:
+        _all_reduce(torch.view_as_real(Xi), dist.ReduceOp.SUM, group)
+    if status == N.RH_CASE_NAN:
+        raise Exception("Nan detected in response vector Xi.")       # raft/raft_model.py:957
+    if status == N.RH_CASE_SINGULAR:
+        raise np.linalg.LinAlgError("Singular matrix")
+    return Xi.cpu().numpy(), iters, status, Bd.cpu().numpy().reshape(6, 6)

@@ -137,3 +137,57 @@ def _qtf_check(rank, world):
 
 def test_sharded_qtf_exchange_world2():
     _run(_qtf_check)
+
+
+# ---- bin sharding of one case (raft/parallel.py bin_fixed_point) -------------------------
+def _toy(nw, nn):
+    """A small fixed point with the structure of the drag loop: per-node sums over ALL bins
+    couple the bins; each bin then updates from the global sums; integer-valued data keep
+    every sum exact, so sharded and single-process runs must agree bit for bit."""
+    rng = np.random.default_rng(4)
+    A = torch.tensor(rng.integers(1, 4, size=[nn, nw]).astype(float))
+    state = {"x": torch.ones(nw, dtype=torch.float64), "xi": torch.zeros(nw, dtype=torch.float64)}
+
+    def partial(lo, hi, out):
+        out.copy_(torch.stack([(A[:, lo:hi] * state["x"][lo:hi]).sum(1)] * 3, 1).reshape(-1))
+
+    def step(sums, lo, hi, flags):
+        s = sums.reshape(-1, 3)[:, 0]
+        new = torch.floor((A[:, lo:hi] * s[:, None]).sum(0) / (64.0 * nn))
+        state["xi"][lo:hi] = new
+        if (new != state["x"][lo:hi]).any():
+            flags[0] = 1
+        state["x"][lo:hi] = torch.floor(0.5 * (state["x"][lo:hi] + new))
+    return partial, step, state
+
+
+def _bins_check(rank, world):
+    from raft.parallel import bin_fixed_point, bin_shard
+    nw, nn = 37, 5
+    solo = [dist.new_group([r]) for r in range(world)][rank]     # single-process reference run
+    partial, step, st = _toy(nw, nn)
+    it1, s1 = bin_fixed_point(partial, step, nn, 6, nw, group=solo, shards=[(0, nw)])
+    ref = st["xi"].clone()
+    partial, step, st = _toy(nw, nn)
+    it2, s2 = bin_fixed_point(partial, step, nn, 6, nw)           # this rank's block of bins
+    lo, hi = bin_shard(nw, rank, world)
+    xi = torch.zeros(nw, dtype=torch.float64)
+    xi[lo:hi] = st["xi"][lo:hi]
+    dist.all_reduce(xi)
+    assert (it1, s1) == (it2, s2)
+    np.testing.assert_array_equal(xi.numpy(), ref.numpy())
+
+
+def test_bin_sharded_fixed_point_world2():
+    _run(_bins_check)
+
+
+def test_bin_shards_cover_every_bin_once():
+    from raft.parallel import bin_shard
+    for nw in (1, 7, 80, 1000):
+        for world in (1, 2, 3, 8):
+            seen = np.zeros(nw, dtype=int)
+            for r in range(world):
+                lo, hi = bin_shard(nw, r, world)
+                seen[lo:hi] += 1
+            assert (seen == 1).all()
