@@ -73,6 +73,11 @@ def lib():
             if not os.path.exists(LIB_PATH):
                 raise NativeError(f"librafthip.so not found at {LIB_PATH}: build it with "
                                   "`python -c 'import __graft_entry__ as g; g.build()'`")
+            # torch first: its bundled HIP runtime has the same SONAME (libamdhip64.so.7) as the
+            # one librafthip links, so loading torch first makes both share ONE runtime.  Loaded
+            # the other way round, torch brings a second HIP/HSA runtime into the process and
+            # the library's hipGetDeviceCount finds no device.
+            import torch  # noqa: F401
             L = ctypes.CDLL(LIB_PATH)
             L.rh_last_error.restype = ctypes.c_char_p
             for name, args in {
