@@ -228,7 +228,7 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
            "full_grid_equiv_per_s": n2 * n2 * steps / dt_max,
            "config": {"workload": "C3: OC4semi-RAFT_QTF slender-body QTF, 400x400 (w1,w2) grid, heading 0",
                       "submerged_nodes": qd.nq, "kay_intervals": nkay, "waterline_members": nwl,
-                      "parallelism": f"row-sharded x{world} + all-reduce"},
+                      "parallelism": f"row-sharded x{world} + all-gather of packed pairs"},
            "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                         "frac": achieved / PEAK_FP64, "traffic": pmc_traffic("k_qtf_pairs"),
                         "kernel": "rh_qtf_slender (all launches; traffic: k_qtf_pairs)",

@@ -9,9 +9,8 @@ One process per GPU, torch.distributed with backend "nccl" (RCCL over xGMI).  Tw
 * QTF (w1, w2) pairs -- upper-triangle rows dealt in snake order (round k gives rank r row
   k world + (r if k even else world-1-r)), so every rank gets n2(n2+1)/(2 world) pairs to
   within one row although rows shorten with i1.  The disjoint
-  row shards are exchanged with one all-reduce(sum) of the zero-initialised [n2, n2, 6]
-  matrix (x + 0 == x, so the exchange is exact), then the Hermitian lower triangle is
-  filled on every rank.
+  row shards are exchanged with one all_gather of each rank's packed upper-triangle pairs
+  (exact copies), then the Hermitian lower triangle is filled on every rank.
 
 The collective helpers take any process group; tests run them with gloo on the CPU.
 """
@@ -75,18 +74,44 @@ def gather_cases(local, n_total, group=None):
     return out
 
 
+_PAIR_INDEX = {}
+
+
+def qtf_pair_index(n2, rank, world, device=None):
+    """Flat indices i1 * n2 + i2 of the upper-triangle pairs (i2 >= i1) of rank's rows, in
+    row order (cached per device)."""
+    import torch
+    key = (n2, rank, world, str(device))
+    if key not in _PAIR_INDEX:
+        rows = qtf_rows(n2, rank, world)
+        flat = np.concatenate([i1 * n2 + np.arange(i1, n2) for i1 in rows]) if len(rows) else np.zeros(0, int)
+        _PAIR_INDEX[key] = torch.tensor(flat, dtype=torch.long, device=device)
+    return _PAIR_INDEX[key]
+
+
 def assemble_qtf(compute_rows, hermitian_fill, n2, device=None, group=None):
     """Row-sharded QTF: compute_rows(out, rank, world) writes the upper-triangle rows of
-    `rank` into the zeroed [n2, n2, 6] complex128 tensor `out`; the shards are summed with
-    one all-reduce and hermitian_fill(out) mirrors the lower triangle."""
+    `rank` into the zeroed [n2, n2, 6] complex128 tensor `out`.  The shards are exchanged by
+    ONE all_gather of each rank's packed upper-triangle pairs (about n2^2/2 / world pairs x
+    96 B, padded to the largest shard) and scattered into place; hermitian_fill(out) then
+    mirrors the lower triangle.  Pure copies, so the result is bitwise the single-device
+    matrix; a rank moves ~4x fewer bytes than an all-reduce of the full matrix would."""
     import torch
     dist = _dist()
     rank, world = world_of(group)
     out = torch.zeros([n2, n2, 6], dtype=torch.complex128, device=device)
     compute_rows(out, rank, world)
     if world > 1:
-        v = torch.view_as_real(out)
-        dist.all_reduce(v, op=dist.ReduceOp.SUM, group=group)
+        flat = out.view(n2 * n2, 6)
+        idx = [qtf_pair_index(n2, r, world, device) for r in range(world)]
+        m = max(int(i.numel()) for i in idx)
+        buf = torch.zeros([m, 6], dtype=torch.complex128, device=device)
+        buf[:idx[rank].numel()] = flat.index_select(0, idx[rank])
+        parts = [torch.empty_like(torch.view_as_real(buf)) for _ in range(world)]
+        dist.all_gather(parts, torch.view_as_real(buf), group=group)
+        for r in range(world):
+            if r != rank:
+                flat.index_copy_(0, idx[r], torch.view_as_complex(parts[r])[:idx[r].numel()])
     hermitian_fill(out)
     return out
 

@@ -1,6 +1,7 @@
 """CPU (gloo, world_size 2): the multi-GPU partitioning of raft/parallel.py -- case blocks
-and their final gather, and the row-sharded QTF exchange (all-reduce of disjoint rows +
-Hermitian fill) -- reproduce the single-process results bit for bit."""
+and their final gather, the row-sharded QTF exchange (all-gather of packed disjoint rows +
+Hermitian fill) and the bin-sharded fixed point -- reproduce the single-process results
+bit for bit."""
 import os
 import socket
 
