@@ -28,20 +28,23 @@ class DesignBatch:
     r6      : platform pose for the linearisation (default: the reference position)
     """
 
-    def __init__(self, designs, statics=None, r6=None, device=0, pool=None):
+    def __init__(self, designs, statics=None, r6=None, device=0, pool=None, light=False):
         """pool: optional multiprocessing pool (see host_pool) that prepares the designs on
-        the host in parallel; results are identical to the serial path."""
+        the host in parallel; results are identical to the serial path.
+        light: keep only what the device side needs of each design (HostDesign: its tables,
+        grid and site scalars) instead of the full Model; from a pool this ships ~40 KB per
+        design instead of ~150 KB of Python objects (the parent's unpickling was the cost)."""
         t0 = time.perf_counter()
         if isinstance(statics, dict) or statics is None:
             statics = [statics] * len(designs)
         if len(statics) != len(designs):
             raise ValueError("statics: one dict for all designs or one per design")
-        jobs = [(d, st, r6, device) for d, st in zip(designs, statics)]
+        jobs = [(d, st, r6, device, light) for d, st in zip(designs, statics)]
         if pool is not None and len(jobs) > 1:
             self.models = pool.map(prepare_design, jobs, chunksize=max(1, len(jobs) // (4 * pool._processes)))
         else:
             self.models = [prepare_design(j) for j in jobs]
-        self.fowts = [m.fowtList[0] for m in self.models]
+        self.fowts = [m if isinstance(m, HostDesign) else m.fowtList[0] for m in self.models]
         m0 = self.models[0]
         for m in self.models[1:]:
             if m.nw != m0.nw or not np.array_equal(m.w, m0.w):
@@ -83,7 +86,8 @@ def prepare_design(job):
     excitation coefficients at pose r6): the per-design part of runRAFT before the case loop
     (raft/raft_model.py:30-170, raft/raft_fowt.py:291-565, 848-880).  Pure NumPy, so it can
     run in a worker process; the device tables are built later by the caller."""
-    d, st, r6, device = job
+    d, st, r6, device = job[:4]
+    light = len(job) > 4 and job[4]
     m = Model(d, statics=None if st is None else [st], device=device)
     if m.nFOWT != 1:
         raise NotImplementedError("DesignBatch handles single-FOWT designs (use Model for arrays)")
@@ -92,7 +96,36 @@ def prepare_design(job):
     f.calcStatics()
     f.calcHydroConstants()
     f.host_tables()            # the device-table layout, built here too (travels with the FOWT)
-    return m
+    return HostDesign(m) if light else m
+
+
+class HostDesign:
+    """What the device side needs of one prepared single-FOWT design: its host tables
+    (prep.host_tables), frequency grid, site scalars and solver settings.  Stands in for the
+    FOWT wherever only device_design() is used (DesignBatch light=True)."""
+
+    def __init__(self, model):
+        f = model.fowtList[0]
+        self.nw, self.w, self.k, self.dw = f.nw, np.asarray(model.w), f.k, f.dw
+        self.depth, self.rho_water, self.g = f.depth, f.rho_water, f.g
+        self.nIter, self.XiStart = model.nIter, model.XiStart
+        self.device_index = f.device_index
+        self._host = f.host_tables()
+        self._dd = None
+
+    def host_tables(self):
+        return self._host
+
+    def device_design(self):
+        if self._dd is None:
+            from .prep import DeviceDesign
+            self._dd = DeviceDesign(self, device=self.device_index)
+        return self._dd
+
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st["_dd"] = None
+        return st
 
 
 def _warm_worker(grids):

@@ -44,3 +44,24 @@ def test_pool_matches_serial():
             np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
         assert b.fowtList[0]._dd is None
         assert np.all(b.fowtList[0].A_BEM == 0) and b.fowtList[0].A_BEM.shape == a.fowtList[0].A_BEM.shape
+
+
+def test_light_designs_carry_the_device_tables():
+    """DesignBatch(light=True) ships HostDesign records: the same device tables and scalars
+    as the full prepared model, far smaller when pickled."""
+    import pickle
+    with open(os.path.join(ROOT, "tests", "golden", "designs", "VolturnUS-S_example.json")) as fh:
+        base = json.load(fh)
+    base["settings"]["min_freq"] = 0.005
+    C_moor = np.load(os.path.join(ROOT, "tests", "golden", "c2_nw1000.npz"))["C_moor"]
+    full = prepare_design((base, {"C_moor": C_moor}, None, 0))
+    light = pickle.loads(pickle.dumps(prepare_design((base, {"C_moor": C_moor}, None, 0, True))))
+    a, b = full.fowtList[0].host_tables(), light.host_tables()
+    np.testing.assert_array_equal(a["packed"], b["packed"])
+    np.testing.assert_array_equal(a["mstart"], b["mstart"])
+    assert a["layout"] == b["layout"] and (a["nn"], a["nm"], a["per_bin"]) == (b["nn"], b["nm"], b["per_bin"])
+    f = full.fowtList[0]
+    assert (light.nw, light.dw, light.depth, light.rho_water, light.g) == (f.nw, f.dw, f.depth, f.rho_water, f.g)
+    assert (light.nIter, light.XiStart) == (full.nIter, full.XiStart)
+    np.testing.assert_array_equal(light.w, full.w)
+    assert len(pickle.dumps(light)) < len(pickle.dumps(full)) / 2
