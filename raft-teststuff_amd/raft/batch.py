@@ -54,8 +54,26 @@ class DesignBatch:
         self.nIter, self.XiStart, self.nw, self.w = m0.nIter, m0.XiStart, m0.nw, m0.w
         self.host_seconds = time.perf_counter() - t0
         t0 = time.perf_counter()
-        self.dds = [f.device_design() for f in self.fowts]
+        self.dds = self._upload(device)
         self.upload_seconds = time.perf_counter() - t0
+
+    def _upload(self, device):
+        """Every design's device tables in one host->device copy (plus one for the member
+        ranges); each DeviceDesign holds views of its slices."""
+        import torch
+        from .prep import DeviceDesign, _torch
+        _torch()
+        hs = [f.host_tables() for f in self.fowts]
+        dev = torch.device("cuda", device)
+        packed = torch.tensor(np.concatenate([h["packed"] for h in hs]), dtype=torch.float64, device=dev)
+        mst = torch.tensor(np.concatenate([h["mstart"] for h in hs]).astype(np.int32), dtype=torch.int32, device=dev)
+        dds, off, moff = [], 0, 0
+        for f, h in zip(self.fowts, hs):
+            n, k = h["packed"].size, h["mstart"].size
+            f._dd = DeviceDesign(f, device=device, packed=packed[off:off + n], mstart=mst[moff:moff + k])
+            dds.append(f._dd)
+            off, moff = off + n, moff + k
+        return dds
 
     def __len__(self):
         return len(self.models)
@@ -63,15 +81,20 @@ class DesignBatch:
     def case_set(self, design_idx, cases):
         """CaseSet of (design index, case dict) pairs; one sea state per case."""
         hd, sp, Hs, Tp, gm = [], [], [], [], []
+
+        def one(c, k, dflt=None):
+            v = c.get(k, dflt)
+            if isinstance(v, (list, tuple, np.ndarray)):
+                if len(v) != 1:
+                    raise NotImplementedError("DesignBatch: one sea state per case")
+                return v[0]
+            return v
         for c in cases:
-            one = lambda k, dflt=None: (np.atleast_1d(c.get(k, dflt))[0] if c.get(k, dflt) is not None else None)
-            if not np.isscalar(c["wave_heading"]) and len(c["wave_heading"]) != 1:
-                raise NotImplementedError("DesignBatch: one sea state per case")
-            hd.append(float(one("wave_heading", 0)))
-            sp.append(str(one("wave_spectrum", "JONSWAP")))
-            Hs.append(float(one("wave_height")))
-            Tp.append(float(one("wave_period")))
-            gm.append(float(one("wave_gamma", 0)))
+            hd.append(float(one(c, "wave_heading", 0)))
+            sp.append(str(one(c, "wave_spectrum", "JONSWAP")))
+            Hs.append(float(one(c, "wave_height")))
+            Tp.append(float(one(c, "wave_period")))
+            gm.append(float(one(c, "wave_gamma", 0)))
         return CaseSet(np.asarray(design_idx, dtype=np.int32), hd, sp, Hs, Tp, gm)
 
     def solve(self, design_idx, cases, tol=0.01, want=("psd", "std", "zeta", "B_drag"), prepared=None):

@@ -119,7 +119,9 @@ def host_tables(fowt):
 class DeviceDesign:
     """Device-resident tables of one FOWT design (caller-owned torch buffers)."""
 
-    def __init__(self, fowt, device=0):
+    def __init__(self, fowt, device=0, packed=None, mstart=None):
+        """packed / mstart: this design's slices of device arrays the caller already holds
+        (DesignBatch uploads every design's tables in one copy); otherwise uploaded here."""
         torch = _torch()
         self.torch = torch
         self.device = torch.device("cuda", device)
@@ -127,12 +129,15 @@ class DeviceDesign:
         self.nw = fowt.nw
         h = fowt.host_tables() if hasattr(fowt, "host_tables") else host_tables(fowt)
         self.nn, self.nm, self.per_bin = h["nn"], h["nm"], h["per_bin"]
-        self._packed = torch.tensor(h["packed"], dtype=torch.float64, device=self.device)
+        if packed is not None and packed.numel() != h["packed"].size:
+            raise ValueError("DeviceDesign: packed slice does not match the design's tables")
+        self._packed = packed if packed is not None else torch.tensor(h["packed"], dtype=torch.float64,
+                                                                        device=self.device)
         for name, (off, shape) in h["layout"].items():   # contiguous views of the one upload
             setattr(self, name, self._packed[off:off + int(np.prod(shape))].view(*shape))
         imat = h["imat"]
         self.imat = torch.tensor(imat, dtype=torch.complex128, device=self.device) if imat is not None else None
-        self.mstart = torch.tensor(h["mstart"], dtype=torch.int32, device=self.device)
+        self.mstart = mstart if mstart is not None else torch.tensor(h["mstart"], dtype=torch.int32, device=self.device)
         self.dw, self.depth, self.rho, self.g = float(fowt.dw), float(fowt.depth), float(fowt.rho_water), float(fowt.g)
         self.headings = None           # tuple of tabulated headings (rad)
         self.uhat = None
