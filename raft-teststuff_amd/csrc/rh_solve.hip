@@ -165,7 +165,7 @@ __host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB) {
                            + (size_t)nn               // node axial coordinate t
                            + (size_t)nm * 18          // member cq, c1, c2
                            + (size_t)2 * kLT * NB     // w and zeta per (padded) bin
-                           + 36 + 108 + kLW * 6)      // B_drag, M|B|C image, std partials
+                           + 36 + 108 + kLW * 6 + 36) // B_drag, M|B|C image, std partials, B_lin+B_drag
          + sizeof(int) * ((size_t)nm + 2);            // member node ranges
 }
 
@@ -196,7 +196,8 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
   double* bd = al + nn * 5;                        // [36]
   double* mbc = bd + 36;                           // [108] M, B_lin, C
   double* sred = mbc + 108;                        // [kLW][6]
-  double* bdn = sred + kLW * 6;                    // [36][nn]
+  double* bsum = sred + kLW * 6;                   // [36] B_lin + B_drag of this iteration
+  double* bdn = bsum + 36;                         // [36][nn]
   double* nt = bdn + 36 * nn;                      // [nn]
   double* mbf = nt + nn;                           // [18][nm]
   double* lw = mbf + 18 * nm;                      // [NWP] w per bin (pad bins: w[nw-1])
@@ -373,6 +374,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
       double s = 0;
       for (int n = 0; n < nn; ++n) s += P[n];
       bd[tid] = s;
+      bsum[tid] = mbc[36 + tid] + s;   // the B_lin + B_drag of every bin's Z (same sum as before)
     }
     __syncthreads();
     PROF_T(ta2);
@@ -470,6 +472,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
         const int zo = opaque_zero();
         const double* zm = mbc + zo;
         const double* zb = bd + zo;
+        const double* zs = bsum + zo;
         const double w2 = -(w * w);
         if (d.mb_per_bin) {
           const double* M = d.M + (size_t)b * 36;
@@ -485,7 +488,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
           for (int r = 0; r < 6; ++r) {
 #pragma unroll
             for (int c = 0; c < 6; ++c)
-              Z[r][c] = mk(w2 * zm[6 * r + c] + zm[72 + 6 * r + c], w * (zm[36 + 6 * r + c] + zb[6 * r + c]));
+              Z[r][c] = mk(w2 * zm[6 * r + c] + zm[72 + 6 * r + c], w * zs[6 * r + c]);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
