@@ -411,9 +411,14 @@ __global__ __launch_bounds__(kQtfTile * NWV) RH_QTF_ATTR void k_qtf_pairs(rh_qtf
   const cd O1[9] = {mk(0, 0), scl(om1[2], -1), om1[1], om1[2], mk(0, 0), scl(om1[0], -1), scl(om1[1], -1), om1[0], mk(0, 0)};
   const cd O2[9] = {mk(0, 0), scl(om2[2], -1), om2[1], om2[2], mk(0, 0), scl(om2[0], -1), scl(om2[1], -1), om2[0], mk(0, 0)};
 
-  // Node terms, one block per term group; each block names the tables it reads (the
-  // compiler merges the repeated loads).  Fencing the blocks apart to shorten live ranges
-  // was measured slower: loads can then no longer be issued ahead of the previous block.
+  // Node terms.  The five term groups of a node share their outer operators, so they are
+  // summed before those are applied (linear algebra, reassociated within FP64 rounding):
+  //   f = (rv CM + rve QM) vM + rv CA vA + rv (I - QM) ax + (ai sq) q
+  // vM: second-order potential acceleration (1), convective (2) and body-motion (4)
+  //     accelerations, with G1 and conj(G2) each applied once to the summed vectors;
+  // vA: Rainey axial divergence (3) and the CA terms of the body rotation (5);
+  // ax: the (I - qMat) term of (5);  sq: the pressure terms of (1), (2) and (4).
+  // One translateForce3to6DOF per node instead of five.
 #pragma unroll 1
   for (int n = wv; n < q.nq; n += NWV) {
     const rh_c128* T = wk.node + (size_t)n * QT_COUNT * n2;
@@ -422,166 +427,104 @@ __global__ __launch_bounds__(kQtfTile * NWV) RH_QTF_ATTR void k_qtf_pairs(rh_qtf
     const double rv = rho * qn(q, RH_QN_VI, n);
     const double rve = rho * qn(q, RH_QN_VE, n) * qn(q, RH_QN_CAE, n);
     const double ai = qn(q, RH_QN_AI, n);
-    // (1) second-order potential acceleration and pressure (f_2ndPot :1541-1542, :1587-1588)
-    if (pot_on && rz <= 0) {
-      cd acc2[3], p2;
-      const double kxy = cosh(nk * (rz + h)) / cnh, kz = sinh(nk * (rz + h)) / cnh;
-      const double th = kx * rx + ky * ry + 0 * rz;
-      const cd ph = mk(cos(th), -sin(th));
-      const cd base = mul(scl(aux2, kxy), ph);
-      acc2[0] = scl(base, (w1 - w2) * kx);
-      acc2[1] = scl(base, (w1 - w2) * ky);
-      acc2[2] = mul(mul(scl(aux2, kz), ph), mk(0, (w1 - w2) * nk));
-      p2 = mul(base, mk(0, -rho * (w1 - w2)));
-      double CM[9], QM[9];
-      ldm9(q, RH_QN_CM, n, CM);
-      ldm9(q, RH_QN_QM, n, QM);
-      cd f[3], t3[3], t4[3];
-      rmv(CM, acc2, t3);
-      rmv(QM, acc2, t4);
+    cd vM[3], vA[3], sq = mk(0, 0);
+    cd u1[3], u2[3], vp1[3], vp2[3], ur1[3], ur2[3];
+    ld3s(T, QT_U, n2, i1, u1);
+    ld3(T, QT_U, n2, i2s, u2);
+    ld3s(T, QT_VP, n2, i1, vp1);
+    ld3(T, QT_VP, n2, i2s, vp2);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) f[i] = add(add(scl(t3[i], rv), scl(p2, ai * qv[i])), scl(t4[i], rve));
-      acc6(Q, f, rx, ry, rz);
+    for (int i = 0; i < 3; ++i) {
+      ur1[i] = sub(u1[i], vp1[i]);
+      ur2[i] = sub(u2[i], vp2[i]);
     }
-    // (2) convective acceleration (:1545-1546, 1589) and Bernoulli pressure drop (:1593-1594)
+    // (2) convective acceleration (:1545-1546) + (4) body motion in the first-order field
+    // (:1552-1553): 0.25 [G1 (conj(u2) + i w1 conj(dr2)) + conj(G2) (u1 - i w2 dr1)]
     {
-      cd u1[3], u2c[3], vp1[3], vp2[3], G1[9], G2c[9], c1v[3], c2v[3], conv[3], t3[3], t4[3], t5[3], cu2[3], f[3];
-      ld3s(T, QT_U, n2, i1, u1);
-      ld3(T, QT_U, n2, i2s, u2c);
+      cd dr1[3], d2c[3], x1v[3], x2v[3], c1v[3], c2v[3];
+      ld3s(T, QT_DR, n2, i1, dr1);
+      ld3(T, QT_DR, n2, i2s, d2c);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) u2c[i] = cconj(u2c[i]);
+      for (int i = 0; i < 3; ++i) {
+        d2c[i] = cconj(d2c[i]);
+        x1v[i] = add(cconj(u2[i]), iw(w1, d2c[i]));
+        x2v[i] = add(u1[i], iw(-w2, dr1[i]));
+      }
+      cd G1[9], G2c[9];
 #pragma unroll
       for (int i = 0; i < 9; ++i) {
         G1[i] = lds(T + (size_t)(QT_GU + i) * n2 + i1);
         G2c[i] = cconj(ld(T + (size_t)(QT_GU + i) * n2 + i2s));
       }
-      cmv(G1, u2c, c1v);
-      cmv(G2c, u1, c2v);
+      cmv(G1, x1v, c1v);
+      cmv(G2c, x2v, c2v);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) conv[i] = scl(add(c1v[i], c2v[i]), 0.25);
+      for (int i = 0; i < 3; ++i) vM[i] = scl(add(c1v[i], c2v[i]), 0.25);
+      // pressure: Bernoulli drop of (2) (:1593-1594) and grad p . dr of (4) (:1590-1592)
       double M9[9];
-      ldm9(q, RH_QN_CM, n, M9);
-      rmv(M9, conv, t3);
-      ldm9(q, RH_QN_QM, n, M9);
-      rmv(M9, conv, t4);
-      ld3s(T, QT_VP, n2, i1, vp1);
-      ld3(T, QT_VP, n2, i2s, vp2);
-      cd ur1[3], ur2[3];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        ur1[i] = sub(u1[i], vp1[i]);
-        ur2[i] = sub(cconj(u2c[i]), vp2[i]);
-      }
+      cd t5[3], cu2[3], gp1[3], gp2[3];
       ldm9(q, RH_QN_P12, n, M9);
       rmv(M9, ur1, t5);
       ldm9(q, RH_QN_CA, n, M9);
       rmv(M9, ur2, cu2);
-      cd pd = mk(0, 0);
+      ld3s(T, QT_GP, n2, i1, gp1);
+      ld3(T, QT_GP, n2, i2s, gp2);
+      cd pd = mk(0, 0), pn = mk(0, 0), pm = mk(0, 0);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) pd = add(pd, mul(t5[i], cconj(cu2[i])));
-      pd = scl(pd, -2 * 0.25 * 0.5 * rho);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) f[i] = add(add(scl(t3[i], rv), scl(t4[i], rve)), scl(pd, ai * qv[i]));
-      acc6(Q, f, rx, ry, rz);
+      for (int i = 0; i < 3; ++i) {
+        pd = add(pd, mul(t5[i], cconj(cu2[i])));
+        pn = add(pn, mul(gp1[i], d2c[i]));
+        pm = add(pm, mul(cconj(gp2[i]), dr1[i]));
+      }
+      sq = add(scl(pd, -2 * 0.25 * 0.5 * rho), add(scl(pn, 0.25), scl(pm, 0.25)));
+    }
+    // (1) second-order potential acceleration and pressure (f_2ndPot :1541-1542, :1587-1588)
+    if (pot_on && rz <= 0) {
+      const double kxy = cosh(nk * (rz + h)) / cnh, kz = sinh(nk * (rz + h)) / cnh;
+      const double th = kx * rx + ky * ry + 0 * rz;
+      const cd ph = mk(cos(th), -sin(th));
+      const cd base = mul(scl(aux2, kxy), ph);
+      vM[0] = add(vM[0], scl(base, (w1 - w2) * kx));
+      vM[1] = add(vM[1], scl(base, (w1 - w2) * ky));
+      vM[2] = add(vM[2], mul(mul(scl(aux2, kz), ph), mk(0, (w1 - w2) * nk)));
+      sq = add(sq, mul(base, mk(0, -rho * (w1 - w2))));
     }
     // (3) Rainey axial divergence (raft/helpers.py:228-251)
     {
-      cd u1[3], u2[3], vp1[3], vp2[3], up1[3], up2[3], a[3], t3[3], f[3];
-      ld3s(T, QT_U, n2, i1, u1);
-      ld3(T, QT_U, n2, i2s, u2);
-      ld3s(T, QT_VP, n2, i1, vp1);
-      ld3(T, QT_VP, n2, i2s, vp2);
       const cd dz1 = lds(T + (size_t)QT_DWDZ * n2 + i1), dz2 = ld(T + (size_t)QT_DWDZ * n2 + i2s);
       const cd s1 = add(add(scl(u1[0], qv[0]), scl(u1[1], qv[1])), scl(u1[2], qv[2]));
       const cd s2 = add(add(scl(u2[0], qv[0]), scl(u2[1], qv[1])), scl(u2[2], qv[2]));
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        up1[i] = sub(u1[i], scl(s1, qv[i]));
-        up2[i] = sub(u2[i], scl(s2, qv[i]));
-        a[i] = scl(add(mul(dz1, cconj(sub(up2[i], vp2[i]))), mul(cconj(dz2), sub(up1[i], vp1[i]))), 0.25);
+        const cd up1 = sub(u1[i], scl(s1, qv[i])), up2 = sub(u2[i], scl(s2, qv[i]));
+        vA[i] = scl(add(mul(dz1, cconj(sub(up2, vp2[i]))), mul(cconj(dz2), sub(up1, vp1[i]))), 0.25);
       }
-      const cd aq = add(add(scl(a[0], qv[0]), scl(a[1], qv[1])), scl(a[2], qv[2]));
+      const cd aq = add(add(scl(vA[0], qv[0]), scl(vA[1], qv[1])), scl(vA[2], qv[2]));
 #pragma unroll
-      for (int i = 0; i < 3; ++i) a[i] = sub(a[i], scl(aq, qv[i]));
-      double CA[9];
-      ldm9(q, RH_QN_CA, n, CA);
-      rmv(CA, a, t3);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) f[i] = scl(t3[i], rv);
-      acc6(Q, f, rx, ry, rz);
-    }
-    // (4) body motion in the first-order field (:1552-1553, 1590-1592)
-    {
-      cd dr1[3], d2c[3], G1[9], G2c[9], a1[3], a2[3], an[3], t3[3], t4[3], f[3];
-      ld3s(T, QT_DR, n2, i1, dr1);
-      ld3(T, QT_DR, n2, i2s, d2c);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) d2c[i] = cconj(d2c[i]);
-#pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        G1[i] = lds(T + (size_t)(QT_GU + i) * n2 + i1);
-        G2c[i] = cconj(ld(T + (size_t)(QT_GU + i) * n2 + i2s));
-      }
-      cmv(G1, d2c, a1);
-      cmv(G2c, dr1, a2);
-      // grad du/dt = i w grad u: 0.25 (i w1 G1) conj(dr2) + 0.25 conj(i w2 G2) dr1
-#pragma unroll
-      for (int i = 0; i < 3; ++i) an[i] = add(scl(iw(w1, a1[i]), 0.25), scl(iw(-w2, a2[i]), 0.25));
-      double M9[9];
-      ldm9(q, RH_QN_CM, n, M9);
-      rmv(M9, an, t3);
-      ldm9(q, RH_QN_QM, n, M9);
-      rmv(M9, an, t4);
-      cd gp1[3], gp2[3];
-      ld3s(T, QT_GP, n2, i1, gp1);
-      ld3(T, QT_GP, n2, i2s, gp2);
-      cd pn = mk(0, 0), pm = mk(0, 0);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        pn = add(pn, mul(gp1[i], d2c[i]));
-        pm = add(pm, mul(cconj(gp2[i]), dr1[i]));
-      }
-      const cd pnab = add(scl(pn, 0.25), scl(pm, 0.25));
-#pragma unroll
-      for (int i = 0; i < 3; ++i) f[i] = add(add(scl(t3[i], rv), scl(t4[i], rve)), scl(pnab, ai * qv[i]));
-      acc6(Q, f, rx, ry, rz);
+      for (int i = 0; i < 3; ++i) vA[i] = sub(vA[i], scl(aq, qv[i]));
     }
     // (5) Rainey body-rotation terms (:1556-1575)
+    cd fr[3];
     {
-      cd x1[3], x2[3], y1[3], y2[3], s[3], t3[3], t4[3], t5[3], fr[3];
+      cd x1[3], x2[3], t4[3], t5[3];
+      double CA[9], QM[9];
+      ldm9(q, RH_QN_CA, n, CA);
+      ldm9(q, RH_QN_QM, n, QM);
       const cd va1 = lds(T + (size_t)QT_VA * n2 + i1), va2 = ld(T + (size_t)QT_VA * n2 + i2s);
-      cd va2q[3] = {cconj(scl(va2, qv[0])), cconj(scl(va2, qv[1])), cconj(scl(va2, qv[2]))};
-      cd va1q[3] = {scl(va1, qv[0]), scl(va1, qv[1]), scl(va1, qv[2])};
+      const cd va2q[3] = {cconj(scl(va2, qv[0])), cconj(scl(va2, qv[1])), cconj(scl(va2, qv[2]))};
+      const cd va1q[3] = {scl(va1, qv[0]), scl(va1, qv[1]), scl(va1, qv[2])};
       cd O2c[9];
 #pragma unroll
       for (int i = 0; i < 9; ++i) O2c[i] = cconj(O2[i]);
       cmv(O1, va2q, x1);
       cmv(O2c, va1q, x2);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) s[i] = add(x1[i], x2[i]);
-      double CA[9], QM[9];
-      ldm9(q, RH_QN_CA, n, CA);
-      rmv(CA, s, t3);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) fr[i] = scl(scl(t3[i], -0.25 * 2), rv);
+      for (int i = 0; i < 3; ++i) vA[i] = sub(vA[i], scl(add(x1[i], x2[i]), 0.5));
       cd V1[9], V2c[9];
 #pragma unroll
       for (int i = 0; i < 9; ++i) {
         V1[i] = add(lds(T + (size_t)(QT_GU + i) * n2 + i1), O1[i]);
         V2c[i] = cconj(add(ld(T + (size_t)(QT_GU + i) * n2 + i2s), O2[i]));
-      }
-      cd ur1[3], ur2[3];
-      {
-        cd u1[3], u2[3], vp1[3], vp2[3];
-        ld3s(T, QT_U, n2, i1, u1);
-        ld3(T, QT_U, n2, i2s, u2);
-        ld3s(T, QT_VP, n2, i1, vp1);
-        ld3(T, QT_VP, n2, i2s, vp2);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          ur1[i] = sub(u1[i], vp1[i]);
-          ur2[i] = sub(u2[i], vp2[i]);
-        }
       }
       // aux = 0.25 (V1 conj(CaM u2a) + conj(V2) CaM u1a); aux -= qMat aux
       cd cu1[3], cu2c[3];
@@ -594,11 +537,10 @@ __global__ __launch_bounds__(kQtfTile * NWV) RH_QTF_ATTR void k_qtf_pairs(rh_qtf
       cd ax[3];
 #pragma unroll
       for (int i = 0; i < 3; ++i) ax[i] = scl(add(x1[i], x2[i]), 0.25);
-      ldm9(q, RH_QN_QM, n, QM);
       rmv(QM, ax, t4);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) fr[i] = add(fr[i], scl(sub(ax[i], t4[i]), rv));
-      // u_aux -= qMat u_aux ; aux = 0.25 (CaM V1 conj(u2a) + CaM conj(V2) u1a)
+      for (int i = 0; i < 3; ++i) fr[i] = sub(ax[i], t4[i]);
+      // u_aux -= qMat u_aux ; aux = 0.25 (CaM V1 conj(u2a) + CaM conj(V2) u1a): into vA
       cd w1a[3], w2a[3];
       rmv(QM, ur1, t4);
       rmv(QM, ur2, t5);
@@ -609,11 +551,25 @@ __global__ __launch_bounds__(kQtfTile * NWV) RH_QTF_ATTR void k_qtf_pairs(rh_qtf
       }
       cmv(V1, w2a, x1);
       cmv(V2c, w1a, x2);
-      rmv(CA, x1, y1);
-      rmv(CA, x2, y2);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) fr[i] = add(fr[i], scl(scl(add(y1[i], y2[i]), 0.25), -rv));
-      acc6(Q, fr, rx, ry, rz);
+      for (int i = 0; i < 3; ++i) vA[i] = sub(vA[i], scl(add(x1[i], x2[i]), 0.25));
+      cd tA[3];
+      rmv(CA, vA, tA);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) fr[i] = add(fr[i], tA[i]);
+    }
+    {
+      double CM[9], QM[9], MP[9];
+      ldm9(q, RH_QN_CM, n, CM);
+      ldm9(q, RH_QN_QM, n, QM);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) MP[i] = rv * CM[i] + rve * QM[i];
+      cd tM[3], f[3];
+      rmv(MP, vM, tM);
+      const cd sa = scl(sq, ai);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) f[i] = add(add(tM[i], scl(fr[i], rv)), scl(sa, qv[i]));
+      acc6(Q, f, rx, ry, rz);
     }
   }
   // ---- waterline relative-elevation force (:1602-1630)
