@@ -18,6 +18,7 @@ namespace rh {
 
 constexpr double kDeg2Rad = 0.017453292519943295;   // raft/helpers.py:27-28
 constexpr int kQtfTile = 64;
+constexpr int kKayT = 6;           // doubles per (KAY row, frequency) in QtfWork::kayt
 
 // per-(node, frequency) table fields (complex) [nq][QT_COUNT][n2]
 enum { QT_U = 0, QT_VP = 3, QT_VA = 6, QT_DR = 7, QT_GU = 10, QT_GP = 19, QT_DWDZ = 22, QT_COUNT = 23 };
@@ -31,12 +32,13 @@ struct QtfWork {
   rh_c128* wl;     // [nmq][WT_COUNT][n2]
   rh_c128* freq;   // [FT_COUNT][n2]
   rh_c128* hinv;   // [nkr][n2][12] reciprocals of the Hankel-derivative table q.hank
-  double* kayt;    // [nkr][n2][2] cosh(k R H), sqrt(k R H tanh(k R H)) of every KAY radius row
+  double* kayt;    // [nkr][n2][6] cosh(k R H), sqrt(k R H tanh(k R H)), exp(+-k (z1 + h)), exp(+-k (z2 + h))
+                   //              of every KAY radius row
 };
 
 __host__ __device__ inline size_t qtf_work_elems(const rh_qtf_design& q) {   // complex elements
   return (size_t)q.nq * QT_COUNT * q.n2 + (size_t)q.nmq * WT_COUNT * q.n2 + (size_t)FT_COUNT * q.n2 +
-         (size_t)q.nkr * q.n2 * 12 + ((size_t)q.nkr * q.n2 * 2 + 1) / 2;
+         (size_t)q.nkr * q.n2 * 12 + ((size_t)q.nkr * q.n2 * kKayT + 1) / 2;
 }
 
 // Loads of wave-uniform table entries through the constant address space: the backend
@@ -305,7 +307,9 @@ __device__ __forceinline__ void ld3s(const rh_c128* T, int field, size_t n2, int
 
 // Per (KAY radius row, frequency) factors of the Kim & Yue correction that do not depend on
 // the pair: the reciprocals R_n = 1 / D_n of the Hankel-derivative table, and the interval
-// factors cosh(k R H), sqrt(k R H tanh(k R H)) of raft_member.py:1185-1190 (H = h / R).
+// factors cosh(k R H), sqrt(k R H tanh(k R H)) of raft_member.py:1185-1190 (H = h / R), and
+// the exponentials exp(+-k (z + h)) at both interval ends, from which the pair kernel forms
+// sinh((k1 +- k2)(z + h)) of :1176-1183 by products instead of four sinh per (pair, row).
 __global__ __launch_bounds__(64) void k_qtf_kay(rh_qtf_design q, QtfWork wk) {
   const int f = blockIdx.x * 64 + threadIdx.x, ir = blockIdx.y;
   if (f >= q.n2) return;
@@ -315,9 +319,15 @@ __global__ __launch_bounds__(64) void k_qtf_kay(rh_qtf_design q, QtfWork wk) {
   for (int n = 0; n < 12; ++n) st(R + n, cdiv(mk(1, 0), ld(D + n)));
   const double Rr = q.kray[RH_KR_R * q.nkr + ir];
   const double kh = q.k2[f] * Rr * (q.depth / Rr);
-  double* t = wk.kayt + ((size_t)ir * q.n2 + f) * 2;
+  double* t = wk.kayt + ((size_t)ir * q.n2 + f) * kKayT;
   t[0] = cosh(kh);
   t[1] = sqrt(kh * tanh(kh));
+  const double x1 = q.k2[f] * (q.kray[RH_KR_Z1 * q.nkr + ir] + q.depth);
+  const double x2 = q.k2[f] * (q.kray[RH_KR_Z2 * q.nkr + ir] + q.depth);
+  t[2] = exp(x1);
+  t[3] = exp(-x1);
+  t[4] = exp(x2);
+  t[5] = exp(-x2);
 }
 
 // omega of raft_member.py:1102-1109, 1 / (H'_{n+1}(k1R) conj H'_n(k2R)) - 1 / (H'_n(k1R) conj H'_{n+1}(k2R)),
@@ -386,7 +396,7 @@ __global__ __launch_bounds__(kQtfTile * NWV) RH_QTF_ATTR void k_qtf_pairs(rh_qtf
   }
   // ---- pair constants of the second-order potential (raft/helpers.py:254-291, Q1)
   const bool pot_on = (w1 != w2) && (k1 > 0) && (k2 > 0);
-  double kx = 0, ky = 0, nk = 0, den12 = 1, den21 = 1, tnh = 0, cnh = 1;
+  double kx = 0, ky = 0, nk = 0, den12 = 1, den21 = 1, tnh = 0, cnh = 1, icnh = 1;
   cd aux2 = mk(0, 0);
   if (pot_on) {
     const double b = beta * kDeg2Rad, cb = cos(b), sb = sin(b);
@@ -396,6 +406,7 @@ __global__ __launch_bounds__(kQtfTile * NWV) RH_QTF_ATTR void k_qtf_pairs(rh_qtf
     const double t1 = tanh(k1 * h), t2 = tanh(k2 * h);
     tnh = tanh(nk * h);
     cnh = cosh(nk * h);
+    icnh = 1.0 / cnh;
     den12 = (w1 - w2) * (w1 - w2) / g - nk * tnh;
     den21 = (w2 - w1) * (w2 - w1) / g - nk * tnh;
     const double n12 = (k1 * k1) * (1 - t1 * t1) - 2 * k1 * k2 * (1 + t1 * t2);
@@ -480,9 +491,12 @@ __global__ __launch_bounds__(kQtfTile * NWV) RH_QTF_ATTR void k_qtf_pairs(rh_qtf
     }
     // (1) second-order potential acceleration and pressure (f_2ndPot :1541-1542, :1587-1588)
     if (pot_on && rz <= 0) {
-      const double kxy = cosh(nk * (rz + h)) / cnh, kz = sinh(nk * (rz + h)) / cnh;
+      const double ez = exp(nk * (rz + h)), iez = 1.0 / ez;     // cosh, sinh of nk (z + h)
+      const double kxy = 0.5 * (ez + iez) * icnh, kz = 0.5 * (ez - iez) * icnh;
       const double th = kx * rx + ky * ry + 0 * rz;
-      const cd ph = mk(cos(th), -sin(th));
+      double sth, cth;
+      sincos(th, &sth, &cth);
+      const cd ph = mk(cth, -sth);
       const cd base = mul(scl(aux2, kxy), ph);
       vM[0] = add(vM[0], scl(base, (w1 - w2) * kx));
       vM[1] = add(vM[1], scl(base, (w1 - w2) * ky));
@@ -615,14 +629,20 @@ __global__ __launch_bounds__(kQtfTile * NWV) RH_QTF_ATTR void k_qtf_pairs(rh_qtf
     const bool cj = k1 < k2;
     const double cb = cos(beta), sb = sin(beta);
     const double kkx = k1 * cb - k2 * cb, kky = k1 * sb - k2 * sb;
-    int m = 0;
+    int m = 0, mph = -1;
+    cd ph = mk(1, 0);
 #pragma unroll 1
     for (int ir = NWV - 1 - wv; ir < q.nkr; ir += NWV) {
       while (ldsi(q.kstart + m + 1) <= ir) ++m;          // member of row ir (rows ascend)
       const int r0 = ldsi(q.kstart + m);
       const double wx = qm(q, RH_QM_WLX, m), wy = qm(q, RH_QM_WLY, m), wz = qm(q, RH_QM_WLZ, m);
-      const double thp = kkx * wx + kky * wy + 0 * wz;
-      const cd ph = mk(cos(thp), -sin(thp));
+      if (m != mph) {   // phase of the member's waterline point, once per member (uniform)
+        const double thp = kkx * wx + kky * wy + 0 * wz;
+        double sp, cp;
+        sincos(thp, &sp, &cp);
+        ph = mk(cp, -sp);
+        mph = m;
+      }
       const double pf[3] = {qm(q, RH_QM_PFX, m), qm(q, RH_QM_PFY, m), qm(q, RH_QM_PFZ, m)};
       const double R = ldsd(q.kray + RH_KR_R * q.nkr + ir);
       const rh_c128* D1 = wk.hinv + ((size_t)ir * n2 + i1) * 12;
@@ -643,18 +663,23 @@ __global__ __launch_bounds__(kQtfTile * NWV) RH_QTF_ATTR void k_qtf_pairs(rh_qtf
         const double z1 = ldsd(q.kray + RH_KR_Z1 * q.nkr + ir), z2 = ldsd(q.kray + RH_KR_Z2 * q.nkr + ir);
         const double H = h / R;
         const double k1h = k1R * H, k2h = k2R * H;
+        const double* t1 = wk.kayt + ((size_t)ir * n2 + i1) * kKayT;
+        const double* t2 = wk.kayt + ((size_t)ir * n2 + i2s) * kKayT;
+        // sinh((k1 +- k2) x) = (e^{k1 x} e^{+-k2 x} - e^{-k1 x} e^{-+k2 x}) / 2 at x = z1 + h, z2 + h
+        const double P1 = ldsd(t1 + 2), M1 = ldsd(t1 + 3), P2 = ldsd(t1 + 4), M2 = ldsd(t1 + 5);
+        const double p1 = t2[2], m1 = t2[3], p2 = t2[4], m2 = t2[5];
+        const double ia = 0.5 / (k1h + k2h);
         double Im, Ip;
-        const double a2 = sinh((k1 + k2) * (z2 + h)) / (k1h + k2h), a1 = sinh((k1 + k2) * (z1 + h)) / (k1h + k2h);
+        const double a2 = (P2 * p2 - M2 * m2) * ia, a1 = (P1 * p1 - M1 * m1) * ia;
         if (w1 == w2) {
           Im = 0.5 * (a2 - (z2 + h) / h - a1 + (z1 + h) / h);
           Ip = 0.5 * (a2 + (z2 + h) / h - a1 - (z1 + h) / h);
         } else {
-          const double d2 = sinh((k1 - k2) * (z2 + h)) / (k1h - k2h), d1 = sinh((k1 - k2) * (z1 + h)) / (k1h - k2h);
+          const double id = 0.5 / (k1h - k2h);
+          const double d2 = (P2 * m2 - M2 * p2) * id, d1 = (P1 * m1 - M1 * p1) * id;
           Im = 0.5 * (a2 - d2 - a1 + d1);
           Ip = 0.5 * (a2 + d2 - a1 - d1);
         }
-        const double* t1 = wk.kayt + ((size_t)ir * n2 + i1) * 2;
-        const double* t2 = wk.kayt + ((size_t)ir * n2 + i2s) * 2;
         // coef / (cosh(k1 R H) cosh(k2 R H)) and Ip / (k1R k2R), hoisted out of the n sum
         const double cc = k1h * k2h / (ldsd(t1 + 1) * t2[1] * ldsd(t1) * t2[0]);
         const double ipr = Ip / (k1R * k2R);

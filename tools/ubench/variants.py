@@ -17,6 +17,9 @@ EDITS = {
     "noLU": [("      my_sing |= !lu_solve<6>(Z, F);", "      F[0] = add(F[0], Z[0][0]);")],
     "stXo": [("        st_nt(Xo + c * nw + b, x);", "        st(Xo + c * nw + b, x);")],
     "noXo": [("        st_nt(Xo + c * nw + b, x);", "        if (x.r == 1234.5) st(Xo + c * nw + b, x);")],
+    "qNoPot": [("rh_qtf.hip", "    if (pot_on && rz <= 0) {", "    if (pot_on && rz <= -1e300) {")],
+    "qNoKY": [("rh_qtf.hip", "    for (int ir = NWV - 1 - wv; ir < q.nkr; ir += NWV) {", "    for (int ir = NWV - 1 - wv; ir < 0; ir += NWV) {")],
+    "qNoRot": [("rh_qtf.hip", "    // (5) Rainey body-rotation terms (:1556-1575)\n    cd fr[3];\n    {", "    // (5) Rainey body-rotation terms (:1556-1575)\n    cd fr[3] = {vA[0], vA[1], vA[2]};\n    if (rz < -1e300) {")],
     "noA": [("      for (int n = 0; n < nn; n += 3) {\n        step(KA, n);\n        if (n + 1 < nn) step(KB, n + 1);",
              "      for (int n = 0; n < 0; n += 3) {\n        step(KA, n);\n        if (n + 1 < nn) step(KB, n + 1);")],
     "noC": [("        for (int n = 0; n < nn; n += 3) {\n          step(KA, n);",
