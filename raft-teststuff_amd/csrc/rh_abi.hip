@@ -154,8 +154,8 @@ int rh_wave_tables(rh_ctx* ctx, const rh_design* d, const double* beta, rh_c128*
   if (int r = check_design(*d, false)) return r;
   if (d->nhead < 1) return fail(RH_EINVAL, "rh_wave_tables: nhead must be >= 1");
   RH_HIP(hipSetDevice(ctx->device));
-  dim3 grid((d->nw + 127) / 128, d->nhead);
-  hipLaunchKernelGGL(rh::k_wave_tables, grid, dim3(128), 0, (hipStream_t)stream, *d, beta, uhat, finer, kproj);
+  dim3 grid((d->nw + 63) / 64, d->nhead);
+  hipLaunchKernelGGL(rh::k_wave_tables, grid, dim3(64 * rh::kWtN), 0, (hipStream_t)stream, *d, beta, uhat, finer, kproj);
   RH_HIP(hipGetLastError());
   return RH_OK;
 }

@@ -76,15 +76,23 @@ __global__ __launch_bounds__(256) void k_sea_state(int nw, const double* __restr
 }
 
 // ----------------------------------------------------------------------------------------
-// k_wave_tables: thread per (heading, bin); loop over nodes.
+// k_wave_tables: a workgroup is 64 bins x kWtN node slots of one heading.  Wave s computes
+// node nb + s of every pass (the trigonometry and the uhat / kproj rows are independent per
+// (node, bin)); its six force contributions go through LDS, and wave 0 adds them to F in node
+// order, so F is bitwise the node-serial sum.  kWtN times the waves of a thread-per-bin
+// loop: one design's tables (1000 bins) are 128 waves instead of 16.
 // ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(128) void k_wave_tables(rh_design d, const double* __restrict__ beta,
-                                                      rh_c128* __restrict__ uhat, rh_c128* __restrict__ finer,
-                                                      rh_c128* __restrict__ kproj) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+constexpr int kWtN = 8;
+__global__ __launch_bounds__(64 * kWtN) void k_wave_tables(rh_design d, const double* __restrict__ beta,
+                                                            rh_c128* __restrict__ uhat, rh_c128* __restrict__ finer,
+                                                            rh_c128* __restrict__ kproj) {
+  __shared__ cd fs[kWtN][6][64];
+  const int lb = (int)threadIdx.x & 63, slot = (int)threadIdx.x >> 6;
   const int h = blockIdx.y;
   const int nw = d.nw, nn = d.nn;
-  if (b >= nw) return;
+  const int b0 = blockIdx.x * 64 + lb;
+  const bool okb = b0 < nw;
+  const int b = okb ? b0 : nw - 1;           // pad lanes compute a valid bin and store nothing
   const double w = d.w[b], k = d.k[b], hd = d.depth;
   const double be = beta[h];
   const double cb = cos(be), sb = sin(be);
@@ -92,72 +100,86 @@ __global__ __launch_bounds__(128) void k_wave_tables(rh_design d, const double* 
 #pragma unroll
   for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
   const double* node = d.node;
-  for (int n = 0; n < nn; ++n) {
-    const double x = nf(node, nn, RH_NF_RX, n), y = nf(node, nn, RH_NF_RY, n), z = nf(node, nn, RH_NF_RZ, n);
-    const double th = k * (cb * x + sb * y);
-    const cd e = mk(cos(th), -sin(th));      // exp(-1j*th)
-    double s_sh, c_sh, c_ch;
-    if (k * hd > 89.4) {                     // deep-water switch (raft/helpers.py:133-136)
-      const double ez = exp(k * z);
-      s_sh = ez;
-      c_sh = ez;
-      c_ch = ez + exp(-k * (z + 2.0 * hd));
-    } else {
-      const double skh = sinh(k * hd);
-      s_sh = sinh(k * (z + hd)) / skh;
-      c_sh = cosh(k * (z + hd)) / skh;
-      c_ch = cosh(k * (z + hd)) / cosh(k * hd);
-    }
-    const cd we = scl(e, w);
-    const cd u0 = scl(scl(we, c_sh), cb);
-    const cd u1 = scl(scl(we, c_sh), sb);
-    const cd u2 = scl(iw(w, e), s_sh);
-    rh_c128* U = uhat + ((size_t)(h * nn + n) * 3) * nw + b;
-    st(U, u0);
-    st(U + nw, u1);
-    st(U + 2 * nw, u2);
-    {  // projections on the member axes: the drag loop's only view of the wave field
-      rh_c128* K = kproj + ((size_t)(h * nn + n) * 3) * nw + b;
-      const int fo[3] = {RH_NF_QX, RH_NF_P1X, RH_NF_P2X};
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const double e0 = nf(node, nn, fo[a], n), e1 = nf(node, nn, fo[a] + 1, n), e2 = nf(node, nn, fo[a] + 2, n);
-        st(K + a * nw, add(add(scl(u0, e0), scl(u1, e1)), scl(u2, e2)));
+  for (int nb = 0; nb < nn; nb += kWtN) {
+    const int n = nb + slot;
+    if (n < nn) {
+      const double x = nf(node, nn, RH_NF_RX, n), y = nf(node, nn, RH_NF_RY, n), z = nf(node, nn, RH_NF_RZ, n);
+      const double th = k * (cb * x + sb * y);
+      const cd e = mk(cos(th), -sin(th));      // exp(-1j*th)
+      double s_sh, c_sh, c_ch;
+      if (k * hd > 89.4) {                     // deep-water switch (raft/helpers.py:133-136)
+        const double ez = exp(k * z);
+        s_sh = ez;
+        c_sh = ez;
+        c_ch = ez + exp(-k * (z + 2.0 * hd));
+      } else {
+        const double skh = sinh(k * hd);
+        s_sh = sinh(k * (z + hd)) / skh;
+        c_sh = cosh(k * (z + hd)) / skh;
+        c_ch = cosh(k * (z + hd)) / cosh(k * hd);
       }
-    }
-    // inertial excitation: Imat ud + pDyn a_i q, ud = i w u  (raft/raft_fowt.py:1113-1124)
-    const cd ud[3] = {iw(w, u0), iw(w, u1), iw(w, u2)};
-    const cd pd = scl(scl(e, d.pdyn_rho_g), c_ch);
-    const double ai = nf(node, nn, RH_NF_AI, n);
-    const double q[3] = {nf(node, nn, RH_NF_QX, n), nf(node, nn, RH_NF_QY, n), nf(node, nn, RH_NF_QZ, n)};
-    const cd pa = scl(pd, ai);
-    cd f[3];
-    if (nf(node, nn, RH_NF_MCF, n) != 0.0) {
-      const rh_c128* I = d.imat_mcf + (size_t)n * 9 * nw + b;
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        cd s = mul(ld(I + (3 * r + 0) * nw), ud[0]);
-        s = add(s, mul(ld(I + (3 * r + 1) * nw), ud[1]));
-        s = add(s, mul(ld(I + (3 * r + 2) * nw), ud[2]));
-        f[r] = add(s, scl(pa, q[r]));
+      const cd we = scl(e, w);
+      const cd u0 = scl(scl(we, c_sh), cb);
+      const cd u1 = scl(scl(we, c_sh), sb);
+      const cd u2 = scl(iw(w, e), s_sh);
+      rh_c128* U = uhat + ((size_t)(h * nn + n) * 3) * nw + b;
+      if (okb) {
+        st(U, u0);
+        st(U + nw, u1);
+        st(U + 2 * nw, u2);
       }
-    } else {
+      {  // projections on the member axes: the drag loop's only view of the wave field
+        rh_c128* K = kproj + ((size_t)(h * nn + n) * 3) * nw + b;
+        const int fo[3] = {RH_NF_QX, RH_NF_P1X, RH_NF_P2X};
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        cd s = scl(ud[0], nf(node, nn, RH_NF_I00 + 3 * r + 0, n));
-        s = add(s, scl(ud[1], nf(node, nn, RH_NF_I00 + 3 * r + 1, n)));
-        s = add(s, scl(ud[2], nf(node, nn, RH_NF_I00 + 3 * r + 2, n)));
-        f[r] = add(s, scl(pa, q[r]));
+        for (int a = 0; a < 3; ++a) {
+          const double e0 = nf(node, nn, fo[a], n), e1 = nf(node, nn, fo[a] + 1, n), e2 = nf(node, nn, fo[a] + 2, n);
+          if (okb) st(K + a * nw, add(add(scl(u0, e0), scl(u1, e1)), scl(u2, e2)));
+        }
       }
+      // inertial excitation: Imat ud + pDyn a_i q, ud = i w u  (raft/raft_fowt.py:1113-1124)
+      const cd ud[3] = {iw(w, u0), iw(w, u1), iw(w, u2)};
+      const cd pd = scl(scl(e, d.pdyn_rho_g), c_ch);
+      const double ai = nf(node, nn, RH_NF_AI, n);
+      const double q[3] = {nf(node, nn, RH_NF_QX, n), nf(node, nn, RH_NF_QY, n), nf(node, nn, RH_NF_QZ, n)};
+      const cd pa = scl(pd, ai);
+      cd f[3];
+      if (nf(node, nn, RH_NF_MCF, n) != 0.0) {
+        const rh_c128* I = d.imat_mcf + (size_t)n * 9 * nw + b;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          cd s = mul(ld(I + (3 * r + 0) * nw), ud[0]);
+          s = add(s, mul(ld(I + (3 * r + 1) * nw), ud[1]));
+          s = add(s, mul(ld(I + (3 * r + 2) * nw), ud[2]));
+          f[r] = add(s, scl(pa, q[r]));
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          cd s = scl(ud[0], nf(node, nn, RH_NF_I00 + 3 * r + 0, n));
+          s = add(s, scl(ud[1], nf(node, nn, RH_NF_I00 + 3 * r + 1, n)));
+          s = add(s, scl(ud[2], nf(node, nn, RH_NF_I00 + 3 * r + 2, n)));
+          f[r] = add(s, scl(pa, q[r]));
+        }
+      }
+      const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
+      fs[slot][0][lb] = f[0];
+      fs[slot][1][lb] = f[1];
+      fs[slot][2][lb] = f[2];
+      fs[slot][3][lb] = sub(scl(f[2], ry), scl(f[1], rz));
+      fs[slot][4][lb] = sub(scl(f[0], rz), scl(f[2], rx));
+      fs[slot][5][lb] = sub(scl(f[1], rx), scl(f[0], ry));
     }
-    const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
-    F[0] = add(F[0], f[0]);
-    F[1] = add(F[1], f[1]);
-    F[2] = add(F[2], f[2]);
-    F[3] = add(F[3], sub(scl(f[2], ry), scl(f[1], rz)));
-    F[4] = add(F[4], sub(scl(f[0], rz), scl(f[2], rx)));
-    F[5] = add(F[5], sub(scl(f[1], rx), scl(f[0], ry)));
+    __syncthreads();
+    if (slot == 0) {
+      const int ns = nn - nb < kWtN ? nn - nb : kWtN;
+      for (int s2 = 0; s2 < ns; ++s2)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) F[c] = add(F[c], fs[s2][c][lb]);
+    }
+    __syncthreads();
   }
+  if (slot != 0 || !okb) return;
   rh_c128* Fo = finer + (size_t)h * 6 * nw + b;
 #pragma unroll
   for (int c = 0; c < 6; ++c) st(Fo + c * nw, F[c]);
