@@ -28,7 +28,7 @@ thread_local std::string g_err;
 bool g_force_v2 = false;   // rh_set_solver(1): always use k_solve_cases (parity cross-checks)
 bool g_no_group = false;   // rh_set_solver(2): ignore group_start (one case per workgroup)
 constexpr int kGroupCases = 2;   // lock-step width of k_solve_grp
-int g_qtf_waves = 4;       // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs
+int g_qtf_waves = 0;       // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -114,7 +114,8 @@ int rh_set_solver(int which) {
 int rh_group_cases(void) { return kGroupCases; }
 
 int rh_set_qtf_waves(int waves) {
-  if (waves != 1 && waves != 2 && waves != 4) return fail(RH_EINVAL, "rh_set_qtf_waves: waves=%d (1, 2 or 4)", waves);
+  if (waves != 0 && waves != 1 && waves != 2 && waves != 4)
+    return fail(RH_EINVAL, "rh_set_qtf_waves: waves=%d (0 = auto, 1, 2 or 4)", waves);
   g_qtf_waves = waves;
   return RH_OK;
 }
@@ -397,7 +398,17 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   const int rows = (q->n2 + nrank - 1) / nrank;     // snake rounds (k_qtf_pairs skips i1 >= n2)
   if (rows > 0) {
     const dim3 grid((q->n2 + rh::kQtfTile - 1) / rh::kQtfTile, rows);
-    switch (g_qtf_waves) {        // waves per 64 pairs (rh_set_qtf_waves; default 4)
+    // waves per 64 pairs (rh_set_qtf_waves).  Auto: the upper triangle of this rank is about
+    // n2^2 / (2 nrank) pairs, n2^2 / (128 nrank) tiles.  One wave per tile is the fastest
+    // when the tiles fill the chip (C3 at one GPU: 1,250 tiles, 0.367 ms against 0.392 ms
+    // with 4 waves, profiles/r01_v9/qtf_kaytables_ab.txt); a sharded grid needs more waves
+    // per tile to keep the CUs busy.
+    int waves = g_qtf_waves;
+    if (waves == 0) {
+      const double tiles = (double)q->n2 * q->n2 / (2.0 * rh::kQtfTile * nrank);
+      waves = tiles >= 1024 ? 1 : tiles >= 512 ? 2 : 4;
+    }
+    switch (waves) {
       case 1:
         hipLaunchKernelGGL(rh::k_qtf_pairs<1>, grid, dim3(rh::kQtfTile), 0, s, *q, wk, qtf, rank, nrank, mirror);
         break;

@@ -47,6 +47,8 @@ def test_library_loads_and_binds(libpath):
     assert L.rh_group_cases() >= 1
     assert L.rh_set_solver(2) == N.RH_OK and L.rh_set_solver(0) == N.RH_OK
     assert L.rh_set_solver(7) == N.RH_EINVAL and L.rh_set_solver(0) == N.RH_OK
+    assert L.rh_set_qtf_waves(3) == N.RH_EINVAL and L.rh_set_qtf_waves(4) == N.RH_OK
+    assert L.rh_set_qtf_waves(0) == N.RH_OK   # auto (the default)
     for f in declared_functions():
         assert hasattr(L, f)
 

@@ -31,7 +31,7 @@ def main(tag):
             ref = qh
         d = np.abs(qh - ref).max() / np.abs(ref).max()
         print(f"{tag:10s} waves={waves} QTF {e0.elapsed_time(e1) / 10:8.3f} ms  maxrel vs waves=1 {d:.2e}", flush=True)
-    N.check(N.lib().rh_set_qtf_waves(4), "rh_set_qtf_waves")
+    N.check(N.lib().rh_set_qtf_waves(0), "rh_set_qtf_waves")
 
 
 if __name__ == "__main__":

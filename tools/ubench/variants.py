@@ -20,6 +20,12 @@ EDITS = {
     "qNoPot": [("rh_qtf.hip", "    if (pot_on && rz <= 0) {", "    if (pot_on && rz <= -1e300) {")],
     "qNoKY": [("rh_qtf.hip", "    for (int ir = NWV - 1 - wv; ir < q.nkr; ir += NWV) {", "    for (int ir = NWV - 1 - wv; ir < 0; ir += NWV) {")],
     "qNoRot": [("rh_qtf.hip", "    // (5) Rainey body-rotation terms (:1556-1575)\n    cd fr[3];\n    {", "    // (5) Rainey body-rotation terms (:1556-1575)\n    cd fr[3] = {vA[0], vA[1], vA[2]};\n    if (rz < -1e300) {")],
+    "qKyUnroll": [("rh_qtf.hip", "#pragma unroll 1\n        for (int nn = 0; nn <= 10; ++nn) s = add(s, kay_omega(D1, D2, nn));",
+                   "#pragma unroll\n        for (int nn = 0; nn <= 10; ++nn) s = add(s, kay_omega(D1, D2, nn));"),
+                  ("rh_qtf.hip", "#pragma unroll 1\n        for (int nn = 0; nn <= 10; ++nn) s = add(s, scl(kay_omega",
+                   "#pragma unroll\n        for (int nn = 0; nn <= 10; ++nn) s = add(s, scl(kay_omega")],
+    "qKyUnroll4": [("rh_qtf.hip", "#pragma unroll 1\n        for (int nn = 0; nn <= 10; ++nn) s = add(s, scl(kay_omega",
+                   "#pragma unroll 4\n        for (int nn = 0; nn <= 10; ++nn) s = add(s, scl(kay_omega")],
     "noA": [("      for (int n = 0; n < nn; n += 3) {\n        step(KA, n);\n        if (n + 1 < nn) step(KB, n + 1);",
              "      for (int n = 0; n < 0; n += 3) {\n        step(KA, n);\n        if (n + 1 < nn) step(KB, n + 1);")],
     "noC": [("        for (int n = 0; n < nn; n += 3) {\n          step(KA, n);",
