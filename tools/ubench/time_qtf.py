@@ -15,7 +15,7 @@ def main(tag):
     from raft import _native as N
     T, f, qd, dd, X, M66, w2, k2, nkay, nwl = bench.build_qtf(0)
     ref = None
-    for waves in ((4,) if tag == "pmc" else (1, 2, 4)):     # PMC passes: the default kernel only
+    for waves in ((0,) if tag == "pmc" else (1, 2, 4)):     # PMC passes: the default (auto) kernel only
         N.check(N.lib().rh_set_qtf_waves(waves), "rh_set_qtf_waves")
         for _ in range(2):
             q = qd.qtf(dd.w, X, M66)
