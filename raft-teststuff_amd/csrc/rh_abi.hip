@@ -381,18 +381,10 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   wk.hinv = wk.freq + (size_t)rh::FT_COUNT * q->n2;
   wk.kayt = reinterpret_cast<double*>(wk.hinv + (size_t)q->nkr * q->n2 * 12);
   const int nb = (q->n2 + 63) / 64;
-  if (q->nkr > 0) {
-    hipLaunchKernelGGL(rh::k_qtf_kay, dim3(nb, q->nkr), dim3(64), 0, s, *q, wk);
-    RH_HIP(hipGetLastError());
-  }
   hipLaunchKernelGGL(rh::k_qtf_freq, dim3(nb), dim3(64), 0, s, *q, nw, w, Xi0, M66, wk);
   RH_HIP(hipGetLastError());
-  if (q->nq > 0) {
-    hipLaunchKernelGGL(rh::k_qtf_nodes, dim3(nb, q->nq), dim3(64), 0, s, *q, wk);
-    RH_HIP(hipGetLastError());
-  }
-  if (q->nmq > 0) {
-    hipLaunchKernelGGL(rh::k_qtf_wl, dim3(nb, q->nmq), dim3(64), 0, s, *q, wk);
+  if (q->nq + q->nmq + q->nkr > 0) {   // node, waterline and KAY tables: one launch
+    hipLaunchKernelGGL(rh::k_qtf_tables, dim3(nb, q->nq + q->nmq + q->nkr), dim3(64), 0, s, *q, wk);
     RH_HIP(hipGetLastError());
   }
   const int rows = (q->n2 + nrank - 1) / nrank;     // snake rounds (k_qtf_pairs skips i1 >= n2)

@@ -3,9 +3,10 @@
 //   k_qtf_freq   : per second-order frequency: RAO resampled from the first-order grid
 //                  (np.interp, left=right=0, raft/raft_fowt.py:1415-1417), first-order force
 //                  F1st = M a (:1437-1439), rotation generator i w theta (:1556-1557)
-//   k_qtf_nodes  : per (node, frequency): incident velocity u, node displacement/velocity,
+//   k_qtf_tables : one launch of the three per-frequency table kinds below:
+//   qtf_nodes_at : per (node, frequency): incident velocity u, node displacement/velocity,
 //                  grad u (raft/helpers.py:157-195), grad p (:202-225), axial projections
-//   k_qtf_wl     : per (member, frequency): waterline kinematics (raft/raft_fowt.py:1486-1502)
+//   qtf_wl_at    : per (member, frequency): waterline kinematics (raft/raft_fowt.py:1486-1502)
 //   k_qtf_pairs  : per (w1 <= w2) pair: Pinkster IV + every node term + waterline term +
 //                  Kim & Yue correction, then the Hermitian fill (:1449-1640, raft_member.py:1090-1205)
 //   k_force2nd   : difference-frequency force spectrum with on-the-fly bilinear resampling
@@ -162,9 +163,7 @@ __device__ __forceinline__ void airy_u(double w, double k, double beta, double h
   if (eta_out) *eta_out = scl(e, c_ch);   // pDyn with rho = g = 1 (raft/raft_fowt.py:1493)
 }
 
-__global__ __launch_bounds__(64) void k_qtf_nodes(rh_qtf_design q, QtfWork wk) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = blockIdx.y;
+__device__ __forceinline__ void qtf_nodes_at(const rh_qtf_design& q, const QtfWork& wk, int f, int n) {
   const int n2 = q.n2;
   if (f >= n2) return;
   const double w = q.w2[f], k = q.k2[f], h = q.depth, beta = q.beta;
@@ -255,9 +254,7 @@ __global__ __launch_bounds__(64) void k_qtf_nodes(rh_qtf_design q, QtfWork wk) {
   st(T + (size_t)QT_DWDZ * n2, dwdz);
 }
 
-__global__ __launch_bounds__(64) void k_qtf_wl(rh_qtf_design q, QtfWork wk) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  const int m = blockIdx.y;
+__device__ __forceinline__ void qtf_wl_at(const rh_qtf_design& q, const QtfWork& wk, int f, int m) {
   const int n2 = q.n2;
   if (f >= n2) return;
   rh_c128* T = wk.wl + (size_t)m * WT_COUNT * n2 + f;
@@ -310,8 +307,7 @@ __device__ __forceinline__ void ld3s(const rh_c128* T, int field, size_t n2, int
 // factors cosh(k R H), sqrt(k R H tanh(k R H)) of raft_member.py:1185-1190 (H = h / R), and
 // the exponentials exp(+-k (z + h)) at both interval ends, from which the pair kernel forms
 // sinh((k1 +- k2)(z + h)) of :1176-1183 by products instead of four sinh per (pair, row).
-__global__ __launch_bounds__(64) void k_qtf_kay(rh_qtf_design q, QtfWork wk) {
-  const int f = blockIdx.x * 64 + threadIdx.x, ir = blockIdx.y;
+__device__ __forceinline__ void qtf_kay_at(const rh_qtf_design& q, const QtfWork& wk, int f, int ir) {
   if (f >= q.n2) return;
   const rh_c128* D = q.hank + ((size_t)ir * q.n2 + f) * 12;
   rh_c128* R = wk.hinv + ((size_t)ir * q.n2 + f) * 12;
@@ -328,6 +324,24 @@ __global__ __launch_bounds__(64) void k_qtf_kay(rh_qtf_design q, QtfWork wk) {
   t[3] = exp(-x1);
   t[4] = exp(x2);
   t[5] = exp(-x2);
+}
+
+// k_qtf_tables: every per-(node | waterline member | KAY row, frequency) table in one launch
+// (blockIdx.y = node, then member, then KAY row), after k_qtf_freq.  One launch instead of
+// three small ones whose grids (a few hundred waves each) left the GPU mostly idle.
+__global__ __launch_bounds__(64) void k_qtf_tables(rh_qtf_design q, QtfWork wk) {
+  const int f = blockIdx.x * 64 + threadIdx.x;
+  int y = blockIdx.y;
+  if (y < q.nq) {
+    qtf_nodes_at(q, wk, f, y);
+    return;
+  }
+  y -= q.nq;
+  if (y < q.nmq) {
+    qtf_wl_at(q, wk, f, y);
+    return;
+  }
+  qtf_kay_at(q, wk, f, y - q.nmq);
 }
 
 // omega of raft_member.py:1102-1109, 1 / (H'_{n+1}(k1R) conj H'_n(k2R)) - 1 / (H'_n(k1R) conj H'_{n+1}(k2R)),
