@@ -165,8 +165,8 @@ int rh_set_solver(int which);
 int rh_group_cases(void);
 
 /* Waves per 64 (w1, w2) pairs in the QTF pair kernel (process-wide; not part of the
- * reference API): 1, 2, 4, or 0 (default: chosen per launch from the number of 64-pair tiles
- * of this rank, 1 wave when the tiles alone fill the GPU, more when a sharded grid is small).
+ * reference API): 1, 2, 4, or 0 (default: auto, currently 4 waves, the fastest measured
+ * both on one GPU and for a row-sharded grid).
  * The per-pair terms are split over the waves and summed in a fixed order, so the result
  * differs between settings only by rounding.
  * Used by the tests and the kernel-tuning scripts. */

@@ -390,16 +390,11 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   const int rows = (q->n2 + nrank - 1) / nrank;     // snake rounds (k_qtf_pairs skips i1 >= n2)
   if (rows > 0) {
     const dim3 grid((q->n2 + rh::kQtfTile - 1) / rh::kQtfTile, rows);
-    // waves per 64 pairs (rh_set_qtf_waves).  Auto: the upper triangle of this rank is about
-    // n2^2 / (2 nrank) pairs, n2^2 / (128 nrank) tiles.  One wave per tile is the fastest
-    // when the tiles fill the chip (C3 at one GPU: 1,250 tiles, 0.367 ms against 0.392 ms
-    // with 4 waves, profiles/r01_v9/qtf_kaytables_ab.txt); a sharded grid needs more waves
-    // per tile to keep the CUs busy.
-    int waves = g_qtf_waves;
-    if (waves == 0) {
-      const double tiles = (double)q->n2 * q->n2 / (2.0 * rh::kQtfTile * nrank);
-      waves = tiles >= 1024 ? 1 : tiles >= 512 ? 2 : 4;
-    }
+    // waves per 64 pairs (rh_set_qtf_waves).  Auto = 4.  With the tiles starting on the
+    // diagonal, 4 waves per tile are the fastest on one GPU too (C3: 0.294 ms against 0.33 ms
+    // with 1 or 2 waves, profiles/r01_v11/qtf_diag_tiles_ab.txt), and a sharded grid needs
+    // them to keep the CUs busy.
+    const int waves = g_qtf_waves == 0 ? 4 : g_qtf_waves;
     switch (waves) {
       case 1:
         hipLaunchKernelGGL(rh::k_qtf_pairs<1>, grid, dim3(rh::kQtfTile), 0, s, *q, wk, qtf, rank, nrank, mirror);

@@ -379,10 +379,13 @@ __global__ __launch_bounds__(kQtfTile * NWV) RH_QTF_ATTR void k_qtf_pairs(rh_qtf
   const int i1 = kr * nrank + ((kr & 1) ? nrank - 1 - rank : rank);
   const int lane = (int)threadIdx.x & (kQtfTile - 1);
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kQtfTile);
-  const int i2 = blockIdx.x * kQtfTile + lane;
+  // Tile t of row i1 covers w2 = i1 + 64 t .. i1 + 64 t + 63: the tiles start on the diagonal,
+  // so only the last tile of a row is partial (C3: 1,456 tiles instead of 1,744 aligned ones,
+  // 14 % idle lanes instead of 28 %).
+  const int i2 = i1 + (int)blockIdx.x * kQtfTile + lane;
   const int n2 = q.n2;
-  if (i1 >= n2 || (int)blockIdx.x * kQtfTile + kQtfTile - 1 < i1) return;     // block-uniform
-  const bool active = i2 < n2 && i2 >= i1 && q.w2[i2] >= q.w2[i1];
+  if (i1 >= n2 || i1 + (int)blockIdx.x * kQtfTile >= n2) return;     // block-uniform
+  const bool active = i2 < n2 && q.w2[i2] >= q.w2[i1];
   const int i2s = active ? i2 : i1;         // inactive lanes compute a harmless valid pair
   const double w1 = ldsd(q.w2 + i1), w2 = q.w2[i2s], k1 = ldsd(q.k2 + i1), k2 = q.k2[i2s];
   const double h = q.depth, rho = q.rho, g = q.g, beta = q.beta;
