@@ -26,7 +26,7 @@ NCASE = 512
 PEAK_FP64 = 78.6e12   # MI355X FP64 dense peak (vector = matrix rate), FLOP/s
 # HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950
 # correction of MI355X_MICROARCH.md + WRITE_SIZE), written by tools/pmc_summary.py
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v10", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v12", "pmc_summary.json")
 
 
 def pmc_traffic(kernel):
