@@ -125,12 +125,30 @@ def _cpu_worker(job):
     return pairs, time.perf_counter() - t0
 
 
-def cpu_baselines(max_procs=16, qtf_seconds=10.0):
-    """CPU baseline on the box's host cores: P = min(affinity, max_procs)
-    single-threaded worker processes.  C2 leg: P whole cases (one per worker, ~20 s wall);
+def host_cores():
+    """(P, note): the host cores this process may run on -- len(os.sched_getaffinity(0)), as
+    SURVEY.md §8(d) prescribes -- capped by the cgroup CPU quota when one is set (a GPU box
+    shows the whole machine's cores in the affinity mask but grants this job a share of
+    them: more single-threaded workers than the quota would only time-slice)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(float(q) // float(per)))
+    except (OSError, ValueError):
+        pass
+    P = aff if quota is None else min(aff, quota)
+    return P, f"affinity {aff} cores, cgroup quota {quota if quota is not None else 'none'}"
+
+
+def cpu_baselines(qtf_seconds=10.0):
+    """CPU baseline on the box's host cores: P = host_cores() single-
+    threaded worker processes.  C2 leg: P whole cases (one per worker, ~10-20 s wall);
     QTF leg: every worker computes C3 sub-grid QTFs for `qtf_seconds`.  Wall clock."""
     import multiprocessing as mp
-    P = max(1, min(len(os.sched_getaffinity(0)), max_procs))
+    P, cores_note = host_cores()
     try:
         with open("/proc/cpuinfo") as fh:
             model = next((l.split(":", 1)[1].strip() for l in fh if l.startswith("model name")), "unknown")
@@ -149,11 +167,11 @@ def cpu_baselines(max_procs=16, qtf_seconds=10.0):
     case = {"value": P / dt, "unit": "cases/s", "cores": P, "kind": "port",
             "sample": f"{P} C2 cases (nw=1000, seeded JONSWAP) through oracle/raft_oracle.py loop=True (the "
                       f"reference's per-node/per-bin loop structure), one per single-threaded process on {P} "
-                      f"cores, {dt:.1f} s wall, {per_case:.1f} s/case/core; CPU {model}"}
+                      f"cores ({cores_note}), {dt:.1f} s wall, {per_case:.1f} s/case/core; CPU {model}"}
     qtf = {"value": npairs / dq, "unit": "pairs/s", "cores": P, "kind": "port",
            "sample": f"{npairs} pairs (24-frequency subsets of the C3 400 grid) through oracle/qtf_oracle.py "
                      f"(vectorised over pairs, faster per pair than the reference's 19-23 ms) on {P} cores, "
-                     f"{dq:.1f} s wall; CPU {model}"}
+                     f"{dq:.1f} s wall ({cores_note}); CPU {model}"}
     return case, qtf
 
 
@@ -167,11 +185,11 @@ W400 = (0.04, 0.35, 0.000825)      # C3 second-order grid [Hz]: 400 frequencies,
 
 def build_qtf(device):
     """C3: OC4semi-RAFT_QTF slender-body QTF on the 400-frequency grid, RAO Xi0 of the
-    reference's first convergence (tests/golden/c3_qtf.npz)."""
+    reference's first convergence (tests/golden/c3_qtf.npz).  Returns the model pieces; the
+    QtfDevice (host tables incl. the hankel1 table + upload) is built by the caller, timed."""
     import raft
     import torch
     from raft.hydro_math import wave_numbers
-    from raft.qtf import QtfDevice
     T = dict(np.load(os.path.join(ROOT, "tests", "golden", "c3_qtf.npz")))
     with open(os.path.join(ROOT, "tests", "golden", "designs", "OC4semi-RAFT_QTF.json")) as fh:
         design = json.load(fh)
@@ -184,23 +202,36 @@ def build_qtf(device):
     f.calcHydroConstants()
     w2 = np.arange(W400[0], W400[1] + 0.5 * W400[0], W400[2]) * 2 * np.pi
     k2 = wave_numbers(w2, f.depth)
-    qd = QtfDevice(f, w2, k2, 0.0, device)
     dd = f.device_design()
     X = torch.tensor(T["out_Xi0"], dtype=torch.complex128, device=dd.device)
     M66 = torch.tensor(f.M_struc, dtype=torch.float64, device=dd.device).contiguous()
-    qm = qd.host["qmemb"]
-    nkay = qd.nkr - int((qm[29] != 0).sum()) if qd.nmq else 0     # KAY rows minus one waterline row per member
-    nwl = int((qm[0] != 0).sum()) if qd.nmq else 0
-    return T, f, qd, dd, X, M66, w2, k2, nkay, nwl
+    return T, f, dd, X, M66, w2, k2
 
 
 def bench_qtf(device, steps, warmup, world, rank, dist):
+    """C3 throughput: one 400x400 QTF per step (upper triangle computed, Hermitian fill), rows
+    sharded over the ranks with one all-gather of packed pairs.  end_to_end_ms: a cold QTF
+    including the per-(design, grid, heading) host tables (hankel1) and their upload."""
     import torch
-    T, f, qd, dd, X, M66, w2, k2, nkay, nwl = build_qtf(device)
+    from raft.qtf import QtfDevice
+    T, f, dd, X, M66, w2, k2 = build_qtf(device)
+    group = dist.group.WORLD if world > 1 else None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    qd = QtfDevice(f, w2, k2, 0.0, device)
+    t_tables = time.perf_counter() - t0
+    q = qd.qtf(dd.w, X, M66, group=group)
+    torch.cuda.synchronize()
+    t_e2e = time.perf_counter() - t0
+    qm = qd.host["qmemb"]
+    nkay = qd.nkr - int((qm[29] != 0).sum()) if qd.nmq else 0     # KAY rows minus one waterline row per member
+    nwl = int((qm[0] != 0).sum()) if qd.nmq else 0
     n2 = len(w2)
     npair = n2 * (n2 + 1) // 2
     for _ in range(warmup):
-        q = qd.qtf(dd.w, X, M66)
+        q = qd.qtf(dd.w, X, M66, group=group)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
@@ -208,32 +239,35 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(steps):
+    for i in range(steps):         # kernel time: start -> this rank's rows computed (before the exchange)
         ev[i][0].record(stream)
-        q = qd.qtf(dd.w, X, M66)
-        ev[i][1].record(stream)
+        q = qd.qtf(dd.w, X, M66, group=group, on_computed=lambda e=ev[i][1]: e.record(stream))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{device}")
+    t = torch.tensor([dt, t_e2e, t_tables], dtype=torch.float64, device=f"cuda:{device}")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt_max = float(t.item())
+    dt_max, e2e_max, tab_max = (float(x) for x in t.cpu())
     ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     fpp = qtf_flops_per_pair(qd.nq, nkay, nwl)
-    achieved = fpp * npair / (ms * 1e-3) / world
+    from raft.parallel import qtf_pairs_of
+    mine = qtf_pairs_of(n2, rank, world)
+    achieved = fpp * mine / (ms * 1e-3)
     out = {"metric": "QTF pairs/sec", "value": npair * steps / dt_max, "unit": "pairs/s", "steps": steps,
-           "ms_per_qtf": dt_max / steps * 1e3, "scaling": "strong", "n2": n2, "pairs_per_qtf": npair,
+           "ms_per_qtf": dt_max / steps * 1e3, "end_to_end_ms": e2e_max * 1e3, "host_tables_ms": tab_max * 1e3,
+           "scaling": "strong", "n_gpus": world, "n2": n2, "pairs_per_qtf": npair,
            "full_grid_equiv_per_s": n2 * n2 * steps / dt_max,
            "config": {"workload": "C3: OC4semi-RAFT_QTF slender-body QTF, 400x400 (w1,w2) grid, heading 0",
                       "submerged_nodes": qd.nq, "kay_intervals": nkay, "waterline_members": nwl,
                       "parallelism": f"row-sharded x{world} + all-gather of packed pairs"},
-           "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
+           "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                         "frac": achieved / PEAK_FP64, "traffic": pmc_traffic("k_qtf_pairs"),
-                        "kernel": "rh_qtf_slender (all launches; traffic: k_qtf_pairs)",
-                        "kernel_ms": ms, "flops_per_pair": fpp,
-                        "note": "FP64 VALU; algorithmic FLOPs from SURVEY.md §8(d); per-GPU rate"}}
+                        "kernel": "rh_qtf_slender%s (table + pair launches of this rank)" % ("_rows" if world > 1 else ""),
+                        "kernel_ms": ms, "flops_per_pair": fpp, "pairs_this_rank": mine,
+                        "note": "FP64 VALU (no MFMA, DESIGN.md §4); algorithmic FLOPs from SURVEY.md §8(d) over "
+                                "this rank's pairs; traffic = HBM bytes per k_qtf_pairs launch (PMC)"}}
     return out
 
 
@@ -329,6 +363,48 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
                        "host_prep_workers_per_rank": nproc}}
 
 
+def relaunch(nproc, argv):
+    """`bench.py --gpus N` started as a plain process: run it again as N ranks under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) as a CHILD process,
+    before this process touches the GPU, and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def harness_check(args, world, rank):
+    """--harness-check: the multi-rank harness without a GPU (gloo, CPU): barrier, K timed
+    stub steps, max-over-ranks time, one JSON line from rank 0.  tests/test_bench.py runs it."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    for _ in range(args.warmup):
+        time.sleep(0.001)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001 * (1 + rank))
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "harness check", "value": args.ncase * world * args.steps / float(t.item()),
+                          "unit": "cases/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": float(t.item()) / args.steps * 1e3, "ranks_seen": world}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -338,11 +414,19 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-qtf", action="store_true")
     ap.add_argument("--no-c5", action="store_true")
+    ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--harness-check", action="store_true", help="multi-rank harness only (gloo, no GPU)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args.gpus, sys.argv[1:]))       # N ranks, one per GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; using {world} ranks", file=sys.stderr)
+    if args.harness_check:
+        return harness_check(args, world, rank)
     baselines = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         baselines = cpu_baselines()          # before this process initialises the GPU
@@ -365,23 +449,28 @@ def main():
                  [0.0] * len(cases))
     prep = prepare_batch([dd], cs)
     want = ("psd", "std", "zeta", "rao")
+    stream = torch.cuda.current_stream()
 
-    def step():
+    def step(e=None):
+        """One C2 step: the per-heading wave tables of the design (k_wave_tables, all headings
+        of the batch in one launch) and the batched drag fixed point (k_solve_lds)."""
+        dd.retabulate()
+        if e is not None:
+            e.record(stream)
         return solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=want, prepared=prep)
 
     for _ in range(args.warmup):
         res = step()
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         ev[i][0].record(stream)
-        res = step()
-        ev[i][1].record(stream)
+        res = step(ev[i][1])
+        ev[i][2].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -390,7 +479,8 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt_max = float(t.item())
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    tab_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    kern_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
 
     iters = res["iters"].cpu().numpy()
     status = res["status"].cpu().numpy()
@@ -413,22 +503,27 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": "C2: VolturnUS-S_example nw=1000, 512 JONSWAP sea states per GPU per step",
+        "config": {"workload": "C2: VolturnUS-S_example nw=1000, 512 JONSWAP sea states per GPU per step "
+                               "(step = per-heading wave tables + batched drag fixed point)",
                    "cases_per_step_per_gpu": args.ncase, "nw": dd.nw, "submerged_nodes": dd.nn,
-                   "nodes_circ_rect": [nc, nr], "nIter": int(m.nIter), "parallelism": f"case-sharded x{world}"},
-        "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
+                   "nodes_circ_rect": [nc, nr], "nIter": int(m.nIter), "headings": len(dd.headings),
+                   "parallelism": f"case-sharded x{world}"},
+        "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP64, "traffic": pmc_traffic(solve_kernel_name(dd.nw).split("<")[0]),
                      "l2": pmc_l2(solve_kernel_name(dd.nw).split("<")[0], kern_ms),
                      "kernel": solve_kernel_name(dd.nw), "kernel_ms": kern_ms,
+                     "wave_tables_ms": tab_ms,
                      "flops_per_launch": flops,
-                     "note": "FP64 VALU bound (peak = MI355X FP64 vector = matrix rate); algorithmic FLOPs from "
-                             "SURVEY.md §8(d); traffic = HBM bytes per launch from "
-                             + os.path.relpath(PMC_SUMMARY, ROOT)},
+                     "note": "FP64 VALU bound (no MFMA, DESIGN.md §4; peak = MI355X FP64 vector rate); algorithmic "
+                             "FLOPs from SURVEY.md §8(d) over the solve launch (HIP events on its stream); traffic = "
+                             "HBM bytes per launch from " + os.path.relpath(PMC_SUMMARY, ROOT)},
         "iterations_mean": float(iters.mean()),
         "converged_frac": float((status == 1).mean()),
     }
     if not args.no_qtf:
         line["qtf"] = bench_qtf(device, max(3, args.steps // 4), 1, world, rank, dist)
+    if not args.no_c4 and "bench_c4" in globals():
+        line["c4"] = bench_c4(device, max(3, args.steps // 4), world, rank, dist)
     if not args.no_c5:
         line["c5"] = bench_c5(device, max(3, args.steps // 4), world, rank, dist, pool, nproc)
     if pool is not None:

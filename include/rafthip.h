@@ -147,6 +147,11 @@ typedef struct {
   rh_c128* Z;             /* [ncase][nw][36] final impedance (fowt.Z, raft/raft_model.py:1013) */
   rh_c128* Xi_prev;       /* [ncase][6][nw] XiLast of the final iteration (the un-relaxed iterate the
                              potSecOrder=1 second pass restarts from, Q6), or NULL */
+  double* margin;         /* [ncase] closest call of the convergence test, or NULL: over the
+                             executed iterations, the value m = max_{bin,dof} |Xi-XiLast|/(|Xi|+tol)
+                             - tol (raft/raft_model.py:961-962) with the smallest |m|.  m < 0 means
+                             that iteration passed.  |m| near rounding level marks a case whose
+                             iteration count could flip between implementations. */
 } rh_solve_out;
 
 const char* rh_last_error(void);
@@ -154,23 +159,23 @@ int rh_ctx_create(int device, rh_ctx** out);
 int rh_ctx_destroy(rh_ctx* ctx);
 int rh_version(void);
 
-/* Kernel selection for rh_solve_cases (process-wide; not part of the reference API):
- * 0 = automatic (the grouped kernel when group_start is given; else the LDS-resident fast
- * path when nw <= 1024 and the node tables fit in LDS; else the general kernel),
- * 1 = always the general kernel, 2 = never the grouped kernel (one case per workgroup).  Used by the parity tests to
- * cross-check the two device paths on the same inputs. */
-int rh_set_solver(int which);
+/* Kernel selection for rh_solve_cases on this context (not part of the reference API):
+ * 0 = automatic (the grouped kernel when group_start is given and no margin is requested;
+ * else the LDS-resident fast path when nw <= 1024 and the node tables fit in LDS; else the
+ * general kernel), 1 = always the general kernel, 2 = never the grouped kernel (one case per
+ * workgroup).  Used by the parity tests to cross-check the device paths on the same inputs. */
+int rh_set_solver(rh_ctx* ctx, int which);
 
 /* Maximum cases per group of rh_cases.group_start (the compiled lock-step width). */
 int rh_group_cases(void);
 
-/* Waves per 64 (w1, w2) pairs in the QTF pair kernel (process-wide; not part of the
+/* Waves per 64 (w1, w2) pairs in the QTF pair kernel on this context (not part of the
  * reference API): 1, 2, 4, or 0 (default: auto, currently 4 waves, the fastest measured
  * both on one GPU and for a row-sharded grid).
  * The per-pair terms are split over the waves and summed in a fixed order, so the result
  * differs between settings only by rounding.
  * Used by the tests and the kernel-tuning scripts. */
-int rh_set_qtf_waves(int waves);
+int rh_set_qtf_waves(rh_ctx* ctx, int waves);
 
 /* Unit-amplitude wave kinematics and strip-theory inertial excitation per heading.
  * Replaces the node loops of FOWT.calcHydroExcitation (raft/raft_fowt.py:1098-1124)
@@ -239,6 +244,16 @@ int rh_sea_state(rh_ctx* ctx, int ncase, int nw, const double* w, double dw, con
  * Xi [ncase][nrow][6][nw] -> psd [ncase][6][nw], std [ncase][6]. */
 int rh_motion_stats(rh_ctx* ctx, int ncase, int nrow, int nw, double dw, const rh_c128* Xi,
                     double* psd, double* std, rh_stream stream);
+
+/* Derived response channels (FOWT.saveTurbineOutputs, raft/raft_fowt.py:1900-1971 with zero
+ * aero loads -- nacelle acceleration AxRNA, tower-base bending moment Mbase -- and mooring
+ * tensions J_moor Xi, :1884-1898).  Channel k is a real linear combination of the DOFs with
+ * an optional w^2 term: x_k(row, b) = sum_d a[k][d] Xi[row][d][b] + w_b^2 sum_d c[k][d] Xi[row][d][b].
+ * Xi [ncase][nrow][ndof][nw], w [nw], coef [nch][2][ndof] = {a, c} -> psd [ncase][nch][nw]
+ * = sum_row 0.5|x_k|^2/dw (getPSD), std [ncase][nch] = sqrt(0.5 sum|x_k|^2) (getRMS); either
+ * output may be NULL. */
+int rh_channel_stats(rh_ctx* ctx, int ncase, int nrow, int ndof, int nw, double dw, const double* w,
+                     const rh_c128* Xi, int nch, const double* coef, double* psd, double* std, rh_stream stream);
 
 /* Coupled array solve (raft/raft_model.py:1021-1065) for nf FOWTs, 6nf <= 12:
  * Z_sys = blockdiag(Z_i) + K ; Xi = Z_sys^-1 F.  Z: [nf][nw][36] per-FOWT impedances,
@@ -315,8 +330,9 @@ int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w,
 /* The upper-triangle rows (w1 <= w2) of one rank of a QTF sharded over nrank devices, no
    Hermitian fill.  Rows are dealt in snake order: round k gives rank r the row
    k nrank + (k even ? r : nrank-1-r), which balances the triangle's pairs.  Entries of other
-   rows are not written (the caller zeroes qtf, sums the shards -- an all-reduce over
-   xGMI -- and then calls rh_qtf_hermitian_fill). */
+   rows are not written.  The caller exchanges the shards (raft/parallel.py assemble_qtf: one
+   all_gather over xGMI of every rank's packed upper-triangle pairs, scattered into place by
+   index) and then calls rh_qtf_hermitian_fill. */
 int rh_qtf_slender_rows(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
                         const double* M66, int rank, int nrank, rh_c128* qtf, void* work, long long work_bytes,
                         rh_stream stream);

@@ -141,6 +141,18 @@ def translate_matrix_3to6(Min, r):
     return out
 
 
+def translate_matrix_6to6(Min, r):
+    """6x6 matrix about a translated reference point (raft/helpers.py:481-503)."""
+    H = get_h(r)
+    Mout = np.zeros([6, 6])
+    Mout[:3, :3] = Min[:3, :3]
+    Mout[:3, 3:] = np.matmul(Min[:3, :3], H) + Min[:3, 3:]
+    Mout[3:, :3] = Mout[:3, 3:].T
+    Mout[3:, 3:] = (np.matmul(np.matmul(H, Min[:3, :3]), H.T) + np.matmul(Min[3:, :3], H) + np.matmul(H.T, Min[:3, 3:])
+                    + Min[3:, 3:])
+    return Mout
+
+
 def translate_force_3to6(F, r):
     """[F; r x F] with a trailing bin axis allowed (raft/helpers.py:386-401)."""
     F = np.asarray(F)
@@ -462,6 +474,41 @@ def motion_outputs(Xi, dw):
         x = Xi[:, i, :] * RAD2DEG if i >= 3 else Xi[:, i, :]
         out[dof + "_std"] = get_rms(x)
         out[dof + "_PSD"] = get_psd(x, dw)
+    return out
+
+
+def rotor_outputs(Xi, w, dw, rot, Xi0_pitch=0.0, g=9.81):
+    """Nacelle-acceleration and tower-base-moment channels of saveTurbineOutputs with zero
+    aero loads (raft/raft_fowt.py:1900-1970), in the reference's arithmetic order.
+    rot: dict of per-rotor arrays r_rel_z (RNA reference height), mRNA, IrRNA, mtower,
+    zCG_tow (tower CG height), zBase (tower member rA z), Mtow [nrot, 6, 6] (tower M_struc)."""
+    nr = len(rot["mRNA"])
+    nw = len(w)
+    out = {k: np.zeros(nr) for k in ["AxRNA_std", "AxRNA_avg", "AxRNA_max", "AxRNA_min",
+                                      "Mbase_avg", "Mbase_std", "Mbase_max", "Mbase_min"]}
+    out["AxRNA_PSD"] = np.zeros([nw, nr])
+    out["Mbase_PSD"] = np.zeros([nw, nr])
+    for ir in range(nr):
+        XiHub = Xi[:, 0, :] + rot["r_rel_z"][ir] * Xi[:, 4, :]                         # :1909
+        out["AxRNA_std"][ir] = get_rms(XiHub * w ** 2)                                 # :1912
+        out["AxRNA_PSD"][:, ir] = get_psd(XiHub * w ** 2, dw)
+        out["AxRNA_avg"][ir] = abs(np.sin(Xi0_pitch) * 9.81)
+        out["AxRNA_max"][ir] = out["AxRNA_avg"][ir] + 3 * out["AxRNA_std"][ir]
+        out["AxRNA_min"][ir] = out["AxRNA_avg"][ir] - 3 * out["AxRNA_std"][ir]
+        m_t = rot["mtower"][ir] + rot["mRNA"][ir]                                       # :1941
+        zCG = (rot["zCG_tow"][ir] * rot["mtower"][ir] + rot["r_rel_z"][ir] * rot["mRNA"][ir]) / m_t
+        hArm = zCG - rot["zBase"][ir]
+        aCG = -w ** 2 * (Xi[:, 0, :] + zCG * Xi[:, 4, :])                               # :1947
+        Mtr = translate_matrix_6to6(np.asarray(rot["Mtow"][ir], dtype=float), [0, 0, -zCG])
+        ICG = Mtr[4, 4] + rot["mRNA"][ir] * (rot["r_rel_z"][ir] - zCG) ** 2 + rot["IrRNA"][ir]
+        M_I = -m_t * aCG * hArm - ICG * (-w ** 2 * Xi[:, 4, :])                        # :1953
+        M_w = m_t * g * hArm * Xi[:, 4]                                                 # :1954
+        dyn = M_I + M_w                                                                  # :1960, aero terms 0
+        out["Mbase_avg"][ir] = m_t * g * hArm * np.sin(Xi0_pitch)                       # :1965, f_aero0 = 0
+        out["Mbase_std"][ir] = get_rms(dyn)
+        out["Mbase_PSD"][:, ir] = get_psd(dyn, dw)
+        out["Mbase_max"][ir] = out["Mbase_avg"][ir] + 3 * out["Mbase_std"][ir]
+        out["Mbase_min"][ir] = out["Mbase_avg"][ir] - 3 * out["Mbase_std"][ir]
     return out
 
 

@@ -21,14 +21,16 @@ struct rh_ctx {
   rh::DevDesign* h_designs = nullptr;   // pinned staging
   int cap = 0;
   hipEvent_t staged = nullptr;          // last copy out of h_designs
+  hipEvent_t used = nullptr;            // after the last kernel that reads d_designs
+  // tuning / cross-check knobs (per context: the ABI has no mutable process globals)
+  bool force_general = false;   // rh_set_solver(ctx, 1): always use k_solve_cases (parity cross-checks)
+  bool no_group = false;        // rh_set_solver(ctx, 2): ignore group_start (one case per workgroup)
+  int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
 };
 
 namespace {
 thread_local std::string g_err;
-bool g_force_v2 = false;   // rh_set_solver(1): always use k_solve_cases (parity cross-checks)
-bool g_no_group = false;   // rh_set_solver(2): ignore group_start (one case per workgroup)
 constexpr int kGroupCases = 2;   // lock-step width of k_solve_grp
-int g_qtf_waves = 0;       // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -48,6 +50,7 @@ int fail(int code, const char* fmt, ...) {
 
 constexpr int kThreads = 256;
 constexpr int kMaxNodes = 1024;
+constexpr size_t kMaxLds = 160 * 1024;   // LDS per workgroup on gfx950
 
 int check_design(const rh_design& d, bool need_tables) {
   if (d.nw < 2 || d.nw > 2048) return fail(RH_EINVAL, "nw=%d outside [2, 2048]", d.nw);
@@ -64,6 +67,7 @@ int check_design(const rh_design& d, bool need_tables) {
 int stage_designs(rh_ctx* ctx, const rh_design* designs, int n, hipStream_t s) {
   if (n > ctx->cap) {
     if (ctx->staged) RH_HIP(hipEventSynchronize(ctx->staged));
+    RH_HIP(hipEventSynchronize(ctx->used));   // no kernel reads the old descriptor array any more
     if (ctx->d_designs) RH_HIP(hipFree(ctx->d_designs));
     if (ctx->h_designs) RH_HIP(hipHostFree(ctx->h_designs));
     int cap = n < 64 ? 64 : n;
@@ -72,9 +76,19 @@ int stage_designs(rh_ctx* ctx, const rh_design* designs, int n, hipStream_t s) {
     ctx->cap = cap;
   }
   if (ctx->staged) RH_HIP(hipEventSynchronize(ctx->staged));  // previous copy has left the staging buffer
+  // d_designs may still be read by a kernel of an earlier call on another stream: order the
+  // overwrite after it (a no-op on the same stream)
+  RH_HIP(hipStreamWaitEvent(s, ctx->used, 0));
   for (int i = 0; i < n; ++i) ctx->h_designs[i].d = designs[i];
   RH_HIP(hipMemcpyAsync(ctx->d_designs, ctx->h_designs, sizeof(rh::DevDesign) * n, hipMemcpyHostToDevice, s));
   RH_HIP(hipEventRecord(ctx->staged, s));
+  return RH_OK;
+}
+
+// after every launch that reads ctx->d_designs
+int designs_used(rh_ctx* ctx, hipStream_t s) {
+  RH_HIP(hipGetLastError());
+  RH_HIP(hipEventRecord(ctx->used, s));
   return RH_OK;
 }
 
@@ -103,20 +117,22 @@ extern "C" int rh_prof_read(unsigned long long* out, int reset) {
 }
 #endif
 
-int rh_set_solver(int which) {
+int rh_set_solver(rh_ctx* ctx, int which) {
+  if (!ctx) return fail(RH_EINVAL, "rh_set_solver: null context");
   if (which < 0 || which > 2)
     return fail(RH_EINVAL, "rh_set_solver: which=%d (0 = auto, 1 = general kernel, 2 = ungrouped)", which);
-  g_force_v2 = which == 1;
-  g_no_group = which == 2;
+  ctx->force_general = which == 1;
+  ctx->no_group = which == 2;
   return RH_OK;
 }
 
 int rh_group_cases(void) { return kGroupCases; }
 
-int rh_set_qtf_waves(int waves) {
+int rh_set_qtf_waves(rh_ctx* ctx, int waves) {
+  if (!ctx) return fail(RH_EINVAL, "rh_set_qtf_waves: null context");
   if (waves != 0 && waves != 1 && waves != 2 && waves != 4)
     return fail(RH_EINVAL, "rh_set_qtf_waves: waves=%d (0 = auto, 1, 2 or 4)", waves);
-  g_qtf_waves = waves;
+  ctx->qtf_waves = waves;
   return RH_OK;
 }
 
@@ -129,7 +145,9 @@ int rh_ctx_create(int device, rh_ctx** out) {
   rh_ctx* c = new rh_ctx;
   c->device = device;
   hipError_t e = hipEventCreateWithFlags(&c->staged, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->used, hipEventDisableTiming);
   if (e != hipSuccess) {
+    if (c->staged) (void)hipEventDestroy(c->staged);
     delete c;
     return fail(RH_EHIP, "hipEventCreate: %s", hipGetErrorString(e));
   }
@@ -142,6 +160,10 @@ int rh_ctx_destroy(rh_ctx* ctx) {
   if (ctx->staged) {
     (void)hipEventSynchronize(ctx->staged);
     (void)hipEventDestroy(ctx->staged);
+  }
+  if (ctx->used) {
+    (void)hipEventSynchronize(ctx->used);
+    (void)hipEventDestroy(ctx->used);
   }
   if (ctx->d_designs) (void)hipFree(ctx->d_designs);
   if (ctx->h_designs) (void)hipHostFree(ctx->h_designs);
@@ -193,7 +215,8 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   a.c = *cases;
   a.o = *out;
   // Grouped path (rh_solve_grp.hip): kGroupCases cases of one (design, heading) per workgroup.
-  if (cases->group_start && cases->ngroup > 0 && !g_force_v2 && !g_no_group) {
+  // (It does not report the convergence margin: with out->margin the ungrouped kernels run.)
+  if (cases->group_start && cases->ngroup > 0 && !ctx->force_general && !ctx->no_group && !out->margin) {
     if (cases->ngroup > cases->ncase) return fail(RH_EINVAL, "rh_solve_cases: ngroup=%d > ncase", cases->ngroup);
     int nmmax = 0;
     for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
@@ -202,12 +225,11 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
     if (lsm <= 160 * 1024) {
       hipLaunchKernelGGL(rh::k_solve_grp<kGroupCases>, dim3(cases->ngroup), dim3(rh::kGT), lsm, s, a,
                          cases->group_start, cases->ngroup);
-      RH_HIP(hipGetLastError());
-      return RH_OK;
+      return designs_used(ctx, s);
     }
   }
   // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case, nw <= 1024.
-  if (nw <= 2 * rh::kLT && !g_force_v2) {
+  if (nw <= 2 * rh::kLT && !ctx->force_general) {
     const int nb = nw <= rh::kLT ? 1 : 2;
     int nmmax = 0;
     for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
@@ -216,11 +238,14 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
       dim3 grid(cases->ncase), block(rh::kLT);
       if (nb == 1) hipLaunchKernelGGL(rh::k_solve_lds<1>, grid, block, lsm, s, a);
       else hipLaunchKernelGGL(rh::k_solve_lds<2>, grid, block, lsm, s, a);
-      RH_HIP(hipGetLastError());
-      return RH_OK;
+      return designs_used(ctx, s);
     }
   }
-  const size_t smem = sizeof(double) * (size_t)((kThreads / 64) * nnmax * 3 + nnmax * 9 + 36 + (kThreads / 64) * 6 + 108 + nnmax * 5);
+  const size_t smem = sizeof(double) * (size_t)((kThreads / 64) * nnmax * 3 + nnmax * 9 + 36 + (kThreads / 64) * 6 + 108 +
+                                                nnmax * 5 + kThreads / 64);
+  if (smem > kMaxLds)
+    return fail(RH_EINVAL, "rh_solve_cases: %d submerged nodes need %zu B of LDS (> %zu B on gfx950)", nnmax, smem,
+                kMaxLds);
   dim3 grid(cases->ncase), block(kThreads);
   switch (nb_for(nw)) {
     case 1: hipLaunchKernelGGL(rh::k_solve_cases<1>, grid, block, smem, s, a); break;
@@ -228,8 +253,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
     case 4: hipLaunchKernelGGL(rh::k_solve_cases<4>, grid, block, smem, s, a); break;
     default: hipLaunchKernelGGL(rh::k_solve_cases<8>, grid, block, smem, s, a); break;
   }
-  RH_HIP(hipGetLastError());
-  return RH_OK;
+  return designs_used(ctx, s);
 }
 
 int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int ncase, const int* design_idx,
@@ -252,8 +276,7 @@ int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int 
   const size_t smem = sizeof(double) * (size_t)(nnmax * 9 + 36 + 108);
   dim3 grid((nw + kThreads - 1) / kThreads, ncase);
   hipLaunchKernelGGL(rh::k_heading_resp, grid, dim3(kThreads), smem, s, a);
-  RH_HIP(hipGetLastError());
-  return RH_OK;
+  return designs_used(ctx, s);
 }
 
 int rh_linearize(rh_ctx* ctx, const rh_design* d, int head, const rh_c128* Xi, const double* zeta, double* B_drag,
@@ -342,6 +365,20 @@ int rh_motion_stats(rh_ctx* ctx, int ncase, int nrow, int nw, double dw, const r
   return RH_OK;
 }
 
+int rh_channel_stats(rh_ctx* ctx, int ncase, int nrow, int ndof, int nw, double dw, const double* w,
+                     const rh_c128* Xi, int nch, const double* coef, double* psd, double* std_, rh_stream stream) {
+  if (!ctx || !w || !Xi || !coef) return fail(RH_EINVAL, "rh_channel_stats: null argument");
+  if (ncase < 0 || nrow <= 0 || ndof <= 0 || nw <= 0 || nch < 0 || !(dw > 0))
+    return fail(RH_EINVAL, "rh_channel_stats: bad sizes ncase=%d nrow=%d ndof=%d nw=%d nch=%d", ncase, nrow, ndof, nw,
+                nch);
+  if (ncase == 0 || nch == 0) return RH_OK;
+  RH_HIP(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(rh::k_channel_stats, dim3(nch, ncase), dim3(kThreads), 0, (hipStream_t)stream, nrow, ndof, nw, dw,
+                     w, Xi, nch, coef, psd, std_);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
 int rh_system_solve(rh_ctx* ctx, int nf, int nw, const rh_c128* Z, const double* K, const rh_c128* F, rh_c128* Xi,
                     rh_stream stream) {
   if (!ctx || !Z || !F || !Xi) return fail(RH_EINVAL, "rh_system_solve: null argument");
@@ -394,7 +431,7 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
     // diagonal, 4 waves per tile are the fastest on one GPU too (C3: 0.294 ms against 0.33 ms
     // with 1 or 2 waves, profiles/r01_v11/qtf_diag_tiles_ab.txt), and a sharded grid needs
     // them to keep the CUs busy.
-    const int waves = g_qtf_waves == 0 ? 4 : g_qtf_waves;
+    const int waves = ctx->qtf_waves == 0 ? 4 : ctx->qtf_waves;
     switch (waves) {
       case 1:
         hipLaunchKernelGGL(rh::k_qtf_pairs<1>, grid, dim3(rh::kQtfTile), 0, s, *q, wk, qtf, rank, nrank, mirror);

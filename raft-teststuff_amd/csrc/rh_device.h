@@ -141,6 +141,18 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// full 64-lane butterfly max (every lane ends with the maximum; NaN inputs are ignored)
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Closest call of the all-bins convergence test (raft/raft_model.py:961-962): of the
+// per-iteration values m = max_bins,dof tolCheck - tol, keep the one with the smallest |m|.
+// A case whose closest call is within rounding of 0 could flip its iteration count.
+__device__ __forceinline__ double closer_call(double best, double m) { return fabs(m) < fabs(best) ? m : best; }
+
 // blockIdx -> work item such that blocks dispatched to the same XCD (b % 8 under the
 // observed round-robin placement) get a CONTIGUOUS range of items; bijective for any G.
 // Placement only affects speed (L2 locality of the per-design/heading tables), never results.

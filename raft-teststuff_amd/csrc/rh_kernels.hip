@@ -353,6 +353,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
   double* sred = bd + 36;                 // [kWaves][6]
   double* mbc = sred + kWaves * 6;        // [108] M, B_lin, C
   double* al = mbc + 108;                 // [nn][5] drag coefficients per node
+  double* mred = al + nn * 5;             // [kWaves] per-wave max of tolCheck
   load_mbc(d, mbc, tid);
 
   const int spec = a.c.spectrum[ic];
@@ -379,6 +380,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
   const int nloop = a.c.nIter + 1;
   const double tol = a.c.tol;
   int status = RH_CASE_NOT_CONVERGED, iters = nloop;
+  double margin = INFINITY;   // closest call of the convergence test (rh_solve_out.margin)
   for (int it = a.c.first_iter; it < nloop; ++it) {
     // ---------------- A: per-node sums of squared relative-velocity components ----------
     // Member-factored (see rh_member_field): per (member, bin) the motion terms
@@ -481,6 +483,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
     __syncthreads();
     // ---------------- C: excitation, Z(w), LU solve, convergence flags ------------------
     bool my_ok = true, my_nan = false, my_sing = false;
+    double my_tmax = 0.0;
 #pragma unroll 1
     for (int j = 0; j < NB; ++j) {
       const int b = tid + kThreads * j;
@@ -510,13 +513,23 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
         // tolCheck = |Xi - XiLast| / (|Xi| + tol) < tol  (raft/raft_model.py:961-962)
         const double t = cabs(sub(x, xlast)) / (cabs(x) + tol);
         my_ok = my_ok && (t < tol);
+        my_tmax = fmax(my_tmax, t);
         st(Xo + c * nw + b, x);
         if (XP) st(XP + c * nw + b, xlast);
         // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged
         st(XL + c * nw + b, add(scl(xlast, 0.2), scl(x, 0.8)));
       }
     }
+    if (a.o.margin) {
+      const double mw = wave_max(my_tmax);
+      if (lane == 0) mred[wv] = mw;
+    }
     const int all_ok = __syncthreads_and(my_ok ? 1 : 0);
+    if (a.o.margin && tid == 0) {   // mred is rewritten only after the next phase-A barrier
+      double mx = mred[0];
+      for (int w = 1; w < kWaves; ++w) mx = fmax(mx, mred[w]);
+      margin = closer_call(margin, mx - tol);
+    }
     const int any_nan = __syncthreads_or(my_nan ? 1 : 0);
     const int any_sing = __syncthreads_or(my_sing ? 1 : 0);
     if (any_nan) {
@@ -540,6 +553,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
   if (tid == 0) {
     a.o.iters[ic] = iters;
     a.o.status[ic] = status;
+    if (a.o.margin) a.o.margin[ic] = margin;
   }
   if (a.o.B_drag && tid < 36) a.o.B_drag[(size_t)ic * 36 + tid] = bd[tid];
   if (a.o.Bmat)
@@ -831,6 +845,50 @@ __global__ __launch_bounds__(kThreads) void k_motion_stats(int nrow, int nw, dou
     double s = 0;
     for (int w = 0; w < kWaves; ++w) s += sred[w][tid];
     stdv[(size_t)ic * 6 + tid] = sqrt(0.5 * s);
+  }
+}
+
+// Derived response channels (raft/raft_fowt.py:1900-1971 with zero aero loads: nacelle
+// acceleration AxRNA and tower-base bending Mbase; mooring tensions J_moor Xi, :1884-1898):
+// real linear combinations of the DOFs with an optional w^2 term,
+//   x_k(row, b) = sum_d a[k][d] Xi[row][d][b] + w_b^2 sum_d c[k][d] Xi[row][d][b]
+// psd[k][b] = sum_row 0.5 |x_k|^2 / dw (getPSD), std[k] = sqrt(0.5 sum_{row,b} |x_k|^2)
+// (getRMS, raft/helpers.py:581-603).  coef: [nch][2][ndof] = {a, c}.  Block per (channel, case).
+__global__ __launch_bounds__(kThreads) void k_channel_stats(int nrow, int ndof, int nw, double dw,
+                                                             const double* __restrict__ w, const rh_c128* __restrict__ Xi,
+                                                             int nch, const double* __restrict__ coef,
+                                                             double* __restrict__ psd, double* __restrict__ stdv) {
+  __shared__ double sred[kWaves];
+  const int k = blockIdx.x, ic = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const double* A = coef + (size_t)k * 2 * ndof;
+  const double* C = A + ndof;
+  double ss = 0;
+  for (int b = tid; b < nw; b += kThreads) {
+    const double w2 = w[b] * w[b];
+    double p = 0;
+    for (int r = 0; r < nrow; ++r) {
+      const rh_c128* X = Xi + ((size_t)ic * nrow + r) * ndof * nw + b;
+      cd xa = mk(0, 0), xc = mk(0, 0);
+      for (int dof = 0; dof < ndof; ++dof) {
+        const double a = A[dof], c = C[dof];
+        if (a == 0.0 && c == 0.0) continue;          // uniform: the coefficient rows are shared
+        const cd x = ld(X + (size_t)dof * nw);
+        xa = add(xa, scl(x, a));
+        xc = add(xc, scl(x, c));
+      }
+      const double m2 = abs2(add(xa, scl(xc, w2)));
+      p += 0.5 * m2 / dw;
+      ss += m2;
+    }
+    if (psd) psd[((size_t)ic * nch + k) * nw + b] = p;
+  }
+  const double s = wave_sum(ss);
+  if (lane == 0) sred[wv] = s;
+  __syncthreads();
+  if (tid == 0 && stdv) {
+    double t = 0;
+    for (int i = 0; i < kWaves; ++i) t += sred[i];
+    stdv[(size_t)ic * nch + k] = sqrt(0.5 * t);
   }
 }
 

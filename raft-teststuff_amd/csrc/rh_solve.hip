@@ -165,7 +165,8 @@ __host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB) {
                            + (size_t)nn               // node axial coordinate t
                            + (size_t)nm * 18          // member cq, c1, c2
                            + (size_t)2 * kLT * NB     // w and zeta per (padded) bin
-                           + 36 + 108 + kLW * 6 + 36) // B_drag, M|B|C image, std partials, B_lin+B_drag
+                           + 36 + 108 + kLW * 6 + 36  // B_drag, M|B|C image, std partials, B_lin+B_drag
+                           + kLW)                     // convergence-margin partials
          + sizeof(int) * ((size_t)nm + 2);            // member node ranges
 }
 
@@ -202,7 +203,8 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
   double* mbf = nt + nn;                           // [18][nm]
   double* lw = mbf + 18 * nm;                      // [NWP] w per bin (pad bins: w[nw-1])
   double* lz = lw + NWP;                           // [NWP] zeta per bin (pad bins: 0)
-  int* mstart = reinterpret_cast<int*>(lz + NWP);  // [nm+1]
+  double* mred = lz + NWP;                         // [kLW] per-wave max of tolCheck
+  int* mstart = reinterpret_cast<int*>(mred + kLW);  // [nm+1]
   load_mbc(d, mbc, tid);
   for (int n = tid; n < nn; n += kLT) nt[n] = node[RH_NF_T * nn + n];
   for (int e = tid; e < 18 * nm; e += kLT) mbf[e] = d.memb[e];   // RH_MF_CQ0..C20 are fields 0..17
@@ -237,6 +239,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
   const int nloop = a.c.nIter + 1;
   const double tol = a.c.tol;
   int status = RH_CASE_NOT_CONVERGED, iters = nloop;
+  double margin = INFINITY;   // closest call of the convergence test (rh_solve_out.margin)
   __syncthreads();
   PROF_T(tp1);
   PROF_ADD(0, tp1 - tp0);
@@ -384,6 +387,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
 #endif
     // ---------------- C: excitation, Z(w), LU solve, convergence flags ------------------
     bool my_ok = true, my_nan = false, my_sing = false;
+    double my_tmax = 0.0;
 #pragma unroll 1
     for (int j = 0; j < NB; ++j) {
       // per-bin scalars picked without dynamic register indexing (the loop is not unrolled,
@@ -503,6 +507,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
         // (magnitudes as sqrt(re^2 + im^2): within an ulp of np.abs's hypot, far cheaper)
         const double tt = sqrt(abs2(sub(x, xlast))) / (sqrt(abs2(x)) + tol);
         my_ok = my_ok && (tt < tol);
+        my_tmax = fmax(my_tmax, tt);
         st_nt(Xo + c * nw + b, x);   // streamed: only the last iteration's value is kept
         if (XP) st(XP + c * nw + b, xlast);
         // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged
@@ -515,7 +520,16 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
     PROF_ADD(3, tc_exc);
     PROF_ADD(4, tc_sol);
     PROF_T(ta3);
+    if (a.o.margin) {
+      const double mw = wave_max(my_tmax);
+      if (lane == 0) mred[wv] = mw;
+    }
     const int all_ok = __syncthreads_and(my_ok ? 1 : 0);
+    if (a.o.margin && tid == 0) {   // mred is rewritten only after the next phase-A barrier
+      double mx = mred[0];
+      for (int w = 1; w < kLW; ++w) mx = fmax(mx, mred[w]);
+      margin = closer_call(margin, mx - tol);
+    }
     const int any_nan = __syncthreads_or(my_nan ? 1 : 0);
     const int any_sing = __syncthreads_or(my_sing ? 1 : 0);
     PROF_T(ta4);
@@ -542,6 +556,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
   if (tid == 0) {
     a.o.iters[ic] = iters;
     a.o.status[ic] = status;
+    if (a.o.margin) a.o.margin[ic] = margin;
   }
   if (a.o.B_drag && tid < 36) a.o.B_drag[(size_t)ic * 36 + tid] = bd[tid];
   if (a.o.Bmat)

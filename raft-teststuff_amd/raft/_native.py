@@ -47,7 +47,7 @@ class RhCases(ctypes.Structure):
 
 class RhSolveOut(ctypes.Structure):
     _fields_ = [("Xi", _p), ("Xi_last", _p), ("iters", _p), ("status", _p), ("zeta", _p), ("B_drag", _p),
-                ("Bmat", _p), ("psd", _p), ("std", _p), ("rao", _p), ("Z", _p), ("Xi_prev", _p)]
+                ("Bmat", _p), ("psd", _p), ("std", _p), ("rao", _p), ("Z", _p), ("Xi_prev", _p), ("margin", _p)]
 
 
 class RhQtfDesign(ctypes.Structure):
@@ -97,13 +97,15 @@ def lib():
                 "rh_sea_state": [_p, ctypes.c_int, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p, _p, _p, _p],
                 "rh_motion_stats": [_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, _p, _p, _p, _p],
                 "rh_system_solve": [_p, ctypes.c_int, ctypes.c_int, _p, _p, _p, _p, _p],
+                "rh_channel_stats": [_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, _p,
+                                     _p, ctypes.c_int, _p, _p, _p, _p],
                 "rh_qtf_slender": [_p, ctypes.POINTER(RhQtfDesign), ctypes.c_int, _p, _p, _p, _p, _p,
                                    ctypes.c_longlong, _p],
                 "rh_qtf_slender_rows": [_p, ctypes.POINTER(RhQtfDesign), ctypes.c_int, _p, _p, _p, ctypes.c_int,
                                         ctypes.c_int, _p, _p, ctypes.c_longlong, _p],
                 "rh_qtf_hermitian_fill": [_p, ctypes.c_int, _p, _p],
-                "rh_set_solver": [ctypes.c_int],
-                "rh_set_qtf_waves": [ctypes.c_int],
+                "rh_set_solver": [_p, ctypes.c_int],
+                "rh_set_qtf_waves": [_p, ctypes.c_int],
                 "rh_force_2nd": [_p, ctypes.c_int, _p, _p, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p],
             }.items():
                 fn = getattr(L, name)

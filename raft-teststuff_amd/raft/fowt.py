@@ -156,12 +156,16 @@ class FOWT:
         (raft/statics.py).  Matrices given to setStatics() override the computed ones (a
         full set skips the computation), and its C_moor stands in for MoorPy's stiffness."""
         given = self._statics or {}
-        if not all(k in given for k in ("M_struc", "C_struc", "C_hydro")):
+        full = all(k in given for k in ("M_struc", "C_struc", "C_hydro"))
+        computable = not self._rotor_submerged and (self.nrotors == 0 or len(self.rnaList) == self.nrotors)
+        if not full and not computable:
             if self._rotor_submerged:
                 raise NotImplementedError("underwater rotors (blade-member buoyancy, raft/raft_fowt.py:386-443) "
                                           "are outside the accelerated path")
-            if self.nrotors > 0 and len(self.rnaList) != self.nrotors:
-                raise ValueError("turbine: mRNA, IxRNA, IrRNA, xCG_RNA, overhang and shaft_tilt are required")
+            raise ValueError("turbine: mRNA, IxRNA, IrRNA, xCG_RNA, overhang and shaft_tilt are required")
+        if computable:
+            # also when a full set is given: the tower masses and member inertias feed the
+            # tower-base channels of saveTurbineOutputs (raft/raft_fowt.py:1939-1970)
             fowt_statics(self)
         self._dd = self._host = None
         if self._statics is None:
@@ -437,10 +441,42 @@ class FOWT:
         return f_mean, f_h
 
     # ------------------------------------------------------------------ outputs
+    def rotor_channels(self):
+        """Coefficient rows of the derived rotor channels for rh_channel_stats and their mean
+        values (raft/raft_fowt.py:1900-1970 with zero aero loads: A_aero = B_aero = f_aero0 = 0,
+        the only state the accelerated path runs).  Per rotor ir:
+          AxRNA_ir = w^2 (Xi_surge + zHub Xi_pitch)                              (:1909-1913)
+          Mbase_ir = m hArm w^2 Xi_surge + (w^2 (m hArm zCG + I_CG) + m g hArm) Xi_pitch
+        (M_I + M_w of :1947-1960 expanded).  Returns (coef [2 nrot, 2, 6], means [2 nrot])."""
+        nr = self.nrotors
+        coef = np.zeros([2 * nr, 2, 6])
+        means = np.zeros(2 * nr)
+        for ir, rot in enumerate(self.rnaList):
+            coef[ir, 1, 0] = 1.0
+            coef[ir, 1, 4] = rot.r_rel[2]
+            means[ir] = abs(np.sin(self.Xi0[4]) * 9.81)                              # :1914
+        for ir, rot in enumerate(self.rnaList[:len(self.mtower)]):
+            mt = self.mtower[ir] + rot.mRNA
+            zCG = (self.rCG_tow[ir][2] * self.mtower[ir] + rot.r_rel[2] * rot.mRNA) / mt
+            tower = self.memberList[self.nplatmems + ir]
+            hArm = zCG - tower.rA[2]
+            ICG = (translate_matrix_6to6(tower.M_struc, [0, 0, -zCG])[4, 4] + rot.mRNA * (rot.r_rel[2] - zCG) ** 2
+                   + rot.IrRNA)
+            k = nr + ir
+            coef[k, 0, 4] = mt * self.g * hArm
+            coef[k, 1, 0] = mt * hArm
+            coef[k, 1, 4] = mt * hArm * zCG + ICG
+            means[k] = mt * self.g * hArm * np.sin(self.Xi0[4])                      # :1965-1966, f_aero0 = 0
+        return coef, means
+
     def saveTurbineOutputs(self, results, case):
-        """Motion part of raft/raft_fowt.py:1821-1875 plus wave_PSD (:1974).  The rotor,
-        tower-base and mooring-tension channels need statics/rotor/MoorPy data that the
-        accelerated path does not build."""
+        """raft/raft_fowt.py:1821-1974: platform motions (RMS, PSD, RA), nacelle acceleration
+        AxRNA_* and tower-base moment Mbase_* per rotor (rh_channel_stats on the device) and
+        wave_PSD.  Rotor-control channels (omega/torque/power/bPitch) are the reference's zeros
+        because aero-servo is inactive in every case the accelerated path runs (wind 0 or a
+        non-operating turbine, raft/raft_fowt.py:2006).  Mooring tensions (Tmoor_*) need a
+        mooring system (MoorPy in the reference)."""
+        import torch
         self.Xi0 = self.r6 - np.array([self.x_ref, self.y_ref, 0, 0, 0, 0])
         stats = getattr(self, "_stats", None)
         if stats is None:
@@ -455,4 +491,31 @@ class FOWT:
             results[f"{dof}_min"] = avg - 3 * std
             results[f"{dof}_PSD"] = stats["psd"][i]
             results[f"{dof}_RA"] = self.Xi[:, i, :] * conv
+        nr = self.nrotors
+        coef, means = self.rotor_channels()
+        psd = np.zeros([2 * nr, self.nw])
+        std = np.zeros(2 * nr)
+        if nr > 0:
+            X = self._xi_dev
+            dev = X.device
+            ct = torch.tensor(coef, dtype=torch.float64, device=dev).contiguous()
+            wt = torch.tensor(self.w, dtype=torch.float64, device=dev)
+            pt = torch.empty([2 * nr, self.nw], dtype=torch.float64, device=dev)
+            stt = torch.empty([2 * nr], dtype=torch.float64, device=dev)
+            N.check(N.lib().rh_channel_stats(N.context(self.device_index), 1, X.shape[0], 6, self.nw, float(self.dw),
+                                             N.ptr(wt), N.ptr(X), 2 * nr, N.ptr(ct), N.ptr(pt), N.ptr(stt),
+                                             N.stream_handle(torch, dev)), "rh_channel_stats")
+            psd, std = pt.cpu().numpy(), stt.cpu().numpy()
+        for j, name in enumerate(["AxRNA", "Mbase"]):
+            sl = slice(j * nr, (j + 1) * nr)
+            results[f"{name}_std"] = std[sl].copy()
+            results[f"{name}_PSD"] = psd[sl].T.copy()                                 # [nw, nrotors]
+            results[f"{name}_avg"] = means[sl].copy()
+            results[f"{name}_max"] = means[sl] + 3 * std[sl]
+            results[f"{name}_min"] = means[sl] - 3 * std[sl]
         results["wave_PSD"] = np.sum(0.5 * np.abs(self.zeta) ** 2 / self.dw, axis=0)
+        for name in ["omega_avg", "omega_std", "omega_max", "omega_min", "torque_avg", "torque_std", "power_avg",
+                     "bPitch_avg", "bPitch_std"]:                                     # :1983-1994
+            results[name] = np.zeros(nr)
+        for name in ["omega_PSD", "torque_PSD", "bPitch_PSD"]:
+            results[name] = np.zeros([self.nw, nr])

@@ -176,6 +176,7 @@ class Model:
             N.check(N.lib().rh_motion_stats(N.context(self.device), 1, nW + 1, self.nw, float(fowt.dw), N.ptr(xi_i),
                                             N.ptr(psd), N.ptr(std), N.stream_handle(torch, dev)), "rh_motion_stats")
             fowt._stats = {"psd": psd.cpu().numpy(), "std": std.cpu().numpy()}
+            fowt._xi_dev = xi_i                        # device copy for the derived channels
             fowt.Xi = self.Xi[:, 6 * i:6 * i + 6, :]
         self.results["response"] = {}
         return self.Xi

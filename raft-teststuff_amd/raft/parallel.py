@@ -89,7 +89,7 @@ def qtf_pair_index(n2, rank, world, device=None):
     return _PAIR_INDEX[key]
 
 
-def assemble_qtf(compute_rows, hermitian_fill, n2, device=None, group=None):
+def assemble_qtf(compute_rows, hermitian_fill, n2, device=None, group=None, on_computed=None):
     """Row-sharded QTF: compute_rows(out, rank, world) writes the upper-triangle rows of
     `rank` into the zeroed [n2, n2, 6] complex128 tensor `out`.  The shards are exchanged by
     ONE all_gather of each rank's packed upper-triangle pairs (about n2^2/2 / world pairs x
@@ -101,6 +101,8 @@ def assemble_qtf(compute_rows, hermitian_fill, n2, device=None, group=None):
     rank, world = world_of(group)
     out = torch.zeros([n2, n2, 6], dtype=torch.complex128, device=device)
     compute_rows(out, rank, world)
+    if on_computed is not None:
+        on_computed()
     if world > 1:
         flat = out.view(n2 * n2, 6)
         idx = [qtf_pair_index(n2, r, world, device) for r in range(world)]
@@ -122,14 +124,14 @@ def solve_cases_sharded(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd
     (solver.CaseSet); with gather=True every rank receives all cases' outputs."""
     from .solver import CaseSet, solve_batch
     rank, world = world_of(group)
+    if gather and cases.n < world:   # decided identically on every rank, before any collective
+        raise ValueError(f"solve_cases_sharded: {cases.n} cases for {world} ranks (every rank needs one)")
     lo, hi = case_shard(cases.n, rank, world)
     sub = CaseSet(cases.design_idx[lo:hi], cases.heading[lo:hi], cases.spectrum[lo:hi], cases.Hs[lo:hi],
                   cases.Tp[lo:hi], cases.gamma[lo:hi])
     res = solve_batch(designs, sub, nIter, XiStart, tol, want=want) if sub.n else None
     if not gather:
         return res, (lo, hi)
-    if res is None:
-        raise ValueError("every rank needs at least one case")
     return gather_cases(dict(res), cases.n, group), (0, cases.n)
 
 

@@ -180,3 +180,14 @@ class DeviceDesign:
                     "rh_wave_tables")
             self._beta_keep = beta_t
         return [self.headings.index(b) for b in betas]
+
+    def retabulate(self, stream=None):
+        """Recompute the wave tables of the tabulated headings in place (same buffers, one
+        rh_wave_tables launch): the per-design table work of a batch, e.g. inside a timed
+        step.  The values are identical to the first tabulation."""
+        if self.uhat is None:
+            raise RuntimeError("retabulate: no headings tabulated yet (ensure_headings)")
+        d = self.struct()
+        s = stream if stream is not None else N.stream_handle(self.torch, self.device)
+        N.check(N.lib().rh_wave_tables(N.context(self.dev_index), ctypes.byref(d), N.ptr(self._beta_keep),
+                                       N.ptr(self.uhat), N.ptr(self.finer), N.ptr(self.kproj), s), "rh_wave_tables")

@@ -18,8 +18,8 @@ QN_COUNT, QM_COUNT, KR_COUNT = 46, 36, 6
 
 def _hank_table(kk, R):
     """[n2, 12] table D_n(k R), n = 0..11 (orders -1..12 of hankel1)."""
-    x = kk * R
-    H = np.array([hankel1(n, x) for n in range(-1, 13)])      # [14, n2]
+    x = np.asarray(kk, dtype=float) * R
+    H = hankel1(np.arange(-1, 13)[:, None], x[None, :])         # [14, n2], one ufunc call
     D = 0.5 * (H[0:12] - H[2:14])                              # D_n = 0.5 (H_{n-1} - H_{n+1})
     return D.T.copy()
 
@@ -151,26 +151,32 @@ class QtfDevice:
         q.kray, q.hank = N.ptr(self.kray), N.ptr(self.hank)
         return q
 
-    def qtf(self, w, Xi0, M66, out=None, group=None):
+    def qtf(self, w, Xi0, M66, out=None, group=None, on_computed=None):
         """Run rh_qtf_slender: w [nw] / Xi0 [6, nw] device tensors -> qtf [n2, n2, 6] device tensor.
-        With an initialised process group of world > 1 the pairs are row-sharded over the
-        ranks (raft/parallel.py) and every rank returns the full matrix."""
+        Sharding is opt-in: only with an explicit process `group` of world > 1 are the pairs
+        row-sharded over its ranks (raft/parallel.py) -- a collective every rank of the group
+        must enter with the same inputs -- and every rank returns the full matrix.  group=None
+        (what FOWT.calcQTF_slenderBody passes) never communicates, so ranks that each solve
+        their own cases or designs can call it independently.  on_computed: optional callback
+        run after this rank's pair kernels are enqueued, before any exchange (bench timing)."""
         torch = self.torch
         from .parallel import assemble_qtf, world_of
-        if world_of(group)[1] > 1:
+        if group is not None and world_of(group)[1] > 1:
             return assemble_qtf(lambda o, r, n: self.qtf_rows(w, Xi0, M66, o, r, n), self.hermitian_fill, self.n2,
-                                device=self.dev, group=group)
+                                device=self.dev, group=group, on_computed=on_computed)
         if out is None:
             out = torch.empty([self.n2, self.n2, 6], dtype=torch.complex128, device=self.dev)
         N.check(N.lib().rh_qtf_slender(N.context(self.dev_index), ctypes.byref(self.struct_), int(w.numel()), N.ptr(w),
                                        N.ptr(Xi0), N.ptr(M66), N.ptr(out), N.ptr(self.work),
                                        ctypes.c_longlong(self.work_bytes), N.stream_handle(torch, self.dev)),
                 "rh_qtf_slender")
+        if on_computed is not None:
+            on_computed()
         return out
 
 
     def qtf_rows(self, w, Xi0, M66, out, rank, nrank):
-        """rh_qtf_slender_rows: upper-triangle rows i1 = rank (mod nrank) into `out`."""
+        """rh_qtf_slender_rows: the upper-triangle rows of `rank` (snake deal, parallel.qtf_rows) into `out`."""
         N.check(N.lib().rh_qtf_slender_rows(N.context(self.dev_index), ctypes.byref(self.struct_), int(w.numel()),
                                             N.ptr(w), N.ptr(Xi0), N.ptr(M66), int(rank), int(nrank), N.ptr(out),
                                             N.ptr(self.work), ctypes.c_longlong(self.work_bytes),

@@ -49,7 +49,8 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
                 fext=None, stream=None, prepared=None, Xi_init=None, first_iter=0):
     """Run rh_solve_cases.  `designs`: list of DeviceDesign (same nw); `cases`: CaseSet.
     Returns a BatchResult of device tensors (stream-ordered; caller synchronises).
-    want may include "Xi_prev" (the un-relaxed XiLast of the final iteration); Xi_init /
+    want may include "Xi_prev" (the un-relaxed XiLast of the final iteration) and "margin"
+    (the closest call of the convergence test per case, rh_solve_out.margin); Xi_init /
     first_iter restart a fixed point from such a state (potSecOrder=1 second pass)."""
     d0 = designs[0]
     torch = d0.torch
@@ -84,6 +85,8 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
         out["Z"] = torch.empty([ncase, nw, 6, 6], **c128)
     if "Xi_prev" in want:
         out["Xi_prev"] = torch.empty([ncase, 6, nw], **c128)
+    if "margin" in want:
+        out["margin"] = torch.empty([ncase], **f64)
     for t, shape in ((fext, [ncase, 6, nw]), (Xi_init, [ncase, 6, nw])):
         if t is not None and (list(t.shape) != shape or t.dtype != torch.complex128 or not t.is_contiguous()):
             raise ValueError(f"expected a contiguous complex128 tensor of shape {shape}")
@@ -98,7 +101,7 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     cs.group_start, cs.ngroup = N.ptr(prep["group_start"]), int(prep["ngroup"])
     o = N.RhSolveOut()
     o.Xi, o.Xi_last, o.iters, o.status = N.ptr(out["Xi"]), N.ptr(xl), N.ptr(out["iters"]), N.ptr(out["status"])
-    for k in ["zeta", "B_drag", "Bmat", "psd", "std", "rao", "Z", "Xi_prev"]:
+    for k in ["zeta", "B_drag", "Bmat", "psd", "std", "rao", "Z", "Xi_prev", "margin"]:
         setattr(o, k, N.ptr(out.get(k)))
     arr = (N.RhDesign * len(designs))(*[d.struct() for d in designs])
     s = stream if stream is not None else N.stream_handle(torch, dev)

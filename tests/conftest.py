@@ -75,3 +75,40 @@ def fixture_design(tag, base_name, fi=0):
         d = sweep_variant(d, G["sweep_mult"])
     T = farm_tables(G)[fi] if "f0_w" in G else G
     return d, T, G
+
+
+def oracle_tables_of(fowt):
+    """The oracle's design-table dict (the keys make_golden.design_tables writes) of a FOWT
+    prepared by the product's host side (members, statics, added mass) -- lets the oracle
+    check the device solve of designs no reference run covers (e.g. C5 sweep variants);
+    the host preparation itself is pinned separately (tests/test_prep.py, test_statics.py)."""
+    rows = []
+    for mem in fowt.memberList:
+        circ = mem.shape == "circular"
+        for il in range(mem.ns):
+            rows.append(dict(member=0, node=il, circ=int(circ), sub=int(mem.r[il, 2] < 0), mcf=int(bool(mem.MCF)),
+                             r=mem.r[il].copy(), r_rel=mem.r[il] - fowt.r6[:3], q=mem.q, p1=mem.p1, p2=mem.p2,
+                             ds=np.resize(np.atleast_1d(mem.ds[il]).astype(float), 2),
+                             drs=np.resize(np.atleast_1d(mem.drs[il]).astype(float), 2), dls=float(mem.dls[il]),
+                             Cd_q=mem.coef("Cd_q", il), Cd_p1=mem.coef("Cd_p1", il), Cd_p2=mem.coef("Cd_p2", il),
+                             Cd_End=mem.coef("Cd_End", il), Ca_p1=mem.coef("Ca_p1", il),
+                             Ca_p2=mem.coef("Ca_p2", il), Ca_End=mem.coef("Ca_End", il), a_i=float(mem.a_i[il]),
+                             Imat=mem.Imat[il].copy(),
+                             Imcf=mem.Imat_MCF[il] if (mem.MCF and mem.Imat_MCF is not None) else None))
+    T = {}
+    for k in ["member", "node", "circ", "sub", "mcf"]:
+        T["node_" + k] = np.array([r[k] for r in rows], dtype=np.int64)
+    for k in ["r", "r_rel", "q", "p1", "p2", "ds", "drs"]:
+        T["node_" + k] = np.array([r[k] for r in rows], dtype=float)
+    for k in ["dls", "Cd_q", "Cd_p1", "Cd_p2", "Cd_End", "Ca_p1", "Ca_p2", "Ca_End", "a_i"]:
+        T["node_" + k] = np.array([r[k] for r in rows], dtype=float)
+    T["node_Imat"] = np.array([r["Imat"] for r in rows])
+    if any(r["Imcf"] is not None for r in rows):
+        T["node_Imat_MCF"] = np.array([r["Imcf"] if r["Imcf"] is not None else np.zeros([3, 3, fowt.nw], complex)
+                                       for r in rows])
+    T.update(w=np.asarray(fowt.w, float), k=np.asarray(fowt.k, float), dw=np.float64(fowt.dw),
+             depth=np.float64(fowt.depth), rho=np.float64(fowt.rho_water), g=np.float64(fowt.g), r6=fowt.r6.copy(),
+             A_BEM=np.zeros([6, 6, fowt.nw]), B_BEM=np.zeros([6, 6, fowt.nw]))
+    for k in ["M_struc", "B_struc", "C_struc", "C_hydro", "C_moor", "A_hydro_morison"]:
+        T[k] = np.array(getattr(fowt, k), dtype=float)
+    return T

@@ -121,6 +121,18 @@ def design_tables(fowt):
     return out
 
 
+def rotor_inputs(fowt):
+    """Per-rotor statics the AxRNA / Mbase channels read (raft/raft_fowt.py:1909-1951)."""
+    rl = fowt.rotorList
+    return dict(rot_r_rel_z=np.array([r.r_rel[2] for r in rl], dtype=float),
+                rot_mRNA=np.array([r.mRNA for r in rl], dtype=float),
+                rot_IrRNA=np.array([r.IrRNA for r in rl], dtype=float),
+                rot_mtower=np.array(fowt.mtower, dtype=float),
+                rot_zCG_tow=np.array([c[2] for c in fowt.rCG_tow], dtype=float),
+                rot_zBase=np.array([fowt.memberList[fowt.nplatmems + i].rA[2] for i in range(len(rl))], dtype=float),
+                rot_Mtow=np.array([fowt.memberList[fowt.nplatmems + i].M_struc for i in range(len(rl))], dtype=float))
+
+
 def run_solve(model, case, tol=0.01):
     buf = io.StringIO()
     t0 = time.perf_counter()
@@ -184,6 +196,12 @@ def golden_solve(tag, yaml_path, cases, settings=None, keep_Z=False):
         out[f"out_{dof}_std"] = np.array([m[f"{dof}_std"] for m in metrics])
         out[f"out_{dof}_PSD"] = np.array([m[f"{dof}_PSD"] for m in metrics])
     out["out_wave_PSD"] = np.array([m["wave_PSD"] for m in metrics])
+    # rotor channels of saveTurbineOutputs (raft/raft_fowt.py:1900-1970) and their inputs
+    for ch in ["AxRNA", "Mbase"]:
+        for st in ["avg", "std", "max", "min", "PSD"]:
+            out[f"out_{ch}_{st}"] = np.array([m[f"{ch}_{st}"] for m in metrics])
+    out["out_metric_keys"] = np.array(sorted(metrics[0].keys()))
+    out.update(rotor_inputs(fowt))
     out["nIter"] = np.int64(model.nIter)
     out["XiStart"] = np.float64(model.XiStart)
     keys = ["wave_spectrum", "wave_period", "wave_height", "wave_heading", "wave_gamma"]

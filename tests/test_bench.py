@@ -1,0 +1,41 @@
+"""CPU: the bench.py multi-rank harness.  `bench.py --gpus 2` started as a plain process
+re-launches itself as two ranks (torch.distributed.run, 127.0.0.1) and rank 0 prints ONE JSON
+line with n_gpus 2.  --harness-check replaces the GPU work by stub steps on gloo, so the
+launch, barrier, max-over-ranks timing and printing are exercised without a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+
+def _run(*argv):
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], capture_output=True, text=True,
+                       timeout=240, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip().startswith("{")]
+    return lines
+
+
+def test_gpus2_launches_two_ranks_one_line():
+    lines = _run("--gpus", "2", "--harness-check", "--steps", "3", "--warmup", "1")
+    assert len(lines) == 1, lines
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["steps"] == 3
+    # rank 1 sleeps twice as long per step: the reported time is the max over ranks
+    assert d["ms_per_step"] >= 2.0
+
+
+def test_gpus1_single_rank():
+    lines = _run("--gpus", "1", "--harness-check", "--steps", "2", "--warmup", "0")
+    assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 1
+
+
+def test_host_cores_respects_affinity():
+    sys.path.insert(0, ROOT)
+    import bench
+    P, note = bench.host_cores()
+    assert 1 <= P <= len(os.sched_getaffinity(0)) and "affinity" in note

@@ -59,6 +59,22 @@ def test_solve_dynamics_matches_reference(tag, design, settings):
             np.testing.assert_allclose(res[dof + "_PSD"], T[f"out_{dof}_PSD"][ic], rtol=RTOL, atol=RTOL * pmax)
         if "out_Z" in T:
             assert rel(f.Z, T["out_Z"][ic]) < 1e-12
+        check_rotor_channels(res, T, ic)
+
+
+def check_rotor_channels(res, T, ic):
+    """AxRNA_* / Mbase_* (raft/raft_fowt.py:1900-1970, rh_channel_stats) against the
+    reference's own saveTurbineOutputs values."""
+    if "out_AxRNA_std" not in T:
+        return
+    for ch in ["AxRNA", "Mbase"]:
+        scale = np.abs(T[f"out_{ch}_std"][ic]).max()
+        pscale = np.abs(T[f"out_{ch}_PSD"][ic]).max()
+        for st in ["avg", "std", "max", "min"]:
+            np.testing.assert_allclose(res[f"{ch}_{st}"], T[f"out_{ch}_{st}"][ic], rtol=RTOL, atol=RTOL * scale,
+                                       err_msg=f"{ch}_{st}")
+        assert res[f"{ch}_PSD"].shape == T[f"out_{ch}_PSD"][ic].shape
+        np.testing.assert_allclose(res[f"{ch}_PSD"], T[f"out_{ch}_PSD"][ic], rtol=RTOL, atol=RTOL * pscale)
 
 
 @pytest.mark.parametrize("tag,design", [("fowt_VolturnUS-S", "VolturnUS-S_test"), ("fowt_OC3spar", "OC3spar_test")])
@@ -166,7 +182,7 @@ def test_full_size_c2_batch_properties():
     T = load_golden("c2_nw1000")
     m, f = make_model("VolturnUS-S_example", T, {"min_freq": 0.0002})
     cases = random_cases(512, 20241016)
-    a = m.analyzeCasesBatch(cases)
+    a = m.analyzeCasesBatch(cases, want=("psd", "std", "zeta", "B_drag", "margin"))
     b = m.analyzeCasesBatch(cases)
     np.testing.assert_array_equal(a["Xi"], b["Xi"])
     np.testing.assert_array_equal(a["iters"], b["iters"])
@@ -175,9 +191,14 @@ def test_full_size_c2_batch_properties():
     np.testing.assert_array_equal(c["Xi"], a["Xi"][perm])
     assert set(np.unique(a["status"])) <= {0, 1}
     assert np.all(a["iters"][a["status"] == 0] == int(T["nIter"]) + 1)
-    for ic in np.random.default_rng(5).choice(len(cases), 6, replace=False):
+    # a random sample plus the 16 closest calls of the convergence test (the cases whose
+    # iteration count is most at risk of flipping, rh_solve_out.margin)
+    close = np.argsort(np.abs(a["margin"]))[:16]
+    pick = np.unique(np.concatenate([np.random.default_rng(5).choice(len(cases), 6, replace=False), close]))
+    print(f"closest calls |margin|/tol: {np.sort(np.abs(a['margin']))[:4] / 0.01}")
+    for ic in pick:
         r = O.solve_dynamics(T, dict(cases[ic]), int(T["nIter"]), float(T["XiStart"]))
-        assert a["iters"][ic] == r["iters"]
+        assert a["iters"][ic] == r["iters"], (ic, a["margin"][ic])
         assert rel(a["Xi"][ic], r["Xi"][0]) < RTOL
 
 
@@ -227,11 +248,11 @@ def test_fast_and_general_kernels_agree(tag, design, settings, ncase, other, mon
     if other == 2:
         monkeypatch.setenv("RAFT_GROUP_WIDTH", "2")
     else:
-        N.check(N.lib().rh_set_solver(other), "rh_set_solver")
+        N.check(N.lib().rh_set_solver(N.context(0), other), "rh_set_solver")
     try:
         b = m.analyzeCasesBatch(cases, want=want)
     finally:
-        N.check(N.lib().rh_set_solver(0), "rh_set_solver")
+        N.check(N.lib().rh_set_solver(N.context(0), 0), "rh_set_solver")
     np.testing.assert_array_equal(a["iters"], b["iters"])
     np.testing.assert_array_equal(a["status"], b["status"])
     for ic in range(ncase):
@@ -261,3 +282,64 @@ def test_solve_with_native_statics(tag, design, settings):
         Xi = m.solveDynamics(dict(case))
         assert f.iterations == T["out_iters"][ic]
         assert rel(Xi, T["out_Xi"][ic]) < RTOL
+
+
+def test_analyze_cases_c1_every_channel():
+    """Model.analyzeCases on OC3spar (C1, the design's own case table, wind 0) with the
+    reference's statics and mooring stiffness: results['case_metrics'][iCase][0] carries every
+    key the reference's saveTurbineOutputs writes (except the mooring-tension Tmoor_*
+    channels, which need a mooring system) and matches its values; the keys the WEIS caller
+    reads (raft/omdao_raft.py:767-801) are present."""
+    import raft
+    T = load_golden("c1_OC3spar")
+    d = load_design("OC3spar")
+    cases = golden_cases(T)
+    d["cases"]["data"] = [[c.get(k, 0) if k not in ("wind_speed",) else 0 for k in d["cases"]["keys"]]
+                          for c in cases]
+    for row, c in zip(d["cases"]["data"], cases):
+        for j, k in enumerate(d["cases"]["keys"]):
+            if k in c:
+                row[j] = c[k]
+    m = raft.Model(d, statics=[statics_of(T)])
+    res = m.analyzeCases()
+    assert set(res) >= {"properties", "case_metrics", "mean_offsets"}
+    ref_keys = set(str(k) for k in T["out_metric_keys"]) - {f"Tmoor_{s}" for s in ["avg", "std", "max", "min", "PSD"]}
+    for ic in range(len(cases)):
+        cm = res["case_metrics"][ic][0]
+        assert set(cm) >= ref_keys, sorted(ref_keys - set(cm))
+        assert rel(cm["surge_RA"], T["out_Xi"][ic][:, 0, :]) < RTOL
+        assert rel(cm["pitch_RA"], T["out_Xi"][ic][:, 4, :] * 57.29577951308232) < RTOL
+        for dof in ["surge", "sway", "heave", "roll", "pitch", "yaw"]:
+            np.testing.assert_allclose(cm[dof + "_std"], T[f"out_{dof}_std"][ic], rtol=RTOL, atol=1e-300)
+        np.testing.assert_allclose(cm["wave_PSD"], T["out_wave_PSD"][ic], rtol=RTOL)
+        check_rotor_channels(cm, T, ic)
+        for n in ["surge", "sway", "heave", "roll", "pitch", "yaw", "AxRNA", "Mbase"]:   # omdao_raft.py:767-777
+            for st in ["avg", "std", "max", "PSD"]:
+                assert f"{n}_{st}" in cm
+        assert "omega_max" in cm                                                          # :800
+
+
+def test_margin_output_and_knobs():
+    """rh_solve_out.margin: the closest call of the convergence test is finite, negative for
+    cases whose final iteration passed, and independent of the kernel choice (per-context
+    knob rh_set_solver)."""
+    from raft import _native as N
+    from raft.solver import CaseSet, solve_batch
+    T = load_golden("c2_nw200")
+    m, f = make_model("VolturnUS-S_example", T)
+    cases = random_cases(24, 5)
+    cs = CaseSet(np.zeros(len(cases), dtype=np.int32), [c["wave_heading"] for c in cases], ["JONSWAP"] * len(cases),
+                 [c["wave_height"] for c in cases], [c["wave_period"] for c in cases], [0.0] * len(cases))
+    a = solve_batch([f.device_design()], cs, m.nIter, m.XiStart, 0.01, want=("margin",)).host()
+    ctx = N.context(0)
+    assert N.lib().rh_set_solver(ctx, 7) == N.RH_EINVAL
+    N.check(N.lib().rh_set_solver(ctx, 1), "rh_set_solver")
+    try:
+        b = solve_batch([f.device_design()], cs, m.nIter, m.XiStart, 0.01, want=("margin",)).host()
+    finally:
+        N.check(N.lib().rh_set_solver(ctx, 0), "rh_set_solver")
+    assert np.all(np.isfinite(a["margin"]))
+    conv = a["status"] == N.RH_CASE_CONVERGED
+    assert np.all(a["margin"][~conv] > 0) or np.all(conv)
+    np.testing.assert_array_equal(a["iters"], b["iters"])
+    np.testing.assert_allclose(a["margin"], b["margin"], rtol=1e-9, atol=1e-15)

@@ -32,6 +32,29 @@ def test_oracle_solve_dynamics_matches_reference(tag):
             np.testing.assert_allclose(mo[dof + "_PSD"], T[f"out_{dof}_PSD"][ic], rtol=1e-11, atol=1e-12 * pmax)
 
 
+ROTOR_TAGS = ["c1_OC3spar", "c2_nw200", "multi_heading", "c2_nw1000"]
+
+
+def rotor_dict(T):
+    return {k[4:]: T[k] for k in T if k.startswith("rot_")}
+
+
+@pytest.mark.parametrize("tag", ROTOR_TAGS)
+def test_oracle_rotor_channels_match_reference(tag):
+    """AxRNA_* / Mbase_* of saveTurbineOutputs (raft/raft_fowt.py:1900-1970) from the
+    reference's own Xi and rotor statics."""
+    T = load_golden(tag)
+    if "out_AxRNA_std" not in T:
+        pytest.skip("fixture predates the rotor channels (regenerate with make_golden.py)")
+    for ic in range(len(T["out_Xi"])):
+        r = O.rotor_outputs(T["out_Xi"][ic], T["w"], float(T["dw"]), rotor_dict(T), Xi0_pitch=T["r6"][4],
+                            g=float(T["g"]))
+        for ch in ["AxRNA", "Mbase"]:
+            for st in ["avg", "std", "max", "min", "PSD"]:
+                ref = T[f"out_{ch}_{st}"][ic]
+                np.testing.assert_allclose(r[f"{ch}_{st}"], ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+
+
 def test_oracle_farm_matches_reference():
     """C4: two coupled FOWTs (tests/test_data/VolturnUS-S_farm.yaml) with the array
     stiffness fixture: per-FOWT iteration counts, the 12-DOF system response, B_drag."""

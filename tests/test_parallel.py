@@ -192,3 +192,43 @@ def test_bin_shards_cover_every_bin_once():
                 lo, hi = bin_shard(nw, r, world)
                 seen[lo:hi] += 1
             assert (seen == 1).all()
+
+
+def _too_few_cases_check(rank, world):
+    """Fewer cases than ranks: every rank raises the same ValueError before any collective
+    (no rank is left waiting in the gather)."""
+    from raft.parallel import solve_cases_sharded
+    from raft.solver import CaseSet
+    cs = CaseSet([0], [0.0], ["JONSWAP"], [2.0], [10.0], [0.0])
+    with pytest.raises(ValueError, match="every rank needs one"):
+        solve_cases_sharded([object()], cs, 4, group=None, gather=True)
+    dist.barrier()          # both ranks got here: nobody hangs
+
+
+def test_too_few_cases_raises_on_every_rank_world2():
+    _run(_too_few_cases_check)
+
+
+def _qtf_local_check(rank, world):
+    """QtfDevice.qtf with group=None stays local under an initialised default group (the
+    FOWT.calcQTF_slenderBody path): ranks solving different cases never enter a collective.
+    Only an explicit group shards."""
+    import raft.parallel as P
+    from raft.qtf import QtfDevice
+    taken = []
+    orig = P.assemble_qtf
+    P.assemble_qtf = lambda *a, **kw: taken.append("sharded")
+    q = QtfDevice.__new__(QtfDevice)         # no device tables: only the dispatch is exercised
+    q.torch, q.n2, q.dev = torch, 3, torch.device("cpu")
+    try:
+        q.qtf(None, None, None, group=dist.group.WORLD)
+        assert taken == ["sharded"]
+        with pytest.raises(Exception):       # the local path reaches the device call (no GPU here)
+            q.qtf(None, None, None)
+        assert taken == ["sharded"]
+    finally:
+        P.assemble_qtf = orig
+
+
+def test_qtf_default_group_is_local_world2():
+    _run(_qtf_local_check)

@@ -29,7 +29,7 @@ def main():
     out = {}
     modes = [int(x) for x in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["2", "0"])]
     for mode in modes:
-        N.check(N.lib().rh_set_solver(mode), "rh_set_solver")
+        N.check(N.lib().rh_set_solver(N.context(0), mode), "rh_set_solver")
         for _ in range(3):
             res = solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=want, prepared=prep)
         torch.cuda.synchronize()
@@ -53,7 +53,7 @@ def main():
         out[mode] = h
         it = h["iters"]
         print(f"mode {mode} n {nc} width {os.environ.get('RAFT_GROUP_WIDTH', '-')}: {ms:8.3f} ms/launch  {nc / ms * 1e3:10.0f} cases/s  iters mean {it.mean():.3f}", flush=True)
-    N.check(N.lib().rh_set_solver(0), "rh_set_solver")
+    N.check(N.lib().rh_set_solver(N.context(0), 0), "rh_set_solver")
     if 0 in out and 2 in out:
         a, b = out[0], out[2]
         same = np.array_equal(a["iters"], b["iters"]) and np.array_equal(a["status"], b["status"])

@@ -16,7 +16,7 @@ def main(tag):
     T, f, qd, dd, X, M66, w2, k2, nkay, nwl = bench.build_qtf(0)
     ref = None
     for waves in ((0,) if tag == "pmc" else (1, 2, 4)):     # PMC passes: the default (auto) kernel only
-        N.check(N.lib().rh_set_qtf_waves(waves), "rh_set_qtf_waves")
+        N.check(N.lib().rh_set_qtf_waves(N.context(0), waves), "rh_set_qtf_waves")
         for _ in range(2):
             q = qd.qtf(dd.w, X, M66)
         torch.cuda.synchronize()
@@ -31,7 +31,7 @@ def main(tag):
             ref = qh
         d = np.abs(qh - ref).max() / np.abs(ref).max()
         print(f"{tag:10s} waves={waves} QTF {e0.elapsed_time(e1) / 10:8.3f} ms  maxrel vs waves=1 {d:.2e}", flush=True)
-    N.check(N.lib().rh_set_qtf_waves(0), "rh_set_qtf_waves")
+    N.check(N.lib().rh_set_qtf_waves(N.context(0), 0), "rh_set_qtf_waves")
 
 
 if __name__ == "__main__":
