@@ -400,10 +400,15 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int b = tid + kThreads * j;
+        const int bc = b < nw ? b : nw - 1;     // unpredicated loads, pad lanes zeroed after
         cd X[6];
 #pragma unroll
-        for (int c = 0; c < 6; ++c) X[c] = (b < nw) ? ld(XL + c * nw + b) : mk(0, 0);
-        const double w = (b < nw) ? d.w[b] : 0.0;
+        for (int c = 0; c < 6; ++c) {
+          const cd v = ld(XL + c * nw + bc);
+          X[c] = (b < nw) ? v : mk(0, 0);
+        }
+        const double wl = d.w[bc];
+        const double w = (b < nw) ? wl : 0.0;
         cd Aq = mk(0, 0), A1 = mk(0, 0), A2 = mk(0, 0);
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
@@ -425,16 +430,15 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
         double s0 = 0, s1 = 0, s2 = 0;
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-          const int b = tid + kThreads * j;
-          if (b < nw) {
-            const double z = zt[j];
-            const cd sq = sub(scl(ld(K + b), z), Bq[j]);
-            const cd sp1 = sub(scl(ld(K + nw + b), z), add(B1[j], scl(E1[j], t)));
-            const cd sp2 = sub(scl(ld(K + 2 * nw + b), z), add(B2[j], scl(E2[j], t)));
-            s0 += abs2(sq);
-            s1 += abs2(sp1);
-            s2 += abs2(sp2);
-          }
+          // pad lanes (b >= nw) read the last bin and add exactly 0: zeta = 0 and XiLast = 0
+          const int b = tid + kThreads * j < nw ? tid + kThreads * j : nw - 1;
+          const double z = zt[j];
+          const cd sq = sub(scl(ld(K + b), z), Bq[j]);
+          const cd sp1 = sub(scl(ld(K + nw + b), z), add(B1[j], scl(E1[j], t)));
+          const cd sp2 = sub(scl(ld(K + 2 * nw + b), z), add(B2[j], scl(E2[j], t)));
+          s0 += abs2(sq);
+          s1 += abs2(sp1);
+          s2 += abs2(sp2);
         }
         s0 = wave_sum(s0);
         s1 = wave_sum(s1);
@@ -484,10 +488,16 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
     // ---------------- C: excitation, Z(w), LU solve, convergence flags ------------------
     bool my_ok = true, my_nan = false, my_sing = false;
     double my_tmax = 0.0;
+    // No lane branches around the register-heavy solve: lanes past the grid (b >= nw)
+    // recompute the last bin and store nothing.  (A divergent region here -- a per-lane
+    // `continue` -- let the compiler's spills of SGPR-holding VGPRs run under a partial EXEC
+    // mask and lose lanes: wrong tables for some cases, caught by the kernel cross-check.)
 #pragma unroll 1
     for (int j = 0; j < NB; ++j) {
-      const int b = tid + kThreads * j;
-      if (b >= nw) continue;
+      const int b0 = tid + kThreads * j;
+      if (!__builtin_amdgcn_ballot_w64(b0 < nw)) continue;   // whole wave past the grid: uniform
+      const bool okb = b0 < nw;
+      const int b = okb ? b0 : nw - 1;
       const double w = d.w[b];
       cd F[6];
       drag_exc_members(d, al, Kp, nw, b, F);
@@ -499,25 +509,28 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
       }
       cd Z[6][6];
       assemble_z(d, mbc, b, w, bd, Z);
-      if (a.o.Z) {
+      if (a.o.Z && okb) {
         rh_c128* Zo = a.o.Z + ((size_t)ic * nw + b) * 36;
 #pragma unroll
         for (int e = 0; e < 36; ++e) st(Zo + e, Z[e / 6][e % 6]);
       }
-      my_sing |= !lu_solve<6>(Z, F);
+      const bool ok_lu = lu_solve<6>(Z, F);
+      my_sing |= okb && !ok_lu;
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
         const cd x = F[c];
         const cd xlast = ld(XL + c * nw + b);
-        my_nan |= (x.r != x.r) || (x.i != x.i);
         // tolCheck = |Xi - XiLast| / (|Xi| + tol) < tol  (raft/raft_model.py:961-962)
         const double t = cabs(sub(x, xlast)) / (cabs(x) + tol);
-        my_ok = my_ok && (t < tol);
-        my_tmax = fmax(my_tmax, t);
-        st(Xo + c * nw + b, x);
-        if (XP) st(XP + c * nw + b, xlast);
-        // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged
-        st(XL + c * nw + b, add(scl(xlast, 0.2), scl(x, 0.8)));
+        if (okb) {
+          my_nan |= (x.r != x.r) || (x.i != x.i);
+          my_ok = my_ok && (t < tol);
+          my_tmax = fmax(my_tmax, t);
+          st(Xo + c * nw + b, x);
+          if (XP) st(XP + c * nw + b, xlast);
+          // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged
+          st(XL + c * nw + b, add(scl(xlast, 0.2), scl(x, 0.8)));
+        }
       }
     }
     if (a.o.margin) {
