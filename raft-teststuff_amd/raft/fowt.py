@@ -119,6 +119,19 @@ class FOWT:
         self.outFolderQTF = plat.get("outFolderQTF")
         self.C_moor = np.zeros([6, 6])
         self.F_moor0 = np.zeros(6)
+        self.body = mpb                    # this FOWT's body in an array-level mooring system
+        # this FOWT's own mooring system (raft/raft_fowt.py:166-189; MoorPy there, raft/mooring.py here)
+        self.ms = None
+        moor = design.get("mooring")
+        if moor:
+            from .mooring import MooringSystem
+            self.ms = MooringSystem.from_yaml(moor)
+            self.ms.transform(trans=[x_ref, y_ref], rot=heading_adjust)
+            self.ms.initialize()
+        self.yawstiff = plat.get("yaw_stiffness", 0)                     # :194-197
+        self.shearExp_water = get_from_dict(site, "shearExp_water", default=0.12)   # :117
+        self.D_hydro = np.zeros(6)
+        self.f_aero0 = np.zeros([6, self.nrotors])
         self.A_BEM = np.zeros([6, 6, self.nw])
         self.B_BEM = np.zeros([6, 6, self.nw])
         self.A_hydro_morison = np.zeros([6, 6])
@@ -135,13 +148,20 @@ class FOWT:
 
     # ------------------------------------------------------------------ set-up
     def setPosition(self, r6):
-        """raft/raft_fowt.py:260-288 (members only; MoorPy is not available)."""
+        """raft/raft_fowt.py:260-288: members, rotors and this FOWT's mooring system; the
+        mooring stiffness C_moor and mean force F_moor0 follow the new pose (unless a C_moor
+        was given to setStatics)."""
         self.r6 = np.array(r6, dtype=float)
         self.Xi0 = self.r6 - np.array([self.x_ref, self.y_ref, 0, 0, 0, 0])
         for mem in self.memberList:
             mem.setPosition(r6=self.r6)
         for rot in self.rnaList:
             rot.setPosition(self.r6)
+        if self.ms is not None:
+            self.ms.set_body_positions([self.r6])
+            self.F_moor0 = self.ms.body_forces(self.ms.bodies[0], lines_only=True)
+            if "C_moor" not in (self._statics or {}):
+                self.C_moor = self.ms.coupled_stiffness_analytic()
         self._dd = self._host = None
         self._qtf_devs = {}
 
@@ -178,6 +198,52 @@ class FOWT:
         if "C_moor" in self._statics:
             self.C_moor = self._statics["C_moor"].copy()
         self._dd = self._host = None
+
+    def calcCurrentLoads(self, case):
+        """Mean Morison drag of a uniform current with a power-law depth profile on every
+        submerged strip node, as forces and moments about the PRP (raft/raft_fowt.py:1297-1382).
+        Host arithmetic: 6 numbers per design and case, outside the response solve."""
+        rho = self.rho_water
+        D = np.zeros(6)
+        speed = get_from_dict(case, "current_speed", shape=0, default=0.0)
+        heading = get_from_dict(case, "current_heading", shape=0, default=0)
+        Zref = 0.0
+        for rot in self.rnaList:
+            if rot.r3[2] < 0:
+                Zref = rot.r3[2]
+        ch, sh = np.cos(np.deg2rad(heading)), np.sin(np.deg2rad(heading))
+        for mem in self.memberList:
+            circ = mem.shape == "circular"
+            for il in range(mem.ns):
+                if not (mem.r[il, 2] < 0):
+                    continue
+                v = speed * ((self.depth - abs(mem.r[il, 2])) / (self.depth + Zref)) ** self.shearExp_water
+                vrel = np.array([v * ch, v * sh, 0])
+                vq = np.sum(vrel * mem.q) * mem.q
+                vp = vrel - vq
+                vp1 = np.sum(vrel * mem.p1) * mem.p1
+                vp2 = np.sum(vrel * mem.p2) * mem.p2
+                ds, drs, dls = mem.ds[il], mem.drs[il], mem.dls[il]
+                if circ:
+                    aq, ap1, ap2 = np.pi * ds * dls, ds * dls, ds * dls
+                    aend = np.abs(np.pi * ds * drs)
+                    n1 = n2 = np.linalg.norm(vp)
+                else:
+                    aq = 2 * (ds[0] + ds[0]) * dls                      # SURVEY.md Q4
+                    ap1, ap2 = ds[0] * dls, ds[1] * dls
+                    aend = np.abs((ds[0] + drs[0]) * (ds[1] + drs[1]) - (ds[0] - drs[0]) * (ds[1] - drs[1]))
+                    n1, n2 = np.linalg.norm(vp1), np.linalg.norm(vp2)
+                nq = np.linalg.norm(vq)
+                Dq = 0.5 * rho * aq * mem.coef("Cd_q", il) * nq * vq
+                Dp1 = 0.5 * rho * ap1 * mem.coef("Cd_p1", il) * n1 * vp1
+                Dp2 = 0.5 * rho * ap2 * mem.coef("Cd_p2", il) * n2 * vp2
+                Dend = 0.5 * rho * aend * mem.coef("Cd_End", il) * nq * vq
+                f = Dq + Dp1 + Dp2 + Dend
+                r = mem.r[il, :] - self.r6[:3]
+                D[:3] += f
+                D[3:] += np.cross(r, f)
+        self.D_hydro = D
+        return D
 
     def calcTurbineConstants(self, case, ptfm_pitch=0):
         """raft/raft_fowt.py:773-845 restricted to what the accelerated path supports: rotor
@@ -519,3 +585,29 @@ class FOWT:
             results[name] = np.zeros(nr)
         for name in ["omega_PSD", "torque_PSD", "bPitch_PSD"]:
             results[name] = np.zeros([self.nw, nr])
+        if self.ms is not None and self.ms.lines:                                      # :1878-1898
+            results.update(mooring_outputs(self.ms, self._xi_dev, self.w, self.device_index, self._xi_dev.shape[0]))
+
+
+def mooring_outputs(ms, X, w, device, nrow):
+    """Mooring-tension channels (raft/raft_fowt.py:1878-1898, raft/raft_model.py:346-388):
+    mean end tensions T = getTensions(), tension amplitudes J_moor Xi with the central-
+    difference tension Jacobian (getCoupledStiffness(tensions=True)), their RMS and PSD
+    (rh_channel_stats; the reference divides this PSD by w[0] instead of dw)."""
+    import torch
+    T = ms.tensions()
+    _, J = ms.coupled_stiffness_fd(tensions=True)
+    nT, ndof = J.shape
+    dev = X.device
+    coef = np.zeros([nT, 2, ndof])
+    coef[:, 0, :] = J
+    ct = torch.tensor(coef, dtype=torch.float64, device=dev).contiguous()
+    wt = torch.tensor(np.asarray(w, dtype=float), dtype=torch.float64, device=dev)
+    pt = torch.empty([nT, len(w)], dtype=torch.float64, device=dev)
+    st = torch.empty([nT], dtype=torch.float64, device=dev)
+    N.check(N.lib().rh_channel_stats(N.context(device), 1, int(nrow), int(ndof), len(w), float(w[0]), N.ptr(wt),
+                                     N.ptr(X.contiguous()), nT, N.ptr(ct), N.ptr(pt), N.ptr(st),
+                                     N.stream_handle(torch, dev)), "rh_channel_stats")
+    std = st.cpu().numpy()
+    return {"Tmoor_avg": T, "Tmoor_std": std, "Tmoor_max": T + 3 * std, "Tmoor_min": T - 3 * std,
+            "Tmoor_PSD": pt.cpu().numpy()}

@@ -15,7 +15,7 @@ import ctypes
 import numpy as np
 
 from . import _native as N
-from .fowt import FOWT
+from .fowt import FOWT, mooring_outputs
 from .hydro_math import DEG2RAD, get_from_dict, wave_numbers
 from .solver import CaseSet, solve_batch
 
@@ -39,7 +39,8 @@ class Model:
         self.depth = get_from_dict(design["site"], "water_depth", dtype=float)
         self.k = wave_numbers(self.w, self.depth)
         self.device = device
-        self.K_array = None          # array-level mooring stiffness [6N,6N] (MoorPy in the reference)
+        self.K_array = None          # array-level mooring stiffness override [6N,6N] (else from self.ms)
+        self.ms = None               # array-level mooring system (raft/raft_model.py:83-102)
         if "array" in design:
             self.nFOWT = len(design["array"]["data"])
             if "turbine" in design and "turbines" not in design:
@@ -49,13 +50,23 @@ class Model:
             if "mooring" in design and "moorings" not in design:
                 design["moorings"] = [design["mooring"]]
             info = [dict(zip(design["array"]["keys"], row)) for row in design["array"]["data"]]
+            if "array_mooring" in design:
+                from .mooring import MooringSystem
+                am = design["array_mooring"]
+                if "file" not in am:
+                    raise Exception("When using 'array_mooring', a MoorDyn-style input file must be provided as 'file'.")
+                self.ms = MooringSystem(depth=self.depth)
+                for i in range(self.nFOWT):
+                    self.ms.add_body([info[i]["x_location"], info[i]["y_location"], 0, 0, 0, 0])
+                self.ms.load_moordyn(am["file"])
             for i in range(self.nFOWT):
                 d_i = {"site": design["site"]}
                 if info[i]["turbineID"] != 0:
                     d_i["turbine"] = design["turbines"][info[i]["turbineID"] - 1]
                 d_i["platform"] = design["platforms"][info[i]["platformID"] - 1]
                 d_i["mooring"] = None if info[i]["mooringID"] == 0 else design["moorings"][info[i]["mooringID"] - 1]
-                self.fowtList.append(FOWT(d_i, self.w, None, depth=self.depth, x_ref=info[i]["x_location"],
+                self.fowtList.append(FOWT(d_i, self.w, self.ms.bodies[i] if self.ms else None, depth=self.depth,
+                                          x_ref=info[i]["x_location"],
                                           y_ref=info[i]["y_location"], heading_adjust=info[i]["heading_adjust"],
                                           device=device))
                 self.coords.append([info[i]["x_location"], info[i]["y_location"]])
@@ -69,6 +80,9 @@ class Model:
             for f, s in zip(self.fowtList, statics):
                 f.setStatics(s)
         self.design = design
+        self.mooring_currentMod = get_from_dict(design.get("mooring") or {}, "currentMod", default=0, dtype=int)
+        if self.ms is not None:
+            self.ms.initialize()
         self.results = {}
 
     @staticmethod
@@ -149,7 +163,7 @@ class Model:
         nW = self.fowtList[-1].nWaves           # the last FOWT's nWaves
         dev = self.fowtList[0].device_design().device
         Xi = torch.zeros([nW + 1, self.nDOF, self.nw], dtype=torch.complex128, device=dev)
-        single = self.nFOWT == 1 and self.K_array is None
+        single = self.nFOWT == 1 and self.K_array is None and self.ms is None
         for ih in range(nW):
             if single and ih == 0:
                 Xi[0] = self.fowtList[0]._res["Xi"][0]                 # Zinv F_wave(0) == last solve
@@ -169,6 +183,7 @@ class Model:
                     Fws[i][ih] = Fws[i][ih] + fowt._f2nd_dev.to(torch.complex128)
                 Xi[ih] = self._system_solve(Zs, [Fw[ih] for Fw in Fws])
         self.Xi = Xi.cpu().numpy()
+        self._xi_dev_all = Xi
         for i, fowt in enumerate(self.fowtList):
             xi_i = Xi[:, 6 * i:6 * i + 6, :].contiguous()
             psd = torch.empty([6, self.nw], dtype=torch.float64, device=dev)
@@ -194,6 +209,15 @@ class Model:
             print(f" Iteration {iters - 1}, converged (< {tol})")
         return status, iters
 
+    def array_stiffness(self):
+        """Array-level mooring stiffness added to Z_sys (raft/raft_model.py:1030-1031): the
+        K_array override, else the array mooring system's analytic coupled stiffness."""
+        if self.K_array is not None:
+            return np.asarray(self.K_array, dtype=float)
+        if self.ms is not None:
+            return self.ms.coupled_stiffness_analytic()
+        return None
+
     def _system_solve(self, Zs, Fs):
         """Z_sys = blockdiag(Z_i) (+ K_array); Xi = Z_sys^-1 F (raft/raft_model.py:1021-1065)."""
         import torch
@@ -202,16 +226,200 @@ class Model:
         Z = torch.stack(Zs).contiguous()                  # [nf, nw, 6, 6]
         F = torch.cat(Fs, dim=0).contiguous()             # [6nf, nw]
         K = None
-        if self.K_array is not None:
-            K = torch.tensor(np.asarray(self.K_array, dtype=float), dtype=torch.float64, device=dev).contiguous()
+        Ka = self.array_stiffness()
+        if Ka is not None:
+            K = torch.tensor(Ka, dtype=torch.float64, device=dev).contiguous()
         X = torch.empty([6 * nf, self.nw], dtype=torch.complex128, device=dev)
         N.check(N.lib().rh_system_solve(N.context(self.device), nf, self.nw, N.ptr(Z), N.ptr(K), N.ptr(F), N.ptr(X),
                                         N.stream_handle(torch, dev)), "rh_system_solve")
         return X
 
+    # --------------------------------------------------------------------- statics
+    def solveStatics(self, case, display=0):
+        """Mean offsets of every FOWT for a load case (raft/raft_model.py:479-790): linear
+        hydrostatics about the reference position (statics_mod 0), constant environmental
+        loads (forcing_mod 0: mean aero = 0 here, current drag, mean wave drift), nonlinear
+        mooring forces, Newton steps on the total stiffness through dsolve2.  Leaves every
+        FOWT at its offset pose (setPosition), as the reference does."""
+        from .dsolve import dsolve2
+        nD = self.nDOF
+        K_hs, F_und = [], np.zeros(nD)
+        F_env = np.zeros(nD)
+        X_init = np.zeros(nD)
+        if case and isinstance(case.get("wind_speed"), list) and len(case["wind_speed"]) != len(self.fowtList):
+            raise IndexError("List of wind speeds must be the same length as the list of wind turbines")
+        for i, fowt in enumerate(self.fowtList):
+            X_init[6 * i:6 * i + 6] = [fowt.x_ref, fowt.y_ref, 0, 0, 0, 0]
+            fowt.setPosition(X_init[6 * i:6 * i + 6])
+            fowt.calcStatics()
+            K_hs.append(fowt.C_struc + fowt.C_hydro)
+            F_und[6 * i:6 * i + 6] += fowt.W_struc + fowt.W_hydro
+            if case:
+                ci = dict(case)
+                if isinstance(case.get("wind_speed"), list):
+                    ci["wind_speed"] = case["wind_speed"][i]
+                fowt.calcTurbineConstants(ci, ptfm_pitch=0)
+                fowt.calcHydroConstants()
+                F_env[6 * i:6 * i + 6] = np.sum(fowt.f_aero0, axis=1) + fowt.calcCurrentLoads(ci)
+                if getattr(fowt, "Fhydro_2nd_mean", None) is not None:
+                    F_env[6 * i:6 * i + 6] += np.sum(fowt.Fhydro_2nd_mean, axis=0)
+        if case and self.mooring_currentMod > 0 and get_from_dict(case, "current_speed", shape=0, default=0.0) > 0:
+            raise NotImplementedError("current loads on mooring lines (mooring currentMod > 0)")
+        tols = np.array([0.05, 0.05, 0.05, 0.005, 0.005, 0.005] * len(self.fowtList))
+
+        def eval_func(X, args):
+            for i, fowt in enumerate(self.fowtList):
+                fowt.setPosition(X[6 * i:6 * i + 6])
+            if self.ms is not None:
+                self.ms.set_body_positions([X[6 * i:6 * i + 6] for i in range(self.nFOWT)])
+            Fnet = np.zeros(nD)
+            for i, fowt in enumerate(self.fowtList):
+                Xi0 = X[6 * i:6 * i + 6] - np.array([fowt.x_ref, fowt.y_ref, 0, 0, 0, 0])
+                Fnet[6 * i:6 * i + 6] += F_und[6 * i:6 * i + 6]
+                Fnet[6 * i:6 * i + 6] += -np.matmul(K_hs[i], Xi0)
+                if case:
+                    Fnet[6 * i:6 * i + 6] += F_env[6 * i:6 * i + 6]
+                Fnet[6 * i:6 * i + 6] += fowt.F_moor0
+                if self.ms is not None:
+                    Fnet[6 * i:6 * i + 6] += self.ms.body_forces(self.ms.bodies[i], lines_only=True)
+            return Fnet, dict(status=1), False
+
+        def step_func(X, args, Y, oths, Ytarget, err, tol_, it, maxIter):
+            K = np.zeros([nD, nD])
+            if self.ms is not None:
+                K += self.ms.coupled_stiffness_analytic()
+            for i, fowt in enumerate(self.fowtList):
+                K6 = K_hs[i].copy()
+                if fowt.ms is not None:
+                    K6 += fowt.ms.coupled_stiffness_analytic()
+                K[6 * i:6 * i + 6, 6 * i:6 * i + 6] += K6
+            kmean = np.mean(K.diagonal())
+            for i in range(nD):
+                if K[i, i] == 0:
+                    K[i, i] = kmean
+            dX = np.linalg.solve(K, Y)
+            for _ in range(10):                       # strengthen the diagonal on a backward step (:738-748)
+                if sum(dX * Y) < 0:
+                    for i in range(nD):
+                        K[i, i] += 0.1 * abs(K[i, i])
+                    dX = np.linalg.solve(K, Y)
+                else:
+                    break
+            return dX
+
+        X, Y, info = dsolve2(eval_func, X_init, step_func=step_func, tol=tols, a_max=1.6, maxIter=20,
+                             args={"display": display})
+        self.Xs2, self.Es2 = info["Xs"], info["Es"]
+        if case and "iCase" in case:
+            self.results.setdefault("mean_offsets", []).append(self.Xs2[-1])
+        if display > 0:
+            for i, fowt in enumerate(self.fowtList):
+                print(f"Found mean offets of FOWT {i + 1} with surge = {fowt.Xi0[0]: .2f} m,  sway  = "
+                      f"{fowt.Xi0[1]: .2f},  and heave = {fowt.Xi0[2]: .2f} m")
+        return X
+
+    def solveEigen(self, display=0):
+        """Natural frequencies [Hz] and mode shapes of the moored system
+        (raft/raft_model.py:391-476): M = M_struc + A_hydro_morison, C = C_struc + C_hydro +
+        C_moor (+ yaw stiffness, + array mooring).  Host LAPACK on a 6N x 6N pencil."""
+        nD = self.nDOF
+        M_tot = np.zeros([nD, nD])
+        C_tot = np.zeros([nD, nD])
+        for i, fowt in enumerate(self.fowtList):
+            i1, i2 = 6 * i, 6 * i + 6
+            M_tot[i1:i2, i1:i2] += fowt.M_struc + fowt.A_hydro_morison
+            C_tot[i1:i2, i1:i2] += fowt.C_struc + fowt.C_hydro + fowt.C_moor
+            C_tot[i1 + 5, i1 + 5] += fowt.yawstiff
+        if self.ms is not None:
+            C_tot += self.ms.coupled_stiffness_analytic()
+        message = ""
+        for i in range(nD):
+            if M_tot[i, i] < 1.0:
+                message += f"Diagonal entry {i} of system mass matrix is less than 1 ({M_tot[i, i]}). "
+            if C_tot[i, i] < 1.0:
+                message += f"Diagonal entry {i} of system stiffness matrix is less than 1 ({C_tot[i, i]}). "
+        if message:
+            raise RuntimeError("System matrices computed by RAFT have one or more small or negative diagonals: "
+                               + message)
+        eigenvals, eigenvectors = np.linalg.eig(np.linalg.solve(M_tot, C_tot))
+        if any(eigenvals <= 0.0):
+            raise RuntimeError("Error: zero or negative system eigenvalues detected.")
+        ind_list = []
+        for i in range(nD - 1, -1, -1):              # DOF order by the largest mode component (:442-456)
+            vec = np.abs(eigenvectors[i, :])
+            for _ in range(nD):
+                ind = np.argmax(vec)
+                if ind in ind_list:
+                    vec[ind] = 0.0
+                else:
+                    ind_list.append(ind)
+                    break
+        ind_list.reverse()
+        fns = np.sqrt(eigenvals[ind_list]) / 2.0 / np.pi
+        modes = eigenvectors[:, ind_list]
+        if display > 0:
+            print("Fn (Hz)" + "".join([f"{fn:10.4f}" for fn in fns]))
+        self.results["eigen"] = {"frequencies": fns, "modes": modes}
+        return fns, modes
+
+    def analyzeUnloaded(self, ballast=0, heave_tol=1):
+        """Unloaded equilibrium and mooring properties (raft/raft_model.py:184-241)."""
+        if len(self.fowtList) > 1:
+            raise Exception("analyzeUnloaded is an old method that only works for a single FOWT.")
+        if ballast:
+            raise NotImplementedError("ballast adjustment (raft/raft_model.py:1434-1625) is outside the accelerated path")
+        f0 = self.fowtList[0]
+        f0.setPosition(np.zeros(6))
+        f0.D_hydr0 = np.zeros(6)
+        f0.f_aero0 = np.zeros([6, f0.nrotors])
+        self.C_moor0 = np.zeros([6, 6])
+        self.F_moor0 = np.zeros(6)
+        for ms in (self.ms, f0.ms):
+            if ms is not None:
+                self.C_moor0 += ms.coupled_stiffness_fd()
+                self.F_moor0 += ms.coupled_forces(lines_only=True)
+        for fowt in self.fowtList:
+            fowt.calcStatics()
+            fowt.calcHydroConstants()
+        self.results["properties"] = {}
+        self.solveStatics(None)
+        self.results["properties"]["offset_unloaded"] = self.fowtList[0].Xi0
+
+    def calcOutputs(self):
+        """System property outputs of the first FOWT (raft/raft_model.py:1150-1189)."""
+        fowt = self.fowtList[0]
+        if "properties" in self.results:
+            C0 = getattr(self, "C_moor0", np.zeros([6, 6]))
+            P = self.results["properties"]
+            P["tower mass"] = fowt.mtower
+            P["tower CG"] = fowt.rCG_tow
+            P["substructure mass"] = fowt.m_sub
+            P["substructure CG"] = fowt.rCG_sub
+            P["shell mass"] = fowt.m_shell
+            P["ballast mass"] = fowt.m_ballast
+            P["ballast densities"] = fowt.pb
+            P["total mass"] = fowt.M_struc[0, 0]
+            P["total CG"] = fowt.rCG
+            P["roll inertia at subCG"] = fowt.props["Ixx_sub"]
+            P["pitch inertia at subCG"] = fowt.props["Iyy_sub"]
+            P["yaw inertia at subCG"] = fowt.props["Izz_sub"]
+            P["buoyancy (pgV)"] = fowt.rho_water * fowt.g * fowt.V
+            P["center of buoyancy"] = fowt.rCB
+            P["C hydrostatic"] = fowt.C_hydro
+            P["C system"] = fowt.C_struc + fowt.C_hydro + C0
+            P["F_lines0"] = getattr(self, "F_moor0", np.zeros(6))
+            P["C_lines0"] = C0
+            P["M support structure"] = fowt.M_struc_sub
+            P["A support structure"] = fowt.A_hydro_morison + fowt.A_BEM[:, :, -1]
+            P["C support structure"] = fowt.C_struc_sub + fowt.C_hydro + C0
+        return self.results
+
     # --------------------------------------------------------------------- cases
     def analyzeCases(self, display=0, meshDir=None, RAO_plot=False):
-        """raft/raft_model.py:244-388 with the mean offsets held at the reference position."""
+        """raft/raft_model.py:244-388: per case, mean offsets (solveStatics), the response
+        solve on the device, and the output channels of every FOWT (plus array-level mooring
+        tensions).  When every FOWT's mooring stiffness was given as a fixture (setStatics with a
+        C_moor, e.g. the reference-run goldens), the platforms stay at their reference position."""
         nCases = len(self.design["cases"]["data"])
         self.results["properties"] = {}
         self.results["case_metrics"] = {}
@@ -220,16 +428,32 @@ class Model:
             fowt.setPosition([fowt.x_ref, fowt.y_ref, 0, 0, 0, 0])
             fowt.calcStatics()
         for iCase in range(nCases):
+            if display > 0:
+                print(f"\n--------------------- Running Case {iCase + 1} ----------------------")
+                print(self.design["cases"]["data"][iCase])
             case = dict(zip(self.design["cases"]["keys"], self.design["cases"]["data"][iCase]))
             case["iCase"] = iCase
+            nWaves = 1 if np.isscalar(case["wave_heading"]) else len(case["wave_heading"])
             self.results["case_metrics"][iCase] = {}
-            for fowt in self.fowtList:
-                fowt.calcTurbineConstants(case, ptfm_pitch=0)
-                fowt.calcHydroConstants()
+            fixture = all("C_moor" in (f._statics or {}) for f in self.fowtList)
+            if fixture:       # mooring given as a stiffness fixture (setStatics): positions held at the reference
+                for fowt in self.fowtList:
+                    fowt.calcTurbineConstants(case, ptfm_pitch=0)
+                    fowt.calcHydroConstants()
+            else:
+                self.solveStatics(case, display=display)
             self.solveDynamics(case, RAO_plot=RAO_plot, display=display)
+            if any(f.potSecOrder > 0 for f in self.fowtList):
+                if not fixture:
+                    self.solveStatics(case)
+                for fowt in self.fowtList:
+                    fowt.Fhydro_2nd_mean *= 0
             for i, fowt in enumerate(self.fowtList):
                 self.results["case_metrics"][iCase][i] = {}
                 fowt.saveTurbineOutputs(self.results["case_metrics"][iCase][i], case)
+            if self.ms is not None:
+                self.results["case_metrics"][iCase]["array_mooring"] = mooring_outputs(
+                    self.ms, self._xi_dev_all, self.w, self.device, nWaves + 1)
         return self.results
 
     def analyzeCasesBatch(self, cases, tol=0.01, want=("psd", "std", "zeta", "B_drag"), host=True):
@@ -253,3 +477,48 @@ class Model:
         cs = CaseSet(np.zeros(len(cases), dtype=np.int32), hd, sp, Hs, Tp, gm)
         res = solve_batch([fowt.device_design()], cs, self.nIter, self.XiStart, tol, want=want)
         return res.host() if host else res
+
+
+def _load_design(input_file):
+    """A design dict from a dict or a YAML file (raft/raft_model.py:2029-2039).  Pickled
+    designs are refused: unpickling can execute code from the file."""
+    if isinstance(input_file, dict):
+        return input_file
+    if str(input_file).endswith((".pkl", ".pickle")):
+        raise ValueError("pickled design files are not loaded (unpickling can execute code); pass a YAML file or a dict")
+    import yaml
+    print("\n\nLoading RAFT input file: " + str(input_file))
+    with open(input_file) as fh:
+        return yaml.safe_load(fh)
+
+
+def runRAFT(input_file, turbine_file="", plot=0, ballast=False, station_plot=[]):
+    """Set up and run RAFT for a design (raft/raft_model.py:2024-2061): Model, unloaded
+    equilibrium, every load case of design['cases'] (mean offsets, device response solve,
+    output channels) and the system property outputs.  Returns the Model."""
+    design = _load_design(input_file)
+    print(" --- making model ---")
+    model = Model(design)
+    print(" --- analyzing unloaded ---")
+    model.analyzeUnloaded(ballast=ballast)
+    print(" --- analyzing cases ---")
+    model.analyzeCases(display=1)
+    model.calcOutputs()
+    if plot:
+        raise NotImplementedError("plotting is outside the accelerated path")
+    return model
+
+
+def runRAFTFarm(input_file, plot=0):
+    """Set up and run a RAFT farm (raft/raft_model.py:2065-2095): no unloaded analysis and no
+    calcOutputs (as in the reference); analyzeCases over the coupled array."""
+    design = _load_design(input_file)
+    print(" --- making model ---")
+    model = Model(design)
+    print("**Note: RAFTFarm cannot run model.analyzeUnloaded()")
+    print(" --- analyzing cases ---")
+    model.analyzeCases(display=1)
+    print("**Note: model.calcOutputs is not supported yet for multi-turbine Farm configurations")
+    if plot:
+        raise NotImplementedError("plotting is outside the accelerated path")
+    return model

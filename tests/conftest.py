@@ -28,7 +28,10 @@ def load_golden(tag):
 
 def load_design(name):
     with open(os.path.join(GOLDEN, "designs", name + ".json")) as f:
-        return json.load(f)
+        d = json.load(f)
+    if "array_mooring" in d:      # the MoorDyn-style array mooring file sits next to the JSON
+        d["array_mooring"]["file"] = os.path.join(GOLDEN, "designs", os.path.basename(d["array_mooring"]["file"]))
+    return d
 
 
 def golden_cases(T):

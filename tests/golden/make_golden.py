@@ -270,9 +270,10 @@ DESIGNS = {
 
 
 def export_designs():
-    """Design inputs as JSON fixtures (the GPU box has no /root/reference).  Only the
-    sections the accelerated path reads are kept: blade/airfoil aero tables and the
-    MoorPy line definitions are dropped (rotor aero and mooring are out of scope)."""
+    """Design inputs as JSON fixtures (the GPU box has no /root/reference).  Blade/airfoil
+    aero tables are dropped (rotor aero is out of scope); the mooring sections (points,
+    lines, line types) are kept for raft/mooring.py, and the farm's MoorDyn-style array
+    mooring file (a data file of the reference's tests) is copied next to the JSON."""
     os.makedirs(os.path.join(HERE, "designs"), exist_ok=True)
     for name, rel in DESIGNS.items():
         with open(os.path.join(REF, rel)) as f:
@@ -282,13 +283,12 @@ def export_designs():
             for t in (ts if isinstance(ts, list) else [ts] if ts else []):
                 for drop in ("blade", "airfoils", "pitch_control", "torque_control", "wt_ops", "gear_ratio"):
                     t.pop(drop, None)
-        for mk in ("mooring", "moorings"):
-            if mk in d and d[mk]:
-                ms = d[mk] if isinstance(d[mk], list) else [d[mk]]
-                kept = [{"water_depth": m.get("water_depth")} for m in ms]
-                d[mk] = kept if isinstance(d[mk], list) else kept[0]
         if "array_mooring" in d:
-            d["array_mooring"] = {"file": os.path.basename(d["array_mooring"].get("file", ""))}
+            src = os.path.join(os.path.dirname(os.path.join(REF, rel)), d["array_mooring"]["file"])
+            base = os.path.basename(src)
+            with open(src) as fi, open(os.path.join(HERE, "designs", base), "w") as fo:
+                fo.write(fi.read())
+            d["array_mooring"] = {"file": base}
         with open(os.path.join(HERE, "designs", name + ".json"), "w") as f:
             json.dump(d, f, indent=1, default=str)
     print("wrote designs/*.json", file=sys.stderr)
