@@ -271,6 +271,72 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
     return out
 
 
+def bench_c4(device, steps, world, rank, dist, ncase=512):
+    """C4 (BASELINE.json configs[3]): tests/test_data/VolturnUS-S_farm.yaml, 2 coupled FOWTs,
+    12-DOF system per bin, nw = 240; a step = `ncase` JONSWAP sea states per GPU through
+    Model.analyzeArrayBatch: every (case, FOWT) drag fixed point in one launch, the wave
+    excitation, the 12x12 system solves of every (case, bin) and the per-FOWT statistics.
+    Mooring: the reference-run fixture (FOWT C_moor + shared-line array stiffness), the
+    configuration tests/golden/c4_farm.npz pins.  Weak scaling (cases per GPU fixed)."""
+    import raft
+    import torch
+    G = dict(np.load(os.path.join(ROOT, "tests", "golden", "c4_farm.npz")))
+    with open(os.path.join(ROOT, "tests", "golden", "designs", "VolturnUS-S_farm.json")) as fh:
+        design = json.load(fh)
+    design.pop("array_mooring", None)                 # the array stiffness comes from the fixture
+    Ts = []
+    i = 0
+    while f"f{i}_w" in G:
+        Ts.append({k[3:]: v for k, v in G.items() if k.startswith(f"f{i}_")})
+        i += 1
+    m = raft.Model(design, statics=[{k: T[k] for k in ["M_struc", "B_struc", "C_struc", "C_hydro", "C_moor"]}
+                                    for T in Ts], device=device)
+    m.K_array = G["K_array"]
+    for f, T in zip(m.fowtList, Ts):
+        f.setPosition(T["r6"])
+        f.calcStatics()
+        f.calcHydroConstants()
+    cases = sea_states(ncase, 20241020 + rank)
+    for _ in range(2):
+        r = m.analyzeArrayBatch(cases, host=False)
+    torch.cuda.synchronize()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+    stream = torch.cuda.current_stream()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        r = m.analyzeArrayBatch(cases, host=False, marks=(ev[i][1], ev[i][2]))
+        ev[i][3].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=f"cuda:{device}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    kern_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    step_ms = float(np.mean([e[0].elapsed_time(e[3]) for e in ev]))
+    iters = r["iters"].cpu().numpy()
+    dd = m.fowtList[0].device_design()
+    circ = dd.node[N_CIRC()].cpu().numpy()
+    nc, nr = int((circ != 0).sum()), int((circ == 0).sum())
+    flops = float(sum(flops_per_case(int(k), dd.nw, nc, nr, dd.nn) for k in iters.ravel()))
+    achieved = flops / (kern_ms * 1e-3)
+    return {"metric": "coupled-array sea-state cases/sec (2 FOWTs, 12-DOF system)", "value": ncase * world * steps / dt,
+            "unit": "cases/s", "scaling": "weak", "n_gpus": world, "steps": steps, "ms_per_step": dt / steps * 1e3,
+            "device_ms_per_step": step_ms, "iterations_mean": float(iters.mean()),
+            "config": {"workload": "C4: VolturnUS-S_farm, 2 FOWTs (x = 0 / 1600 m), nw=240, JONSWAP sea states",
+                       "cases_per_step_per_gpu": ncase, "nw": dd.nw, "fowts": len(m.fowtList),
+                       "parallelism": f"case-sharded x{world}"},
+            "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_FP64, "traffic": None, "kernel": solve_kernel_name(dd.nw),
+                         "kernel_ms": kern_ms, "flops_per_launch": flops,
+                         "note": "the (case, FOWT) drag fixed-point launch; SURVEY.md §8(d) formula per (case, FOWT)"}}
+
+
 C5_DESIGNS = 250
 
 
@@ -522,7 +588,7 @@ def main():
     }
     if not args.no_qtf:
         line["qtf"] = bench_qtf(device, max(3, args.steps // 4), 1, world, rank, dist)
-    if not args.no_c4 and "bench_c4" in globals():
+    if not args.no_c4:
         line["c4"] = bench_c4(device, max(3, args.steps // 4), world, rank, dist)
     if not args.no_c5:
         line["c5"] = bench_c5(device, max(3, args.steps // 4), world, rank, dist, pool, nproc)

@@ -205,6 +205,12 @@ int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int 
                         const int* design_idx, const int* head, const double* zeta,
                         const double* B_drag, const double* Bmat, rh_c128* Xi, rh_stream stream);
 
+/* Wave excitation of solved cases with the final linearisation, without the solve:
+ * F = zeta_h finer_h + zeta_h sum_n T_n Bmat_n uhat_h,n  -- F_wave of the system solve of an
+ * array (raft/raft_model.py:1049-1061).  Arguments as rh_heading_response; F out: [ncase][6][nw]. */
+int rh_wave_excitation(rh_ctx* ctx, const rh_design* designs, int ndesign, int ncase, const int* design_idx,
+                       const int* head, const double* zeta, const double* Bmat, rh_c128* F, rh_stream stream);
+
 /* Stand-alone FOWT.calcHydroLinearization(Xi) + calcDragExcitation (raft/raft_fowt.py:1152-1293)
  * for one design and one sea state: Xi [6][nw], zeta [nw] (u = zeta*uhat[head]).
  * Outputs: B_drag [36], Bmat [nn][9], F_drag [6][nw]. */
@@ -260,6 +266,11 @@ int rh_channel_stats(rh_ctx* ctx, int ncase, int nrow, int ndof, int nw, double 
  * K: [6nf*6nf] array mooring stiffness (or NULL), F: [6nf][nw], Xi out: [6nf][nw]. */
 int rh_system_solve(rh_ctx* ctx, int nf, int nw, const rh_c128* Z, const double* K,
                     const rh_c128* F, rh_c128* Xi, rh_stream stream);
+
+/* rh_system_solve for ncase independent cases of one array in one launch (the batched farm
+ * path, Model.analyzeCasesBatch): Z [ncase][nf][nw][36], F / Xi [ncase][6nf][nw], K shared. */
+int rh_system_solve_batch(rh_ctx* ctx, int ncase, int nf, int nw, const rh_c128* Z, const double* K,
+                          const rh_c128* F, rh_c128* Xi, rh_stream stream);
 
 /* ------------------------------------------------------------------------------------
  * Slender-body second-order QTF (FOWT.calcQTF_slenderBody, raft/raft_fowt.py:1385-1648)

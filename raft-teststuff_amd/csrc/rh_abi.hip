@@ -272,7 +272,29 @@ int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int 
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
-  rh::HeadArgs a{ctx->d_designs, ncase, design_idx, head, zeta, B_drag, Bmat, Xi};
+  rh::HeadArgs a{ctx->d_designs, ncase, design_idx, head, zeta, B_drag, Bmat, Xi, nullptr};
+  const size_t smem = sizeof(double) * (size_t)(nnmax * 9 + 36 + 108);
+  dim3 grid((nw + kThreads - 1) / kThreads, ncase);
+  hipLaunchKernelGGL(rh::k_heading_resp, grid, dim3(kThreads), smem, s, a);
+  return designs_used(ctx, s);
+}
+
+int rh_wave_excitation(rh_ctx* ctx, const rh_design* designs, int ndesign, int ncase, const int* design_idx,
+                       const int* head, const double* zeta, const double* Bmat, rh_c128* F, rh_stream stream) {
+  if (!ctx || !designs || !design_idx || !head || !zeta || !Bmat || !F)
+    return fail(RH_EINVAL, "rh_wave_excitation: null argument");
+  if (ncase <= 0) return ncase == 0 ? RH_OK : fail(RH_EINVAL, "ncase=%d", ncase);
+  const int nw = designs[0].nw;
+  int nnmax = 0;
+  for (int i = 0; i < ndesign; ++i) {
+    if (int r = check_design(designs[i], true)) return r;
+    if (designs[i].nw != nw) return fail(RH_EINVAL, "rh_wave_excitation: all designs must share nw");
+    if (designs[i].nn > nnmax) nnmax = designs[i].nn;
+  }
+  RH_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
+  rh::HeadArgs a{ctx->d_designs, ncase, design_idx, head, zeta, nullptr, Bmat, nullptr, F};
   const size_t smem = sizeof(double) * (size_t)(nnmax * 9 + 36 + 108);
   dim3 grid((nw + kThreads - 1) / kThreads, ncase);
   hipLaunchKernelGGL(rh::k_heading_resp, grid, dim3(kThreads), smem, s, a);
@@ -381,13 +403,19 @@ int rh_channel_stats(rh_ctx* ctx, int ncase, int nrow, int ndof, int nw, double 
 
 int rh_system_solve(rh_ctx* ctx, int nf, int nw, const rh_c128* Z, const double* K, const rh_c128* F, rh_c128* Xi,
                     rh_stream stream) {
+  return rh_system_solve_batch(ctx, 1, nf, nw, Z, K, F, Xi, stream);
+}
+
+int rh_system_solve_batch(rh_ctx* ctx, int ncase, int nf, int nw, const rh_c128* Z, const double* K, const rh_c128* F,
+                          rh_c128* Xi, rh_stream stream) {
   if (!ctx || !Z || !F || !Xi) return fail(RH_EINVAL, "rh_system_solve: null argument");
-  if (nw <= 0) return fail(RH_EINVAL, "rh_system_solve: nw=%d", nw);
+  if (nw <= 0 || ncase < 0) return fail(RH_EINVAL, "rh_system_solve: nw=%d ncase=%d", nw, ncase);
   if (nf < 1 || nf > 2) return fail(RH_EINVAL, "rh_system_solve: nf=%d (supported: 1, 2)", nf);
+  if (ncase == 0) return RH_OK;
   RH_HIP(hipSetDevice(ctx->device));
   const int N = 6 * nf;
   const size_t smem = sizeof(double) * 2 * (size_t)(N * N + N) * rh::kSysThreads;
-  dim3 grid((nw + rh::kSysThreads - 1) / rh::kSysThreads);
+  dim3 grid((nw + rh::kSysThreads - 1) / rh::kSysThreads, ncase);
   hipLaunchKernelGGL(rh::k_system_solve, grid, dim3(rh::kSysThreads), smem, (hipStream_t)stream, N, nw, Z, K, F, Xi);
   RH_HIP(hipGetLastError());
   return RH_OK;

@@ -618,6 +618,7 @@ struct HeadArgs {
   const double* B_drag;
   const double* Bmat;
   rh_c128* Xi;
+  rh_c128* F;             // non-NULL: store the wave excitation only (no solve)
 };
 
 __global__ __launch_bounds__(kThreads, 2) void k_heading_resp(HeadArgs a) {
@@ -630,7 +631,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_heading_resp(HeadArgs a) {
   double* mbc = bd + 36;
   load_mbc(d, mbc, threadIdx.x);
   for (int e = threadIdx.x; e < nn * 9; e += blockDim.x) bm[e] = a.Bmat[(size_t)ic * nn * 9 + e];
-  if (threadIdx.x < 36) bd[threadIdx.x] = a.B_drag[(size_t)ic * 36 + threadIdx.x];
+  if (threadIdx.x < 36 && a.B_drag) bd[threadIdx.x] = a.B_drag[(size_t)ic * 36 + threadIdx.x];
   __syncthreads();
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nw) return;
@@ -642,6 +643,11 @@ __global__ __launch_bounds__(kThreads, 2) void k_heading_resp(HeadArgs a) {
   drag_exc_bin(d.node, nn, bm, Uh, nw, b, F);
 #pragma unroll
   for (int c = 0; c < 6; ++c) F[c] = add(scl(ld(Fe + c * nw + b), z), scl(F[c], z));
+  if (a.F) {              // F_wave of raft/raft_model.py:1049-1061 for the system solve
+#pragma unroll
+    for (int c = 0; c < 6; ++c) st(a.F + ((size_t)ic * 6 + c) * nw + b, F[c]);
+    return;
+  }
   cd Z[6][6];
   assemble_z(d, mbc, b, d.w[b], bd, Z);
   lu_solve<6>(Z, F);
@@ -914,6 +920,12 @@ __global__ __launch_bounds__(kSysThreads) void k_system_solve(int N, int nw, con
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int t = threadIdx.x;
   const int b = blockIdx.x * blockDim.x + t;
+  {                       // case blockIdx.y of a batch: [ncase][nf][nw][36], [ncase][N][nw]
+    const size_t ic = blockIdx.y;
+    Z += ic * (size_t)(N / 6) * nw * 36;
+    F += ic * (size_t)N * nw;
+    Xi += ic * (size_t)N * nw;
+  }
   // A[i][j] of this thread at smem[2*((i*N + j)*kSysThreads + t)], x[i] after the matrix
   auto Ar = [&](int i, int j) -> double& { return smem[2 * ((i * N + j) * kSysThreads + t)]; };
   auto Ai = [&](int i, int j) -> double& { return smem[2 * ((i * N + j) * kSysThreads + t) + 1]; };

@@ -457,12 +457,20 @@ class Model:
         return self.results
 
     def analyzeCasesBatch(self, cases, tol=0.01, want=("psd", "std", "zeta", "B_drag"), host=True):
-        """Solve many single-sea-state cases of a single-FOWT model in one device call.
+        """Solve many single-sea-state cases in one device call (one workgroup per case).
         cases: list of case dicts (wave_heading/spectrum/period/height/gamma).  Returns a dict
-        of arrays: Xi [n,6,nw], iters, status, psd [n,6,nw], std [n,6], ..."""
+        of arrays: Xi [n,6,nw], iters, status, psd [n,6,nw], std [n,6], ...
+        Arrays (nFOWT > 1) go through analyzeArrayBatch: Xi [n,6N,nw], iters [n,N], ..."""
         if self.nFOWT != 1:
-            raise NotImplementedError("analyzeCasesBatch handles single-FOWT models")
+            return self.analyzeArrayBatch(cases, tol=tol, host=host)
         fowt = self.fowtList[0]
+        hd, sp, Hs, Tp, gm = self._case_columns(cases)
+        cs = CaseSet(np.zeros(len(cases), dtype=np.int32), hd, sp, Hs, Tp, gm)
+        res = solve_batch([fowt.device_design()], cs, self.nIter, self.XiStart, tol, want=want)
+        return res.host() if host else res
+
+    @staticmethod
+    def _case_columns(cases):
         hd, sp, Hs, Tp, gm = [], [], [], [], []
         for c in cases:
             c = dict(c)
@@ -474,9 +482,57 @@ class Model:
             Hs.append(float(one("wave_height")))
             Tp.append(float(one("wave_period")))
             gm.append(float(one("wave_gamma", 0)))
-        cs = CaseSet(np.zeros(len(cases), dtype=np.int32), hd, sp, Hs, Tp, gm)
-        res = solve_batch([fowt.device_design()], cs, self.nIter, self.XiStart, tol, want=want)
-        return res.host() if host else res
+        return hd, sp, Hs, Tp, gm
+
+    def analyzeArrayBatch(self, cases, tol=0.01, host=True, marks=None):
+        """The coupled-array response of many single-sea-state cases (raft/raft_model.py:852-1065
+        for nFOWT > 1) in four device calls instead of per-case, per-FOWT host round trips:
+          1. every (case, FOWT) drag fixed point in one rh_solve_cases launch;
+          2. the wave excitation of each (case, FOWT) with its final linearisation
+             (rh_wave_excitation);
+          3. Z_sys = blockdiag(Z_i) + array mooring stiffness, Xi = Z_sys^-1 F_wave for every
+             case and bin (rh_system_solve_batch);
+          4. per-FOWT motion PSD / RMS (rh_motion_stats).
+        Returns Xi [n, 6N, nw], iters / status [n, N], psd [n, N, 6, nw], std [n, N, 6], zeta.
+        marks: optional two timing events recorded around the fixed-point launch (bench)."""
+        import torch
+        nf, n, nw = self.nFOWT, len(cases), self.nw
+        dds = [f.device_design() for f in self.fowtList]
+        if len(set(d.nn for d in dds)) != 1:
+            raise NotImplementedError("analyzeArrayBatch: FOWTs with different submerged node counts")
+        hd, sp, Hs, Tp, gm = self._case_columns(cases)
+        rep = lambda v: [x for x in v for _ in range(nf)]          # case-major, FOWT-minor
+        cs = CaseSet(np.tile(np.arange(nf, dtype=np.int32), n), rep(hd), rep(sp), rep(Hs), rep(Tp), rep(gm))
+        dev = dds[0].device
+        from .solver import prepare_batch
+        prep = prepare_batch(dds, cs)
+        if marks:
+            marks[0].record(torch.cuda.current_stream(dev))
+        res = solve_batch(dds, cs, self.nIter, self.XiStart, tol, want=("zeta", "Bmat", "Z"), prepared=prep)
+        if marks:
+            marks[1].record(torch.cuda.current_stream(dev))
+        F = torch.empty([n * nf, 6, nw], dtype=torch.complex128, device=dev)
+        arr = (N.RhDesign * nf)(*[d.struct() for d in dds])
+        s = N.stream_handle(torch, dev)
+        ctx = N.context(self.device)
+        N.check(N.lib().rh_wave_excitation(ctx, arr, nf, n * nf, N.ptr(prep["design"]), N.ptr(prep["head"]),
+                                           N.ptr(res["zeta"]), N.ptr(res["Bmat"].contiguous()), N.ptr(F), s),
+                "rh_wave_excitation")
+        Ka = self.array_stiffness()
+        K = None if Ka is None else torch.tensor(Ka, dtype=torch.float64, device=dev).contiguous()
+        X = torch.empty([n, 6 * nf, nw], dtype=torch.complex128, device=dev)
+        N.check(N.lib().rh_system_solve_batch(ctx, n, nf, nw, N.ptr(res["Z"]), N.ptr(K), N.ptr(F), N.ptr(X), s),
+                "rh_system_solve_batch")
+        psd = torch.empty([n * nf, 6, nw], dtype=torch.float64, device=dev)
+        std = torch.empty([n * nf, 6], dtype=torch.float64, device=dev)
+        N.check(N.lib().rh_motion_stats(ctx, n * nf, 1, nw, float(self.fowtList[0].dw), N.ptr(X), N.ptr(psd),
+                                        N.ptr(std), s), "rh_motion_stats")
+        out = {"Xi": X, "iters": res["iters"].view(n, nf), "status": res["status"].view(n, nf),
+               "psd": psd.view(n, nf, 6, nw), "std": std.view(n, nf, 6), "zeta": res["zeta"].view(n, nf, nw)[:, 0]}
+        out["_keep"] = (res, F, arr, K)
+        if host:
+            return {k: v.cpu().numpy() for k, v in out.items() if k != "_keep"}
+        return out
 
 
 def _load_design(input_file):

@@ -148,3 +148,33 @@ def test_farm_seeded_cases_match_oracle():
         r = O.solve_farm(Ts, dict(case), int(T["nIter"]), T["K_array"], float(T["XiStart"]))
         assert [f.iterations for f in m.fowtList] == r["iters"]
         assert rel(Xi, r["Xi"]) < RTOL
+
+
+def test_farm_batch_matches_reference_and_oracle():
+    """C4 batched (Model.analyzeArrayBatch): the golden sea states plus 40 seeded ones in one
+    batch -- every (case, FOWT) drag loop in one launch, the 12-DOF system solves of all cases in
+    another.  Golden cases against the reference run, a sample of the seeded ones against the
+    oracle; identical iteration counts; per-FOWT statistics against the host formula."""
+    T = load_golden("c4_farm")
+    m, Ts = _farm_model(T)
+    gold = golden_cases(T)
+    rng = np.random.default_rng(45)
+    seeded = [dict(wave_spectrum="JONSWAP", wave_period=float(rng.uniform(6, 18)), wave_height=float(rng.uniform(1, 10)),
+                   wave_heading=float(rng.choice([0, 45, 135, 270])), wave_gamma=float(rng.choice([0.0, 2.0])))
+              for _ in range(40)]
+    cases = gold + seeded
+    r = m.analyzeCasesBatch(cases)
+    assert r["Xi"].shape == (len(cases), 12, m.nw)
+    for ic in range(len(gold)):
+        assert list(r["iters"][ic]) == list(T["out_iters"][ic])
+        assert rel(r["Xi"][ic], T["out_Xi"][ic][0]) < RTOL, rel(r["Xi"][ic], T["out_Xi"][ic][0])
+    for j in [0, 7, 23, 39]:
+        o = O.solve_farm(Ts, dict(seeded[j]), int(T["nIter"]), T["K_array"], float(T["XiStart"]))
+        assert list(r["iters"][len(gold) + j]) == o["iters"]
+        assert rel(r["Xi"][len(gold) + j], o["Xi"][0]) < RTOL
+    dw = float(m.fowtList[0].dw)
+    for i in range(2):
+        x = r["Xi"][:, 6 * i:6 * i + 6, :].copy()
+        x[:, 3:] *= 57.29577951308232
+        np.testing.assert_allclose(r["psd"][:, i], 0.5 * np.abs(x) ** 2 / dw, rtol=1e-12, atol=1e-300)
+        np.testing.assert_allclose(r["std"][:, i], np.sqrt(0.5 * np.sum(np.abs(x) ** 2, axis=2)), rtol=1e-12)
