@@ -177,6 +177,10 @@ int rh_group_cases(void);
  * Used by the tests and the kernel-tuning scripts. */
 int rh_set_qtf_waves(rh_ctx* ctx, int waves);
 
+/* QTF pair-sum path of this context: 0 (default) = FP64 MFMA GEMMs when the grid is sorted
+ * (rh_qtf_design.order == 1), 1 = the per-pair kernel k_qtf_pairs (parity cross-checks). */
+int rh_set_qtf_path(rh_ctx* ctx, int path);
+
 /* Unit-amplitude wave kinematics and strip-theory inertial excitation per heading.
  * Replaces the node loops of FOWT.calcHydroExcitation (raft/raft_fowt.py:1098-1124)
  * and helpers.getWaveKin (raft/helpers.py:105-154):
@@ -327,6 +331,8 @@ typedef struct {
   const int* kstart;       /* [nmq+1] ranges in the KAY radius table                    */
   const double* kray;      /* [RH_KR_COUNT][nkr]                                        */
   const rh_c128* hank;     /* [nkr][n2][12]  0.5 (H1_{n-1}(k R) - H1_{n+1}(k R)), n = 0..11 (scipy hankel1) */
+  int order;               /* 1: w2 and k2 strictly increasing (checked by the caller): the pair sum
+                              runs as FP64 MFMA GEMMs (rh_qtf_mfma.hip); 0: the per-pair kernel     */
 } rh_qtf_design;
 
 /* Device workspace (bytes) rh_qtf_slender needs for a design. */
@@ -338,12 +344,13 @@ long long rh_qtf_workspace_bytes(const rh_qtf_design* q);
 int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
                    const double* M66, rh_c128* qtf, void* work, long long work_bytes, rh_stream stream);
 
-/* The upper-triangle rows (w1 <= w2) of one rank of a QTF sharded over nrank devices, no
-   Hermitian fill.  Rows are dealt in snake order: round k gives rank r the row
-   k nrank + (k even ? r : nrank-1-r), which balances the triangle's pairs.  Entries of other
-   rows are not written.  The caller exchanges the shards (raft/parallel.py assemble_qtf: one
-   all_gather over xGMI of every rank's packed upper-triangle pairs, scattered into place by
-   index) and then calls rh_qtf_hermitian_fill. */
+/* The upper-triangle pairs (w1 <= w2) of one rank of a QTF sharded over nrank devices, no
+   Hermitian fill.  The upper triangle is cut into 16 x 16 pair tiles (i1 tile T1 <= i2 tile T2,
+   n2 rounded up to 16), numbered row-major; rank r owns the tiles t with t % nrank == r
+   (raft/parallel.py qtf_tiles).  Entries of other tiles are not written (order == 0: every
+   rank computes the whole triangle, a superset).  The caller exchanges the shards
+   (raft/parallel.py assemble_qtf: one all_gather over xGMI of every rank's packed pairs,
+   scattered into place by index) and then calls rh_qtf_hermitian_fill. */
 int rh_qtf_slender_rows(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
                         const double* M66, int rank, int nrank, rh_c128* qtf, void* work, long long work_bytes,
                         rh_stream stream);

@@ -12,6 +12,7 @@
 
 #include "rh_kernels.hip"   // single translation unit: kernels + their host launchers
 #include "rh_qtf.hip"
+#include "rh_qtf_mfma.hip"
 #include "rh_solve.hip"
 #include "rh_solve_grp.hip"
 
@@ -26,6 +27,7 @@ struct rh_ctx {
   bool force_general = false;   // rh_set_solver(ctx, 1): always use k_solve_cases (parity cross-checks)
   bool no_group = false;        // rh_set_solver(ctx, 2): ignore group_start (one case per workgroup)
   int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
+  bool qtf_direct = false;      // rh_set_qtf_path(ctx, 1): the per-pair kernel even on a sorted grid
 };
 
 namespace {
@@ -133,6 +135,13 @@ int rh_set_qtf_waves(rh_ctx* ctx, int waves) {
   if (waves != 0 && waves != 1 && waves != 2 && waves != 4)
     return fail(RH_EINVAL, "rh_set_qtf_waves: waves=%d (0 = auto, 1, 2 or 4)", waves);
   ctx->qtf_waves = waves;
+  return RH_OK;
+}
+
+int rh_set_qtf_path(rh_ctx* ctx, int path) {
+  if (!ctx) return fail(RH_EINVAL, "rh_set_qtf_path: null context");
+  if (path != 0 && path != 1) return fail(RH_EINVAL, "rh_set_qtf_path: path=%d (0 = MFMA GEMMs when order == 1, 1 = per-pair kernel)", path);
+  ctx->qtf_direct = path == 1;
   return RH_OK;
 }
 
@@ -437,21 +446,39 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
       (q->nkr > 0 && (!q->kray || !q->hank)))
     return fail(RH_EINVAL, "%s: null table", who);
   if (work_bytes < rh_qtf_workspace_bytes(q)) return fail(RH_EINVAL, "%s: workspace too small", who);
+  if (q->order != 0 && q->order != 1) return fail(RH_EINVAL, "%s: order=%d (0 or 1)", who, q->order);
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
-  rh::QtfWork wk;
-  wk.node = (rh_c128*)work;
-  wk.wl = wk.node + (size_t)q->nq * rh::QT_COUNT * q->n2;
-  wk.freq = wk.wl + (size_t)q->nmq * rh::WT_COUNT * q->n2;
-  wk.hinv = wk.freq + (size_t)rh::FT_COUNT * q->n2;
-  wk.kayt = reinterpret_cast<double*>(wk.hinv + (size_t)q->nkr * q->n2 * 12);
-  const int nb = (q->n2 + 63) / 64;
+  rh::QtfWork wk = rh::qtf_carve(*q, work);
+  const bool gemm = q->order == 1 && !ctx->qtf_direct;
+  if (!gemm) wk.R = nullptr;                                 // the table kernels skip the GEMM operands
+  const int n2p = rh::qtf_n2p(*q);
+  const int nb = (n2p + 63) / 64;
   hipLaunchKernelGGL(rh::k_qtf_freq, dim3(nb), dim3(64), 0, s, *q, nw, w, Xi0, M66, wk);
   RH_HIP(hipGetLastError());
-  if (q->nq + q->nmq + q->nkr > 0) {   // node, waterline and KAY tables: one launch
-    hipLaunchKernelGGL(rh::k_qtf_tables, dim3(nb, q->nq + q->nmq + q->nkr), dim3(64), 0, s, *q, wk);
+  const int trows = q->nq + q->nmq + q->nkr + (gemm ? q->nq + rh::qtf_npad(*q) : 0);
+  if (trows > 0) {   // node, waterline and KAY tables (+ GEMM basis and zero K tails): one launch
+    hipLaunchKernelGGL(rh::k_qtf_tables, dim3(nb, trows), dim3(64), 0, s, *q, wk);
     RH_HIP(hipGetLastError());
   }
+  if (gemm) {
+    // w1-side coefficients, then the pair tiles: bilinear + potential GEMMs, then Kim & Yue
+    // and the Hermitian fill (rh_qtf_mfma.hip)
+    hipLaunchKernelGGL(rh::k_qtf_lcoef, dim3(nb, 18 + q->nq + q->nmq), dim3(512), 0, s, *q, wk, M66);
+    RH_HIP(hipGetLastError());
+    const int nt = n2p / 16, ntile = nt * (nt + 1) / 2;
+    const int blocks = (ntile - rank + nrank - 1) / nrank;
+    if (blocks > 0) {
+      hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(6 * blocks), dim3(128), 0, s, *q, wk, qtf, rank, nrank);
+      RH_HIP(hipGetLastError());
+      hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, s, *q, wk, qtf, rank, nrank, mirror);
+      RH_HIP(hipGetLastError());
+    }
+    return RH_OK;
+  }
+  // per-pair kernel; a sharded call computes the whole triangle (a superset of the rank's tiles)
+  rank = 0;
+  nrank = 1;
   const int rows = (q->n2 + nrank - 1) / nrank;     // snake rounds (k_qtf_pairs skips i1 >= n2)
   if (rows > 0) {
     const dim3 grid((q->n2 + rh::kQtfTile - 1) / rh::kQtfTile, rows);

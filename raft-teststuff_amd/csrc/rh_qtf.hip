@@ -19,7 +19,7 @@ namespace rh {
 
 constexpr double kDeg2Rad = 0.017453292519943295;   // raft/helpers.py:27-28
 constexpr int kQtfTile = 64;
-constexpr int kKayT = 6;           // doubles per (KAY row, frequency) in QtfWork::kayt
+constexpr int kKayT = 8;           // doubles per (KAY row, frequency) in QtfWork::kayt
 
 // per-(node, frequency) table fields (complex) [nq][QT_COUNT][n2]
 enum { QT_U = 0, QT_VP = 3, QT_VA = 6, QT_DR = 7, QT_GU = 10, QT_GP = 19, QT_DWDZ = 22, QT_COUNT = 23 };
@@ -28,19 +28,73 @@ enum { WT_ETAR = 0, WT_UD = 1, WT_A = 4, WT_GE = 7, WT_COUNT = 10 };
 // per-frequency fields (complex) [FT_COUNT][n2]
 enum { FT_XI = 0, FT_F1 = 6, FT_OM = 12, FT_COUNT = 15 };
 
+// Bilinear (MFMA) form of the pair sum, rh_qtf_mfma.hip.  Every term of the node, waterline
+// and Pinkster sums is a product of a w1-side and a conj(w2-side) first-order quantity, and
+// the w2-side quantities of a node are linear combinations of a few per-frequency basis
+// functions (8 per node, 3 per waterline member, and the 18 motions X, w X, w^2 X shared by
+// all).  So the upper triangle is Q_d(i1, i2) = sum_k L_d[k](i1) R[k](i2): one complex GEMM
+// per DOF with K = 8 nq + 3 nmq + 18.  Column layout of R / L:
+__host__ __device__ inline int qtf_n2p(const rh_qtf_design& q) { return (q.n2 + 15) & ~15; }
+__host__ __device__ inline int qtf_kb(const rh_qtf_design& q) { return 8 * q.nq + 3 * q.nmq + 18; }
+// K rounded up to 16: the GEMM loops run in groups of four k-steps of four
+__host__ __device__ inline int qtf_kp(const rh_qtf_design& q) { return (qtf_kb(q) + 15) & ~15; }
+__host__ __device__ inline int qtf_kq(const rh_qtf_design& q) { return (2 * q.nq + 15) & ~15; }
+__host__ __device__ inline int qcol_node(int n, int j) { return 8 * n + j; }
+__host__ __device__ inline int qcol_wl(const rh_qtf_design& q, int m, int j) { return 8 * q.nq + 3 * m + j; }
+__host__ __device__ inline int qcol_glob(const rh_qtf_design& q, int g) { return 8 * q.nq + 3 * q.nmq + g; }
+constexpr int kKayK = 24;          // real K of the Kim & Yue dots: 12 complex Hankel orders as (re, im)
+
 struct QtfWork {
   rh_c128* node;   // [nq][QT_COUNT][n2]
   rh_c128* wl;     // [nmq][WT_COUNT][n2]
   rh_c128* freq;   // [FT_COUNT][n2]
   rh_c128* hinv;   // [nkr][n2][12] reciprocals of the Hankel-derivative table q.hank
-  double* kayt;    // [nkr][n2][6] cosh(k R H), sqrt(k R H tanh(k R H)), exp(+-k (z1 + h)), exp(+-k (z2 + h))
-                   //              of every KAY radius row
+  double* kayt;    // [nkr][n2][8] cosh(k R H), sqrt(k R H tanh(k R H)), exp(+-k (z1 + h)), exp(+-k (z2 + h)),
+                   //              k R H / (sqrt(..) cosh(..)), 1 / (k R) of every KAY radius row
+  // MFMA path (n2p = n2 rounded up to 16, zero padded; Kp, Kq rounded up to 16, zero rows)
+  rh_c128* R;      // [Kp][n2p]   conj of the w2-side basis
+  rh_c128* L;      // [6][Kp][n2p] w1-side coefficients per DOF
+  rh_c128* Rp;     // [2][Kq][n2p] second-order-potential channels (+, -): b(w2), k2 b(w2)
+  rh_c128* Lp;     // [2][6][Kq][n2p]
+  double* KA;      // [nkr][24][n2p] Kim & Yue: (Re, Im) of the w1-side coefficients of sum omega_n
+  double* KB;      // [nkr][24][n2p]                                      ... of sum n (n+1) omega_n
+  double* KR;      // [nkr][24][n2p] (Im, Re) of conj(1 / D_n(k2 R))
 };
 
 __host__ __device__ inline size_t qtf_work_elems(const rh_qtf_design& q) {   // complex elements
+  const size_t n2p = (size_t)qtf_n2p(q), kp = (size_t)qtf_kp(q), kq = (size_t)qtf_kq(q);
   return (size_t)q.nq * QT_COUNT * q.n2 + (size_t)q.nmq * WT_COUNT * q.n2 + (size_t)FT_COUNT * q.n2 +
-         (size_t)q.nkr * q.n2 * 12 + ((size_t)q.nkr * q.n2 * kKayT + 1) / 2;
+         (size_t)q.nkr * q.n2 * 12 + ((size_t)q.nkr * q.n2 * kKayT + 1) / 2 +
+         7 * kp * n2p + 14 * kq * n2p + ((size_t)3 * q.nkr * kKayK * n2p + 1) / 2;
 }
+
+// carve the workspace (same order as qtf_work_elems)
+__host__ inline QtfWork qtf_carve(const rh_qtf_design& q, void* work) {
+  QtfWork wk;
+  const size_t n2p = (size_t)qtf_n2p(q), kp = (size_t)qtf_kp(q), kq = (size_t)qtf_kq(q);
+  wk.node = (rh_c128*)work;
+  wk.wl = wk.node + (size_t)q.nq * QT_COUNT * q.n2;
+  wk.freq = wk.wl + (size_t)q.nmq * WT_COUNT * q.n2;
+  wk.hinv = wk.freq + (size_t)FT_COUNT * q.n2;
+  rh_c128* after_kayt = wk.hinv + (size_t)q.nkr * q.n2 * 12 + ((size_t)q.nkr * q.n2 * kKayT + 1) / 2;
+  wk.kayt = reinterpret_cast<double*>(wk.hinv + (size_t)q.nkr * q.n2 * 12);
+  wk.R = after_kayt;
+  wk.L = wk.R + kp * n2p;
+  wk.Rp = wk.L + 6 * kp * n2p;
+  wk.Lp = wk.Rp + 2 * kq * n2p;
+  wk.KA = reinterpret_cast<double*>(wk.Lp + 12 * kq * n2p);
+  wk.KB = wk.KA + (size_t)q.nkr * kKayK * n2p;
+  wk.KR = wk.KB + (size_t)q.nkr * kKayK * n2p;
+  return wk;
+}
+
+// basis writers (rh_qtf_mfma.hip): called by the table kernels below for every (row, f < n2p)
+__device__ void qtf_node_basis(const rh_qtf_design& q, const QtfWork& wk, int f, int n);
+__device__ void qtf_wl_basis(const rh_qtf_design& q, const QtfWork& wk, int f, int m);
+__device__ void qtf_kay_basis(const rh_qtf_design& q, const QtfWork& wk, int f, int ir);
+__device__ void qtf_glob_basis(const rh_qtf_design& q, const QtfWork& wk, int f, const cd* X);
+__host__ __device__ inline int qtf_npad(const rh_qtf_design& q);
+__device__ void qtf_pad_row(const rh_qtf_design& q, const QtfWork& wk, int f, int p);
 
 // Loads of wave-uniform table entries through the constant address space: the backend
 // then issues scalar loads into SGPRs instead of 64 identical vector loads into VGPRs (the
@@ -93,7 +147,10 @@ __global__ __launch_bounds__(64) void k_qtf_freq(rh_qtf_design q, int nw, const 
                                                   QtfWork wk) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   const int n2 = q.n2;
-  if (f >= n2) return;
+  if (f >= n2) {
+    if (wk.R && f < qtf_n2p(q)) qtf_glob_basis(q, wk, f, nullptr);   // zero padding of the GEMM operands
+    return;
+  }
   const double x = q.w2[f];
   cd X[6];
   // np.interp(x, w, Xi0[d], left=0, right=0): j with w[j] <= x < w[j+1]
@@ -134,6 +191,7 @@ __global__ __launch_bounds__(64) void k_qtf_freq(rh_qtf_design q, int nw, const 
   }
 #pragma unroll
   for (int d = 0; d < 3; ++d) st(wk.freq + (size_t)(FT_OM + d) * n2 + f, iw(x, X[3 + d]));
+  if (wk.R) qtf_glob_basis(q, wk, f, X);
 }
 
 // unit-amplitude Airy velocity at a point (raft/helpers.py:105-154, zeta0 = 1)
@@ -324,13 +382,18 @@ __device__ __forceinline__ void qtf_kay_at(const rh_qtf_design& q, const QtfWork
   t[3] = exp(-x1);
   t[4] = exp(x2);
   t[5] = exp(-x2);
+  t[6] = kh / (t[1] * t[0]);          // the MFMA path's separable cc = t6(k1) t6(k2)
+  t[7] = 1.0 / (q.k2[f] * Rr);
 }
 
 // k_qtf_tables: every per-(node | waterline member | KAY row, frequency) table in one launch
 // (blockIdx.y = node, then member, then KAY row), after k_qtf_freq.  One launch instead of
 // three small ones whose grids (a few hundred waves each) left the GPU mostly idle.
 __global__ __launch_bounds__(64) void k_qtf_tables(rh_qtf_design q, QtfWork wk) {
+  // blockIdx.y: node tables, waterline tables, KAY tables; on the MFMA path also the node
+  // GEMM basis and the zero K-tail rows, as rows of their own (more waves in flight)
   const int f = blockIdx.x * 64 + threadIdx.x;
+  const bool basis = wk.R != nullptr && f < qtf_n2p(q);   // MFMA path operands (zero padded to n2p)
   int y = blockIdx.y;
   if (y < q.nq) {
     qtf_nodes_at(q, wk, f, y);
@@ -339,9 +402,23 @@ __global__ __launch_bounds__(64) void k_qtf_tables(rh_qtf_design q, QtfWork wk) 
   y -= q.nq;
   if (y < q.nmq) {
     qtf_wl_at(q, wk, f, y);
+    if (basis) qtf_wl_basis(q, wk, f, y);
     return;
   }
-  qtf_kay_at(q, wk, f, y - q.nmq);
+  y -= q.nmq;
+  if (y < q.nkr) {
+    qtf_kay_at(q, wk, f, y);
+    if (basis) qtf_kay_basis(q, wk, f, y);
+    return;
+  }
+  y -= q.nkr;
+  if (!basis) return;
+  if (y < q.nq) {
+    qtf_node_basis(q, wk, f, y);
+    return;
+  }
+  y -= q.nq;
+  if (y < qtf_npad(q)) qtf_pad_row(q, wk, f, y);
 }
 
 // omega of raft_member.py:1102-1109, 1 / (H'_{n+1}(k1R) conj H'_n(k2R)) - 1 / (H'_n(k1R) conj H'_{n+1}(k2R)),

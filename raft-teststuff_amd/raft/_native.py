@@ -54,7 +54,7 @@ class RhQtfDesign(ctypes.Structure):
     _fields_ = [("n2", ctypes.c_int), ("nq", ctypes.c_int), ("nmq", ctypes.c_int), ("nkr", ctypes.c_int),
                 ("beta", ctypes.c_double), ("depth", ctypes.c_double), ("rho", ctypes.c_double), ("g", ctypes.c_double),
                 ("w2", _p), ("k2", _p), ("qnode", _p), ("qmemb", _p), ("qmstart", _p), ("kstart", _p),
-                ("kray", _p), ("hank", _p)]
+                ("kray", _p), ("hank", _p), ("order", ctypes.c_int)]
 
 
 class NativeError(RuntimeError):
@@ -109,6 +109,7 @@ def lib():
                 "rh_qtf_hermitian_fill": [_p, ctypes.c_int, _p, _p],
                 "rh_set_solver": [_p, ctypes.c_int],
                 "rh_set_qtf_waves": [_p, ctypes.c_int],
+                "rh_set_qtf_path": [_p, ctypes.c_int],
                 "rh_force_2nd": [_p, ctypes.c_int, _p, _p, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p],
             }.items():
                 fn = getattr(L, name)

@@ -6,11 +6,11 @@ One process per GPU, torch.distributed with backend "nccl" (RCCL over xGMI).  Tw
   through rh_solve_cases with no collective inside the drag fixed point (cases are
   independent); the responses are gathered once at the end (all_gather), the "final
   response-spectrum gather" of the north star.  Weak scaling in bench.py.
-* QTF (w1, w2) pairs -- upper-triangle rows dealt in snake order (round k gives rank r row
-  k world + (r if k even else world-1-r)), so every rank gets n2(n2+1)/(2 world) pairs to
-  within one row although rows shorten with i1.  The disjoint
-  row shards are exchanged with one all_gather of each rank's packed upper-triangle pairs
-  (exact copies), then the Hermitian lower triangle is filled on every rank.
+* QTF (w1, w2) pairs -- the upper triangle in 16 x 16 pair tiles (the MFMA tile of
+  rh_qtf_mfma.hip), numbered row-major and dealt round robin, so every rank gets
+  n2(n2+1)/(2 world) pairs to within about a tile row.  The disjoint tile shards are
+  exchanged with one all_gather of each rank's packed upper-triangle pairs (exact copies),
+  then the Hermitian lower triangle is filled on every rank.
 
 The collective helpers take any process group; tests run them with gloo on the CPU.
 """
@@ -36,16 +36,32 @@ def case_shard(n, rank, world):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def qtf_rows(n2, rank, world):
-    """Upper-triangle rows i1 owned by rank (snake deal, as k_qtf_pairs)."""
-    k = np.arange(-(-n2 // world))
-    rows = k * world + np.where(k % 2 == 1, world - 1 - rank, rank)
-    return rows[rows < n2]
+QTF_TILE = 16
+
+
+def qtf_tiles(n2, rank, world):
+    """16 x 16 upper-triangle pair tiles (T1 <= T2) of rank, as rh_qtf_slender_rows deals
+    them: tiles numbered row-major, tile t goes to rank t % world."""
+    nt = -(-n2 // QTF_TILE)
+    allt = [(a, b) for a in range(nt) for b in range(a, nt)]
+    return allt[rank::world]
+
+
+def qtf_pair_flat(n2, tiles):
+    """Flat indices i1 * n2 + i2 of the pairs (i1 <= i2 < n2) of `tiles`, tile by tile."""
+    out = []
+    for a, b in tiles:
+        i1 = np.arange(QTF_TILE * a, min(QTF_TILE * (a + 1), n2))
+        i2 = np.arange(QTF_TILE * b, min(QTF_TILE * (b + 1), n2))
+        I1, I2 = np.meshgrid(i1, i2, indexing="ij")
+        keep = I2 >= I1
+        out.append((I1 * n2 + I2)[keep])
+    return np.concatenate(out) if out else np.zeros(0, int)
 
 
 def qtf_pairs_of(n2, rank, world):
     """Number of (i1 <= i2) pairs rank computes."""
-    return int(sum(n2 - i for i in qtf_rows(n2, rank, world)))
+    return int(len(qtf_pair_flat(n2, qtf_tiles(n2, rank, world))))
 
 
 def gather_cases(local, n_total, group=None):
@@ -78,20 +94,19 @@ _PAIR_INDEX = {}
 
 
 def qtf_pair_index(n2, rank, world, device=None):
-    """Flat indices i1 * n2 + i2 of the upper-triangle pairs (i2 >= i1) of rank's rows, in
-    row order (cached per device)."""
+    """Flat indices i1 * n2 + i2 of the upper-triangle pairs (i2 >= i1) of rank's tiles
+    (cached per device)."""
     import torch
     key = (n2, rank, world, str(device))
     if key not in _PAIR_INDEX:
-        rows = qtf_rows(n2, rank, world)
-        flat = np.concatenate([i1 * n2 + np.arange(i1, n2) for i1 in rows]) if len(rows) else np.zeros(0, int)
+        flat = qtf_pair_flat(n2, qtf_tiles(n2, rank, world))
         _PAIR_INDEX[key] = torch.tensor(flat, dtype=torch.long, device=device)
     return _PAIR_INDEX[key]
 
 
 def assemble_qtf(compute_rows, hermitian_fill, n2, device=None, group=None, on_computed=None):
-    """Row-sharded QTF: compute_rows(out, rank, world) writes the upper-triangle rows of
-    `rank` into the zeroed [n2, n2, 6] complex128 tensor `out`.  The shards are exchanged by
+    """Tile-sharded QTF: compute_rows(out, rank, world) writes the upper-triangle pairs of
+    `rank`'s tiles (qtf_tiles) into the zeroed [n2, n2, 6] complex128 tensor `out`.  The shards are exchanged by
     ONE all_gather of each rank's packed upper-triangle pairs (about n2^2/2 / world pairs x
     96 B, padded to the largest shard) and scattered into place; hermitian_fill(out) then
     mirrors the lower triangle.  Pure copies, so the result is bitwise the single-device

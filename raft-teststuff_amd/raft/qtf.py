@@ -137,6 +137,9 @@ class QtfDevice:
         self.qmstart = torch.tensor(t["qmstart"], dtype=torch.int32, device=self.dev)
         self.kstart = torch.tensor(t["kstart"], dtype=torch.int32, device=self.dev)
         self.rho, self.g, self.h = t["rho"], t["g"], t["h"]
+        # the MFMA pair path needs the upper triangle to be i2 >= i1 and nk = k2 - k1
+        w2a, k2a = np.asarray(w2, dtype=float), np.asarray(k2, dtype=float)
+        self.order = int(bool(np.all(np.diff(w2a) > 0) and np.all(np.diff(k2a) > 0)))
         self.struct_ = self.struct()
         nbytes = N.lib().rh_qtf_workspace_bytes(ctypes.byref(self.struct_))
         self.work = torch.empty(int(nbytes) // 16 + 1, dtype=torch.complex128, device=self.dev)
@@ -149,6 +152,7 @@ class QtfDevice:
         q.w2, q.k2 = N.ptr(self.w2), N.ptr(self.k2)
         q.qnode, q.qmemb, q.qmstart, q.kstart = N.ptr(self.qnode), N.ptr(self.qmemb), N.ptr(self.qmstart), N.ptr(self.kstart)
         q.kray, q.hank = N.ptr(self.kray), N.ptr(self.hank)
+        q.order = self.order
         return q
 
     def qtf(self, w, Xi0, M66, out=None, group=None, on_computed=None):
@@ -176,7 +180,7 @@ class QtfDevice:
 
 
     def qtf_rows(self, w, Xi0, M66, out, rank, nrank):
-        """rh_qtf_slender_rows: the upper-triangle rows of `rank` (snake deal, parallel.qtf_rows) into `out`."""
+        """rh_qtf_slender_rows: the upper-triangle pair tiles of `rank` (parallel.qtf_tiles) into `out`."""
         N.check(N.lib().rh_qtf_slender_rows(N.context(self.dev_index), ctypes.byref(self.struct_), int(w.numel()),
                                             N.ptr(w), N.ptr(Xi0), N.ptr(M66), int(rank), int(nrank), N.ptr(out),
                                             N.ptr(self.work), ctypes.c_longlong(self.work_bytes),

@@ -98,6 +98,44 @@ def test_qtf_full_size_400_grid(T):
     np.testing.assert_array_equal(f.qtf, q1)
 
 
+@pytest.mark.parametrize("beta_deg", [0.0, 30.0])
+@pytest.mark.parametrize("grid", ["golden42", "full400"])
+def test_mfma_path_matches_per_pair_kernel(T, beta_deg, grid):
+    """The default QTF path on a sorted grid (the pair sum as FP64 MFMA GEMMs, rh_qtf_mfma.hip)
+    against the per-pair kernel k_qtf_pairs (rh_set_qtf_path(ctx, 1)): the same arithmetic
+    reassociated, so they agree far inside the 1e-9 parity bar (1e-12 normwise, elementwise
+    to 1e-12 of the largest entry), with the moving body and fixed, at 0 and 30 degrees (Q1)."""
+    import torch
+    from raft import _native as N
+    from raft.hydro_math import wave_numbers
+    from raft.qtf import QtfDevice
+    m, f = make(T)
+    dd = f.device_design()
+    M66 = torch.tensor(f.M_struc, dtype=torch.float64, device=dd.device).contiguous()
+    if grid == "golden42":
+        w2, k2 = T["w1_2nd"], T["k1_2nd"]
+    else:
+        w2 = np.arange(0.04, 0.35 + 0.5 * 0.04, 0.000825) * 2 * np.pi
+        k2 = wave_numbers(w2, f.depth)
+    qd = QtfDevice(f, w2, k2, np.deg2rad(beta_deg), 0)
+    assert qd.order == 1
+    ctx = N.context(0)
+    for X0 in (T["out_Xi0"], np.zeros_like(T["out_Xi0"])):
+        X = torch.tensor(X0, dtype=torch.complex128, device=dd.device)
+        out = []
+        try:
+            for path in (0, 1):
+                N.check(N.lib().rh_set_qtf_path(ctx, path), "rh_set_qtf_path")
+                out.append(qd.qtf(dd.w, X, M66).cpu().numpy())
+        finally:
+            N.check(N.lib().rh_set_qtf_path(ctx, 0), "rh_set_qtf_path")
+        a, b = out
+        assert rel(a, b) < 1e-12, rel(a, b)
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-12 * np.abs(b).max())
+        i, j = np.tril_indices(len(w2), -1)
+        np.testing.assert_array_equal(a[i, j], np.conj(a[j, i]))
+
+
 def test_fixed_body_qtf_matches_oracle(T):
     """Xi0=None (fixed body) against the oracle at the n2=42 grid."""
     from oracle import qtf_oracle as Q
@@ -140,8 +178,9 @@ def test_qtf_text_outputs(T, tmp_path):
     assert f2.shape == (len(T["w"]), 7)
 
 
-def test_row_sharded_qtf_equals_single_device(T):
-    """rh_qtf_slender_rows over 3 simulated ranks + sum + rh_qtf_hermitian_fill reproduces
+def test_tile_sharded_qtf_equals_single_device(T):
+    """rh_qtf_slender_rows over 3 simulated ranks (tiles dealt round robin) + sum +
+    rh_qtf_hermitian_fill reproduces
     rh_qtf_slender bit for bit (the multi-GPU exchange of raft/parallel.py)."""
     import torch
     m, f = make(T)

@@ -38,7 +38,7 @@ def _worker(rank, world, port, fn, args):
 
 
 def test_case_shard_partitions_every_case_once():
-    from raft.parallel import case_shard, qtf_pairs_of, qtf_rows
+    from raft.parallel import case_shard, qtf_pair_flat, qtf_pairs_of, qtf_tiles
     for n in [1, 7, 512, 10000]:
         for world in [1, 2, 3, 8]:
             blocks = [case_shard(n, r, world) for r in range(world)]
@@ -46,13 +46,16 @@ def test_case_shard_partitions_every_case_once():
             assert all(blocks[i][1] == blocks[i + 1][0] for i in range(world - 1))
             sizes = [b - a for a, b in blocks]
             assert max(sizes) - min(sizes) <= 1
-    for n2 in [42, 400]:
+    for n2 in [42, 400, 401]:
+        iu = np.triu_indices(n2)
+        every = np.sort(iu[0] * n2 + iu[1])
         for world in [1, 2, 8]:
-            rows = np.concatenate([qtf_rows(n2, r, world) for r in range(world)])
-            assert sorted(rows.tolist()) == list(range(n2))
+            flat = np.concatenate([qtf_pair_flat(n2, qtf_tiles(n2, r, world)) for r in range(world)])
+            np.testing.assert_array_equal(np.sort(flat), every)   # every upper pair exactly once
             pairs = [qtf_pairs_of(n2, r, world) for r in range(world)]
             assert sum(pairs) == n2 * (n2 + 1) // 2
-            assert max(pairs) - min(pairs) <= n2                 # snake deal: within one row
+            nt = -(-n2 // 16)
+            assert max(pairs) - min(pairs) <= 16 * 16 * -(-nt // world) + 256   # about a tile row
 
 
 def test_sweep_shard_covers_every_case_and_its_design():
@@ -117,15 +120,15 @@ def test_case_gather_world2():
 
 def _qtf_check(rank, world):
     from oracle import qtf_oracle as Q
-    from raft.parallel import assemble_qtf, qtf_rows
+    from raft.parallel import assemble_qtf, qtf_pair_flat, qtf_tiles
     T = load_golden("c3_qtf")
     ref = Q.qtf_slender(T, T["out_Xi0"], T["w1_2nd"], T["k1_2nd"], 0.0)[:, :, 0, :]
     n2 = len(T["w1_2nd"])
     iu = np.triu(np.ones([n2, n2], dtype=bool))
 
-    def rows(out, r, w):                      # stand-in for rh_qtf_slender_rows: upper rows of rank r
-        for i1 in qtf_rows(n2, r, w):
-            out[i1, i1:] = torch.tensor(ref[i1, i1:])
+    def rows(out, r, w):                      # stand-in for rh_qtf_slender_rows: the pairs of rank r's tiles
+        flat = qtf_pair_flat(n2, qtf_tiles(n2, r, w))
+        out.view(n2 * n2, 6)[torch.tensor(flat)] = torch.tensor(ref.reshape(n2 * n2, 6)[flat])
 
     def fill(out):                            # same semantics as k_qtf_fill
         x = out.numpy()

@@ -13,6 +13,15 @@ CSRC = os.path.join(ROOT, "raft-teststuff_amd", "csrc")
 EDITS = {
     "qNoKay": [("rh_qtf.hip", "    if (qm(q, RH_QM_KAY, m) != 0.0) {", "    if (qm(q, RH_QM_KAY, m) == 12345.0) {")],
     "qNoNodes": [("rh_qtf.hip", "    for (int n = n0; n < n1; ++n) {\n      const rh_c128* T = wk.node", "    for (int n = n0; n < n0; ++n) {\n      const rh_c128* T = wk.node")],
+    # MFMA QTF path (rh_qtf_mfma.hip) ablations
+    "kNoEpi": [("rh_qtf_mfma.hip", "        if (wl) {   // waterline term (:1133-1149): Re(-i kap A) = kap Im(A)\n          sre = kap * ca[r];\n        } else {",
+                "        if (true) {\n          sre = kap * (ca[r] + cbk[r]);\n        } else {")],
+    "kNoMfma": [("rh_qtf_mfma.hip", "          ca = mfma64(va[s], vr[s], ca);\n          cbk = mfma64(vb[s], vr[s], cbk);",
+                 "          ca[0] += va[s] * vr[s];\n          cbk[0] += vb[s] * vr[s];")],
+    "kNoFinal": [("rh_qtf_mfma.hip", "  if (a1 >= n2 || a2 >= n2 || a2 < a1) return;", "  if (a1 >= -1) return;")],
+    "kNoRows": [("rh_qtf_mfma.hip", "    for (int ir = rlo; ir < rhi; ++ir) {", "    for (int ir = rlo; ir < rlo; ++ir) {")],
+    "gNoPot": [("rh_qtf_mfma.hip", "  cgemm_steps(wk.Lp + ", "  if (nk < 0) cgemm_steps(wk.Lp + ")],
+    "gNoMain": [("rh_qtf_mfma.hip", "  if (nk > 0)\n    cgemm_steps(", "  if (nk < 0)\n    cgemm_steps(")],
     "prof": [],          # unmodified source built with -DRH_PROF (phase cycle counters)
     "noLU": [("      my_sing |= !lu_solve<6>(Z, F);", "      F[0] = add(F[0], Z[0][0]);")],
     "stXo": [("        st_nt(Xo + c * nw + b, x);", "        st(Xo + c * nw + b, x);")],
