@@ -469,7 +469,7 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
     const int nt = n2p / 16, ntile = nt * (nt + 1) / 2;
     const int blocks = (ntile - rank + nrank - 1) / nrank;
     if (blocks > 0) {
-      hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(6 * blocks), dim3(128), 0, s, *q, wk, qtf, rank, nrank);
+      hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(2 * blocks), dim3(384), 0, s, *q, wk, qtf, rank, nrank);
       RH_HIP(hipGetLastError());
       hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, s, *q, wk, qtf, rank, nrank, mirror);
       RH_HIP(hipGetLastError());

@@ -753,12 +753,14 @@ __global__ __launch_bounds__(512) void k_qtf_lcoef(rh_qtf_design q, QtfWork wk, 
 // pair tiles: 16 (i1) x 16 (i2), upper-triangle tiles in row-major order, dealt round robin
 // over the ranks (tile t of the order goes to rank t mod nrank)
 // ---------------------------------------------------------------------------------------
-// Complex GEMM steps k0 .. k0 + nsteps of one 16 x 16 tile: A[m = i1][k] (lane l holds
-// A[l & 15][4 s + (l >> 4)]), B[k][n = i2] (B[4 s + (l >> 4)][l & 15]); four real MFMAs per step
-// into four accumulators.  nsteps is a multiple of 4: the loads of the next four steps are in
-// flight while the MFMAs of the current four run.
+// Complex GEMM steps of one 16 x 16 tile: A[m = i1][k] (lane l holds A[l & 15][4 s + (l >> 4)]),
+// B[k][n = i2] (B[4 s + (l >> 4)][l & 15]).  Three real MFMAs per step (Gauss):
+// P1 = Ar Br, P2 = Ai Bi, P3 = (Ar + Ai)(Br + Bi); Re = P1 - P2, Im = P3 - P1 - P2.  nsteps is a
+// multiple of 4: the loads of the next four steps are in flight while the MFMAs of the current
+// four run.
 __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const rh_c128* __restrict__ B, size_t step,
-                                            int nsteps, d4& ar, d4& br, d4& ai, d4& bi) {
+                                            int nsteps, d4& p1, d4& p2, d4& p3) {
+  d4 q1 = {0, 0, 0, 0}, q2 = q1, q3 = q1;
   cd a[4], b[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -777,11 +779,13 @@ __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ar = mfma64(a[j].r, b[j].r, ar);
-      br = mfma64(-a[j].i, b[j].i, br);
-      ai = mfma64(a[j].r, b[j].i, ai);
-      bi = mfma64(a[j].i, b[j].r, bi);
+    for (int j = 0; j < 4; j += 2) {   // two accumulator sets: six independent MFMA chains
+      p1 = mfma64(a[j].r, b[j].r, p1);
+      p2 = mfma64(a[j].i, b[j].i, p2);
+      p3 = mfma64(a[j].r + a[j].i, b[j].r + b[j].i, p3);
+      q1 = mfma64(a[j + 1].r, b[j + 1].r, q1);
+      q2 = mfma64(a[j + 1].i, b[j + 1].i, q2);
+      q3 = mfma64(a[j + 1].r + a[j + 1].i, b[j + 1].r + b[j + 1].i, q3);
     }
     if (more) {
 #pragma unroll
@@ -791,21 +795,28 @@ __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const
       }
     }
   }
+  p1 += q1;
+  p2 += q2;
+  p3 += q3;
 }
 
-// Q_d over the bilinear terms and the two potential channels for one (tile, DOF d).
-// Workgroup = 2 waves: wave 0 takes the first half of K and channel +, wave 1 the second half
-// and channel -; wave 1's partial sums reach wave 0 through LDS.  Blocks are (tile, d) pairs,
-// remapped so that an XCD works on a contiguous run of tiles (their L rows stay in its L2).
-__global__ __launch_bounds__(128) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf, int rank,
+// Q_d over the bilinear terms and the two potential channels for one tile and three DOFs.
+// Workgroup = 6 waves: wave w takes DOF 3 dg + (w % 3) (dg = the block's DOF half) and half
+// w / 3 of the work: the first half of K and channel +, or the second half and channel -
+// (the three waves of a half share the R tile through L1); the second half's partial sums
+// reach the first through LDS.  Blocks are (tile, DOF half) pairs, remapped so that an XCD
+// works on a contiguous run of tiles (their L rows stay in its L2).
+__global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf, int rank,
                                                   int nrank) {
-  __shared__ double part[16][64];
+  __shared__ double part[3][16][64];
+  __shared__ double pscal[4][256];   // per pair: aux2 (w1 - w2) alpha+, ... alpha- (complex)
   const int lane = (int)threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int half = w / 3, dl = w % 3;
   const int n2 = q.n2, n2p = qtf_n2p(q), nt = n2p / 16, kp = qtf_kp(q), kq = qtf_kq(q);
   const int slot = xcd_remap((int)blockIdx.x, (int)gridDim.x);
-  const int d = slot % 6;
-  int T1 = 0, t = rank + nrank * (slot / 6);
+  const int d = 3 * (slot & 1) + dl;
+  int T1 = 0, t = rank + nrank * (slot >> 1);
   while (t >= nt - T1) {   // block-uniform
     t -= nt - T1;
     ++T1;
@@ -815,51 +826,63 @@ __global__ __launch_bounds__(128) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
   const int i1b = 16 * T1, i2b = 16 * T2;
   const size_t step = (size_t)4 * n2p;
   const int ns = kp / 4, ns0 = 4 * ((ns / 4 + 1) / 2);
-  const int k0 = wv == 0 ? 0 : ns0, nk = wv == 0 ? ns0 : ns - ns0;
-  d4 ar = {0, 0, 0, 0}, br = ar, ai = ar, bi = ar;
+  const int k0 = half == 0 ? 0 : ns0, nk = half == 0 ? ns0 : ns - ns0;
+  d4 p1 = {0, 0, 0, 0}, p2 = p1, p3 = p1;
   if (nk > 0)
     cgemm_steps(wk.L + ((size_t)d * kp + 4 * k0 + kr) * n2p + i1b + mr, wk.R + ((size_t)4 * k0 + kr) * n2p + i2b + mr,
-                step, nk, ar, br, ai, bi);
-  d4 pr = {0, 0, 0, 0}, qr = pr, pi = pr, qi = pr;   // channel c = wv
-  cgemm_steps(wk.Lp + (((size_t)wv * 6 + d) * kq + kr) * n2p + i1b + mr, wk.Rp + ((size_t)wv * kq + kr) * n2p + i2b + mr,
-              step, kq / 4, pr, qr, pi, qi);
-  const d4 mre = ar + br, mim = ai + bi, cre = pr + qr, cim = pi + qi;
-  if (wv == 1) {
+                step, nk, p1, p2, p3);
+  d4 c1 = {0, 0, 0, 0}, c2 = c1, c3 = c1;   // potential channel c = half
+  cgemm_steps(wk.Lp + (((size_t)half * 6 + d) * kq + kr) * n2p + i1b + mr,
+              wk.Rp + ((size_t)half * kq + kr) * n2p + i2b + mr, step, kq / 4, c1, c2, c3);
+  const d4 mre = p1 - p2, mim = p3 - p1 - p2, cre = c1 - c2, cim = c3 - c1 - c2;
+  const double h = q.depth, g = q.g, bt = q.beta * kDeg2Rad, cb = cos(bt), sb = sin(bt);
+  if (half == 1) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      part[r][lane] = mre[r];
-      part[4 + r][lane] = mim[r];
-      part[8 + r][lane] = cre[r];
-      part[12 + r][lane] = cim[r];
+      part[dl][r][lane] = mre[r];
+      part[dl][4 + r][lane] = mim[r];
+      part[dl][8 + r][lane] = cre[r];
+      part[dl][12 + r][lane] = cim[r];
+    }
+    // the pair scalars of the second-order potential (raft/helpers.py:254-291), once per pair:
+    // aux2 (w1 - w2) alpha+ and aux2 (w1 - w2) alpha-, with
+    // cosh(nk (z+h)) / cosh(nk h) = alpha+ e^{nk z} + alpha- e^{-nk z}
+    for (int e = (int)threadIdx.x - 192; e < 256; e += 192) {
+      const int i1 = min(i1b + (e >> 4), n2 - 1), i2 = min(i2b + (e & 15), n2 - 1);
+      const double w1 = q.w2[i1], k1 = q.k2[i1], w2 = q.w2[i2], k2 = q.k2[i2];
+      cd sp = mk(0, 0), sm = mk(0, 0);
+      if ((w1 != w2) && (k1 > 0) && (k2 > 0)) {
+        const double kx = k1 * cb - k2 * cb, ky = k1 * sb - k2 * sb;
+        const double nk = sqrt(kx * kx + ky * ky);
+        const double t1 = tanh(k1 * h), t2 = tanh(k2 * h), tnh = tanh(nk * h);
+        const double den12 = (w1 - w2) * (w1 - w2) / g - nk * tnh;
+        const double den21 = (w2 - w1) * (w2 - w1) / g - nk * tnh;
+        const double n12 = (k1 * k1) * (1 - t1 * t1) - 2 * k1 * k2 * (1 + t1 * t2);
+        const double n21 = (k2 * k2) * (1 - t2 * t2) - 2 * k2 * k1 * (1 + t2 * t1);
+        const cd g12 = scl(mk(0, -g / (2 * w1)), n12 / den12);
+        const cd g21 = scl(mk(0, -g / (2 * w2)), n21 / den21);
+        const cd a2w = scl(scl(add(g21, cconj(g12)), 0.5), w1 - w2);
+        const double e2 = exp(-2.0 * nk * h), ap = 1.0 / (1.0 + e2), am = e2 * ap;
+        sp = scl(a2w, ap);
+        sm = scl(a2w, am);
+      }
+      pscal[0][e] = sp.r;
+      pscal[1][e] = sp.i;
+      pscal[2][e] = sm.r;
+      pscal[3][e] = sm.i;
     }
   }
   __syncthreads();
-  if (wv == 1) return;
-  const double h = q.depth, g = q.g, bt = q.beta * kDeg2Rad, cb = cos(bt), sb = sin(bt);
+  if (half == 1) return;
   const int i2 = i2b + mr;
-  const double w2 = i2 < n2 ? q.w2[i2] : 0.0, k2 = i2 < n2 ? q.k2[i2] : 0.0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i1 = i1b + kr + 4 * r;
     if (i1 >= n2 || i2 >= n2 || i2 < i1) continue;
-    cd Qd = mk(mre[r] + part[r][lane], mim[r] + part[4 + r][lane]);
-    const double w1 = q.w2[i1], k1 = q.k2[i1];
-    if ((w1 != w2) && (k1 > 0) && (k2 > 0)) {   // second-order potential (raft/helpers.py:254-291)
-      const double kx = k1 * cb - k2 * cb, ky = k1 * sb - k2 * sb;
-      const double nk = sqrt(kx * kx + ky * ky);
-      const double t1 = tanh(k1 * h), t2 = tanh(k2 * h), tnh = tanh(nk * h);
-      const double den12 = (w1 - w2) * (w1 - w2) / g - nk * tnh;
-      const double den21 = (w2 - w1) * (w2 - w1) / g - nk * tnh;
-      const double n12 = (k1 * k1) * (1 - t1 * t1) - 2 * k1 * k2 * (1 + t1 * t2);
-      const double n21 = (k2 * k2) * (1 - t2 * t2) - 2 * k2 * k1 * (1 + t2 * t1);
-      const cd g12 = scl(mk(0, -g / (2 * w1)), n12 / den12);
-      const cd g21 = scl(mk(0, -g / (2 * w2)), n21 / den21);
-      const cd aux2 = scl(add(g21, cconj(g12)), 0.5);
-      // cosh(nk (z+h)) / cosh(nk h) = alpha+ e^{nk z} + alpha- e^{-nk z}
-      const double e2 = exp(-2.0 * nk * h), ap = 1.0 / (1.0 + e2), am = e2 * ap;
-      const cd P = add(scl(mk(cre[r], cim[r]), ap), scl(mk(part[8 + r][lane], part[12 + r][lane]), am));
-      Qd = add(Qd, mul(scl(aux2, w1 - w2), P));
-    }
+    const int e = (kr + 4 * r) * 16 + mr;
+    const cd Pp = mk(cre[r], cim[r]), Pm = mk(part[dl][8 + r][lane], part[dl][12 + r][lane]);
+    const cd Qd = add(mk(mre[r] + part[dl][r][lane], mim[r] + part[dl][4 + r][lane]),
+                      add(mul(mk(pscal[0][e], pscal[1][e]), Pp), mul(mk(pscal[2][e], pscal[3][e]), Pm)));
     st(qtf + ((size_t)i1 * n2 + i2) * 6 + d, Qd);
   }
 }

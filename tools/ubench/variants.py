@@ -20,6 +20,12 @@ EDITS = {
                  "          ca[0] += va[s] * vr[s];\n          cbk[0] += vb[s] * vr[s];")],
     "kNoFinal": [("rh_qtf_mfma.hip", "  if (a1 >= n2 || a2 >= n2 || a2 < a1) return;", "  if (a1 >= -1) return;")],
     "kNoRows": [("rh_qtf_mfma.hip", "    for (int ir = rlo; ir < rhi; ++ir) {", "    for (int ir = rlo; ir < rlo; ++ir) {")],
+    "gNoMfmaOps": [("rh_qtf_mfma.hip", "      p1 = mfma64(a[j].r, b[j].r, p1);\n      p2 = mfma64(a[j].i, b[j].i, p2);\n      p3 = mfma64(a[j].r + a[j].i, b[j].r + b[j].i, p3);",
+                    "      p1[0] += a[j].r * b[j].r;\n      p2[0] += a[j].i * b[j].i;\n      p3[0] += a[j].r * b[j].i;")],
+    "gFixedLoads": [("rh_qtf_mfma.hip", "        an[j] = ld(A + (s + 4 + j) * step);\n        bn[j] = ld(B + (s + 4 + j) * step);",
+                     "        an[j] = ld(A + j * step);\n        bn[j] = ld(B + j * step);")],
+    "gNoEpi": [("rh_qtf_mfma.hip", "    if ((w1 != w2) && (k1 > 0) && (k2 > 0)) {   // second-order potential (raft/helpers.py:254-291)\n      const double kx = k1 * cb - k2 * cb",
+                "    if (w1 < -1.0) {\n      const double kx = k1 * cb - k2 * cb")],
     "gNoPot": [("rh_qtf_mfma.hip", "  cgemm_steps(wk.Lp + ", "  if (nk < 0) cgemm_steps(wk.Lp + ")],
     "gNoMain": [("rh_qtf_mfma.hip", "  if (nk > 0)\n    cgemm_steps(", "  if (nk < 0)\n    cgemm_steps(")],
     "prof": [],          # unmodified source built with -DRH_PROF (phase cycle counters)
