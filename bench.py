@@ -26,20 +26,25 @@ NCASE = 512
 PEAK_FP64 = 78.6e12   # MI355X FP64 dense peak (vector = matrix rate), FLOP/s
 # HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950
 # correction of MI355X_MICROARCH.md + WRITE_SIZE), written by tools/pmc_summary.py
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v12", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_v2", "pmc_summary.json")
 
 
-def pmc_traffic(kernel):
-    """HBM traffic (bytes per launch) of `kernel` from PMC_SUMMARY, or None."""
+def pmc_traffic(*kernels):
+    """HBM traffic (bytes per call) summed over the kernels named in `kernels` (one launch
+    each per call) from PMC_SUMMARY, or None if any of them is missing."""
     try:
         with open(PMC_SUMMARY) as fh:
             d = json.load(fh)
     except (OSError, ValueError):
         return None
-    for name, v in d.items():
-        if kernel in name and "hbm_read_bytes_corrected" in v and "hbm_write_bytes" in v:
-            return v["hbm_read_bytes_corrected"] + v["hbm_write_bytes"]
-    return None
+    total = 0.0
+    for kernel in kernels:
+        hit = [v for name, v in d.items()
+               if kernel in name and "hbm_read_bytes_corrected" in v and "hbm_write_bytes" in v]
+        if not hit:
+            return None
+        total += hit[0]["hbm_read_bytes_corrected"] + hit[0]["hbm_write_bytes"]
+    return total
 
 
 L2_PEAK = 34.5e12     # MI355X aggregate L2 bandwidth, B/s (MI355X_MICROARCH.md, L2 per XCD)
@@ -209,9 +214,10 @@ def build_qtf(device):
 
 
 def bench_qtf(device, steps, warmup, world, rank, dist):
-    """C3 throughput: one 400x400 QTF per step (upper triangle computed, Hermitian fill), rows
-    sharded over the ranks with one all-gather of packed pairs.  end_to_end_ms: a cold QTF
-    including the per-(design, grid, heading) host tables (hankel1) and their upload."""
+    """C3 throughput: one 400x400 QTF per step (upper triangle computed, Hermitian fill), 16 x 16
+    pair tiles sharded over the ranks with one all-gather of packed pairs.  end_to_end_ms: a
+    cold QTF including the per-(design, grid, heading) tables (host geometry, device Hankel
+    table) and their upload."""
     import torch
     from raft.qtf import QtfDevice
     T, f, dd, X, M66, w2, k2 = build_qtf(device)
@@ -261,13 +267,16 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
            "full_grid_equiv_per_s": n2 * n2 * steps / dt_max,
            "config": {"workload": "C3: OC4semi-RAFT_QTF slender-body QTF, 400x400 (w1,w2) grid, heading 0",
                       "submerged_nodes": qd.nq, "kay_intervals": nkay, "waterline_members": nwl,
-                      "parallelism": f"row-sharded x{world} + all-gather of packed pairs"},
-           "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
-                        "frac": achieved / PEAK_FP64, "traffic": pmc_traffic("k_qtf_pairs"),
-                        "kernel": "rh_qtf_slender%s (table + pair launches of this rank)" % ("_rows" if world > 1 else ""),
+                      "parallelism": f"tile-sharded x{world} + all-gather of packed pairs"},
+           "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
+                        "frac": achieved / PEAK_FP64,
+                        "traffic": pmc_traffic("k_qtf_freq", "k_qtf_tables", "k_qtf_lcoef", "k_qtf_gemm", "k_qtf_kay"),
+                        "kernel": "rh_qtf_slender%s: k_qtf_freq, k_qtf_tables, k_qtf_lcoef, k_qtf_gemm, k_qtf_kay "
+                                  "(every launch of a QTF on this rank)" % ("_rows" if world > 1 else ""),
                         "kernel_ms": ms, "flops_per_pair": fpp, "pairs_this_rank": mine,
-                        "note": "FP64 VALU (no MFMA, DESIGN.md §4); algorithmic FLOPs from SURVEY.md §8(d) over "
-                                "this rank's pairs; traffic = HBM bytes per k_qtf_pairs launch (PMC)"}}
+                        "note": "FP64: the pair sum as MFMA GEMMs (k_qtf_gemm) + VALU Kim & Yue epilogue (DESIGN.md "
+                                "§4); peak = MI355X FP64 dense (matrix = vector rate); algorithmic FLOPs from SURVEY.md "
+                                "§8(d) over this rank's pairs; traffic = HBM bytes of all five launches of a QTF (PMC)"}}
     return out
 
 

@@ -355,6 +355,12 @@ int rh_qtf_slender_rows(rh_ctx* ctx, const rh_qtf_design* q, int nw, const doubl
                         const double* M66, int rank, int nrank, rh_c128* qtf, void* work, long long work_bytes,
                         rh_stream stream);
 
+/* The Kim & Yue Hankel table of rh_qtf_design.hank on the device: hank[ir][f][n] =
+ * 0.5 (H1_{n-1}(x) - H1_{n+1}(x)), x = k2[f] R[ir], n = 0..11 -- the values the reference takes
+ * from scipy.special.hankel1 (raft/raft_member.py:1104-1107).  R: [nkr] radii (the RH_KR_R row
+ * of the radius table).  J by series / Miller recurrence, Y by forward recurrence from y0, y1. */
+int rh_qtf_hankel(rh_ctx* ctx, int n2, const double* k2, int nkr, const double* R, rh_c128* hank, rh_stream stream);
+
 /* qtf[i2][i1] = conj(qtf[i1][i2]) for i2 > i1 (raft/raft_fowt.py:1639-1640). */
 int rh_qtf_hermitian_fill(rh_ctx* ctx, int n2, rh_c128* qtf, rh_stream stream);
 

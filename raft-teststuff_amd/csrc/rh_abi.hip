@@ -513,6 +513,15 @@ int rh_qtf_slender_rows(rh_ctx* ctx, const rh_qtf_design* q, int nw, const doubl
   return qtf_launch(ctx, q, nw, w, Xi0, M66, rank, nrank, 0, qtf, work, work_bytes, stream, "rh_qtf_slender_rows");
 }
 
+int rh_qtf_hankel(rh_ctx* ctx, int n2, const double* k2, int nkr, const double* R, rh_c128* hank, rh_stream stream) {
+  if (!ctx || n2 < 1 || nkr < 0 || (nkr > 0 && (!k2 || !R || !hank))) return fail(RH_EINVAL, "rh_qtf_hankel: bad argument");
+  if (nkr == 0) return RH_OK;
+  RH_HIP(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(rh::k_qtf_hankel, dim3((n2 + 63) / 64, nkr), dim3(64), 0, (hipStream_t)stream, n2, k2, nkr, R, hank);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
 int rh_qtf_hermitian_fill(rh_ctx* ctx, int n2, rh_c128* qtf, rh_stream stream) {
   if (!ctx || !qtf || n2 < 1) return fail(RH_EINVAL, "rh_qtf_hermitian_fill: bad argument");
   RH_HIP(hipSetDevice(ctx->device));

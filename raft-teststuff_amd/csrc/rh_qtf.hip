@@ -15,6 +15,8 @@
 // Layout: every per-frequency table is frequency-contiguous, so the lanes of a wave (64
 // consecutive w2 of one w1 row) read coalesced rows for the w2 side and a broadcast for the
 // w1 side.
+#include "rh_bessel.h"
+
 namespace rh {
 
 constexpr double kDeg2Rad = 0.017453292519943295;   // raft/helpers.py:27-28
@@ -384,6 +386,22 @@ __device__ __forceinline__ void qtf_kay_at(const rh_qtf_design& q, const QtfWork
   t[5] = exp(-x2);
   t[6] = kh / (t[1] * t[0]);          // the MFMA path's separable cc = t6(k1) t6(k2)
   t[7] = 1.0 / (q.k2[f] * Rr);
+}
+
+// Bessel J_n, Y_n (n = 0..12) without library calls: rh_bessel.h (checked against scipy on the
+// CPU by tests/test_bessel.py and on the device by tests/test_gpu_qtf.py)
+// D_n(k R) = 0.5 (H1_{n-1}(k R) - H1_{n+1}(k R)), n = 0..11, per (row, frequency); H1_{-1} = -H1_1
+__global__ __launch_bounds__(64) void k_qtf_hankel(int n2, const double* __restrict__ k2, int nkr,
+                                                   const double* __restrict__ R, rh_c128* __restrict__ hank) {
+  const int f = blockIdx.x * 64 + threadIdx.x, ir = blockIdx.y;
+  if (f >= n2 || ir >= nkr) return;
+  const double x = k2[f] * R[ir];
+  double J[13], Y[13];
+  bessel_jy12(x, J, Y);
+  rh_c128* o = hank + ((size_t)ir * n2 + f) * 12;
+  st(o, mk(-J[1], -Y[1]));
+#pragma unroll
+  for (int n = 1; n < 12; ++n) st(o + n, mk(0.5 * (J[n - 1] - J[n + 1]), 0.5 * (Y[n - 1] - Y[n + 1])));
 }
 
 // k_qtf_tables: every per-(node | waterline member | KAY row, frequency) table in one launch

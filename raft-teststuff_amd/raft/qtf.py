@@ -1,10 +1,10 @@
 """Device tables for the slender-body QTF.
 
 Per design, per second-order grid and heading: the static node/member/Kim-Yue tables of
-include/rafthip.h (rh_qtf_design).  The only host arithmetic is geometry bookkeeping and
-the Hankel-function table 0.5 (H1_{n-1}(kR) - H1_{n+1}(kR)) that the reference evaluates
-with scipy.special.hankel1 (raft/raft_member.py:1104-1107); every per-pair quantity is
-computed on the device by rh_qtf_slender.
+include/rafthip.h (rh_qtf_design).  The only host arithmetic is geometry bookkeeping; the
+Hankel-function table 0.5 (H1_{n-1}(kR) - H1_{n+1}(kR)) that the reference evaluates with
+scipy.special.hankel1 (raft/raft_member.py:1104-1107) is built on the device
+(rh_qtf_hankel), and every per-pair quantity is computed on the device by rh_qtf_slender.
 """
 import ctypes
 
@@ -16,16 +16,18 @@ from . import _native as N
 QN_COUNT, QM_COUNT, KR_COUNT = 46, 36, 6
 
 
-def _hank_table(kk, R):
-    """[n2, 12] table D_n(k R), n = 0..11 (orders -1..12 of hankel1)."""
+def hank_table(kk, R):
+    """[n2, 12] table D_n(k R), n = 0..11 (orders -1..12 of scipy's hankel1): the host
+    restatement rh_qtf_hankel is tested against (tests/test_gpu_qtf.py)."""
     x = np.asarray(kk, dtype=float) * R
     H = hankel1(np.arange(-1, 13)[:, None], x[None, :])         # [14, n2], one ufunc call
     D = 0.5 * (H[0:12] - H[2:14])                              # D_n = 0.5 (H_{n-1} - H_{n+1})
     return D.T.copy()
 
 
-def build_tables(fowt, w2, k2, beta):
-    """Static QTF tables of a FOWT for grid (w2, k2) and heading beta [rad]."""
+def build_tables(fowt, w2, k2, beta, host_hankel=False):
+    """Static QTF tables of a FOWT for grid (w2, k2) and heading beta [rad].  The Hankel
+    table is built on the host only with host_hankel=True (the device builds it otherwise)."""
     rho, g, h = float(fowt.rho_water), float(fowt.g), float(fowt.depth)
     ncols, mcols, kcols, hank = [], [], [], []
     qmstart, kstart = [0], [0]
@@ -84,7 +86,8 @@ def build_tables(fowt, w2, k2, beta):
             rwl = mem.rA + (mem.rB - mem.rA) * (0 - mem.rA[2]) / (mem.rB[2] - mem.rA[2])
             R = np.interp(0, mem.r[:, 2], 0.5 * np.array(mem.ds))
             kcols.append([R, 0.0, 0.0, *rwl])
-            hank.append(_hank_table(k2, R))
+            if host_hankel:
+                hank.append(hank_table(k2, R))
             for il in range(mem.ns - 1):
                 z1 = mem.r[il, 2]
                 if z1 > 0:
@@ -99,14 +102,15 @@ def build_tables(fowt, w2, k2, beta):
                     R2 = mem.ds[il]                               # Q9
                 Rm = 0.5 * (R1 + R2)
                 kcols.append([Rm, z1, z2, *(0.5 * (mem.r[il] + mem.r[il + 1]))])
-                hank.append(_hank_table(k2, Rm))
+                if host_hankel:
+                    hank.append(hank_table(k2, Rm))
         kstart.append(len(kcols))
         mcols.append([1.0 if wl else 0.0, *rint, awl, *last_cm.ravel(), *last_ca.ravel(), *mem.p1, *mem.p2,
                       1.0 if kay else 0.0, *pf, *rwl])
     qnode = np.array(ncols, dtype=float).T.copy() if ncols else np.zeros([QN_COUNT, 0])
     qmemb = np.array(mcols, dtype=float).T.copy() if mcols else np.zeros([QM_COUNT, 0])
     kray = np.array(kcols, dtype=float).T.copy() if kcols else np.zeros([KR_COUNT, 0])
-    hk = np.array(hank, dtype=complex) if hank else np.zeros([0, len(w2), 12], dtype=complex)
+    hk = np.array(hank, dtype=complex) if hank else None
     assert qnode.shape[0] == QN_COUNT and qmemb.shape[0] == QM_COUNT
     return dict(qnode=qnode, qmemb=qmemb, kray=kray, hank=hk, qmstart=np.array(qmstart, dtype=np.int32),
                 kstart=np.array(kstart, dtype=np.int32), rho=rho, g=g, h=h)
@@ -132,8 +136,11 @@ class QtfDevice:
         self.qnode = torch.tensor(pad(t["qnode"], QN_COUNT), **f64).contiguous()
         self.qmemb = torch.tensor(pad(t["qmemb"], QM_COUNT), **f64).contiguous()
         self.kray = torch.tensor(pad(t["kray"], KR_COUNT), **f64).contiguous()
-        self.hank = torch.tensor(t["hank"] if len(t["hank"]) else np.zeros([1, self.n2, 12], dtype=complex),
-                                 dtype=torch.complex128, device=self.dev).contiguous()
+        # Kim & Yue Hankel table [nkr][n2][12], built on the device from k2 and the radii
+        self.hank = torch.zeros([max(self.nkr, 1), self.n2, 12], dtype=torch.complex128, device=self.dev)
+        if self.nkr:
+            N.check(N.lib().rh_qtf_hankel(N.context(device), self.n2, N.ptr(self.k2), self.nkr, N.ptr(self.kray),
+                                          N.ptr(self.hank), N.stream_handle(torch, self.dev)), "rh_qtf_hankel")
         self.qmstart = torch.tensor(t["qmstart"], dtype=torch.int32, device=self.dev)
         self.kstart = torch.tensor(t["kstart"], dtype=torch.int32, device=self.dev)
         self.rho, self.g, self.h = t["rho"], t["g"], t["h"]

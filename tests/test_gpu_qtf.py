@@ -136,6 +136,35 @@ def test_mfma_path_matches_per_pair_kernel(T, beta_deg, grid):
         np.testing.assert_array_equal(a[i, j], np.conj(a[j, i]))
 
 
+def test_device_hankel_table_matches_scipy(T):
+    """rh_qtf_hankel against scipy.special.hankel1 (the reference's call, raft_member.py:1104-1107)
+    on the C3 400 grid for every Kim & Yue radius of OC4semi, and on a wide argument sweep
+    (x = kR from 1e-3 to 40: series, Miller and forward-recurrence ranges): 1e-13 relative."""
+    import torch
+    from raft import _native as N
+    from raft.hydro_math import wave_numbers
+    from raft.qtf import QtfDevice, hank_table
+    m, f = make(T)
+    w2 = np.arange(0.04, 0.35 + 0.5 * 0.04, 0.000825) * 2 * np.pi
+    k2 = wave_numbers(w2, f.depth)
+    qd = QtfDevice(f, w2, k2, 0.0, 0)
+    R = qd.kray[0].cpu().numpy()
+    dev = qd.hank.cpu().numpy()
+    for ir, r in enumerate(R):
+        ref = hank_table(k2, r)
+        err = np.abs(dev[ir] - ref) / np.abs(ref)
+        assert err.max() < 1e-13, (ir, r, err.max())
+    x = np.geomspace(1e-3, 40.0, 2000)
+    kk = torch.tensor(x, dtype=torch.float64, device=qd.dev)
+    one = torch.ones(1, dtype=torch.float64, device=qd.dev)
+    out = torch.empty([1, len(x), 12], dtype=torch.complex128, device=qd.dev)
+    N.check(N.lib().rh_qtf_hankel(N.context(0), len(x), N.ptr(kk), 1, N.ptr(one), N.ptr(out),
+                                  N.stream_handle(torch, qd.dev)), "rh_qtf_hankel")
+    ref = hank_table(x, 1.0)
+    err = np.abs(out[0].cpu().numpy() - ref) / np.abs(ref)
+    assert err.max() < 1e-13, err.max()
+
+
 def test_fixed_body_qtf_matches_oracle(T):
     """Xi0=None (fixed body) against the oracle at the n2=42 grid."""
     from oracle import qtf_oracle as Q

@@ -13,9 +13,14 @@ def main(tag):
     import torch
     import bench
     from raft import _native as N
-    T, f, qd, dd, X, M66, w2, k2, nkay, nwl = bench.build_qtf(0)
+    from raft.qtf import QtfDevice
+    T, f, dd, X, M66, w2, k2 = bench.build_qtf(0)
+    qd = QtfDevice(f, w2, k2, 0.0, 0)
     ref = None
-    for waves in ((0,) if tag == "pmc" else (1, 2, 4)):     # PMC passes: the default (auto) kernel only
+    # PMC passes: the default path only (MFMA GEMMs on this sorted grid); otherwise the
+    # per-pair kernel at 1, 2 and 4 waves per tile
+    for waves in ((0,) if tag == "pmc" else (1, 2, 4)):
+        N.check(N.lib().rh_set_qtf_path(N.context(0), 0 if tag == "pmc" else 1), "rh_set_qtf_path")
         N.check(N.lib().rh_set_qtf_waves(N.context(0), waves), "rh_set_qtf_waves")
         for _ in range(2):
             q = qd.qtf(dd.w, X, M66)
@@ -32,6 +37,7 @@ def main(tag):
         d = np.abs(qh - ref).max() / np.abs(ref).max()
         print(f"{tag:10s} waves={waves} QTF {e0.elapsed_time(e1) / 10:8.3f} ms  maxrel vs waves=1 {d:.2e}", flush=True)
     N.check(N.lib().rh_set_qtf_waves(N.context(0), 0), "rh_set_qtf_waves")
+    N.check(N.lib().rh_set_qtf_path(N.context(0), 0), "rh_set_qtf_path")
 
 
 if __name__ == "__main__":
