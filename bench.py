@@ -70,6 +70,8 @@ def pmc_l2(kernel, kernel_ms):
 
 def solve_kernel_name(nw):
     """The kernel rh_solve_cases launches for this grid (dispatch in rh_abi.hip)."""
+    if nw <= 256:
+        return "rh::k_solve_lds<1, 256>"
     if nw <= 1024:
         return f"rh::k_solve_lds<{1 if nw <= 512 else 2}>"
     return "rh::k_solve_cases<4>"

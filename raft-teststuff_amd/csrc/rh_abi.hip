@@ -237,15 +237,17 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
       return designs_used(ctx, s);
     }
   }
-  // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case, nw <= 1024.
+  // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case (256 for nw <= 256), nw <= 1024.
   if (nw <= 2 * rh::kLT && !ctx->force_general) {
     const int nb = nw <= rh::kLT ? 1 : 2;
     int nmmax = 0;
     for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
-    const size_t lsm = rh::solve_lds_smem(nnmax, nmmax, nb);
+    const int lt = nw <= rh::kLT / 2 ? rh::kLT / 2 : rh::kLT;   // nw <= 256: 256 threads, two cases per CU
+    const size_t lsm = rh::solve_lds_smem(nnmax, nmmax, nb, lt);
     if (lsm <= 160 * 1024) {
-      dim3 grid(cases->ncase), block(rh::kLT);
-      if (nb == 1) hipLaunchKernelGGL(rh::k_solve_lds<1>, grid, block, lsm, s, a);
+      dim3 grid(cases->ncase), block(lt);
+      if (lt < rh::kLT) hipLaunchKernelGGL((rh::k_solve_lds<1, rh::kLT / 2>), grid, block, lsm, s, a);
+      else if (nb == 1) hipLaunchKernelGGL(rh::k_solve_lds<1>, grid, block, lsm, s, a);
       else hipLaunchKernelGGL(rh::k_solve_lds<2>, grid, block, lsm, s, a);
       return designs_used(ctx, s);
     }
@@ -423,6 +425,15 @@ int rh_system_solve_batch(rh_ctx* ctx, int ncase, int nf, int nw, const rh_c128*
   if (ncase == 0) return RH_OK;
   RH_HIP(hipSetDevice(ctx->device));
   const int N = 6 * nf;
+  if (!ctx->force_general) {   // register kernels (rh_set_solver(ctx, 1) keeps the LDS elimination for cross-checks)
+    const dim3 g((nw + 63) / 64, ncase);
+    if (nf == 1)
+      hipLaunchKernelGGL(rh::k_system_solve_reg<1>, g, dim3(64), 0, (hipStream_t)stream, nw, Z, K, F, Xi);
+    else
+      hipLaunchKernelGGL(rh::k_system_solve_reg<2>, g, dim3(64), 0, (hipStream_t)stream, nw, Z, K, F, Xi);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+  }
   const size_t smem = sizeof(double) * 2 * (size_t)(N * N + N) * rh::kSysThreads;
   dim3 grid((nw + rh::kSysThreads - 1) / rh::kSysThreads, ncase);
   hipLaunchKernelGGL(rh::k_system_solve, grid, dim3(rh::kSysThreads), smem, (hipStream_t)stream, N, nw, Z, K, F, Xi);

@@ -105,6 +105,76 @@ __device__ __forceinline__ bool lu_solve(cd (&A)[N][N], cd (&x)[N]) {
   return ok;
 }
 
+// Factor-once / solve-many form of lu_solve (same pivot rule: max |re|+|im|, first maximum):
+// A holds L below the diagonal, U above, the reciprocal pivots on it; piv[k] the row exchanged
+// with k at step k.  Rows are exchanged in columns >= k only, so the multipliers of column k
+// stay where they were formed and lu_apply replays each exchange before that column's
+// elimination (as lu_solve does in one pass).  Returns false on an exactly zero pivot.
+template <int N>
+__device__ __forceinline__ bool lu_factor(cd (&A)[N][N], int (&piv)[N]) {
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    int p = k;
+    double best = cabs1(A[k][k]);
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) {
+      const double v = cabs1(A[i][k]);
+      if (v > best) { best = v; p = i; }
+    }
+    ok = ok && (best != 0.0);
+    piv[k] = p;
+    if (__builtin_amdgcn_ballot_w64(p != k) != 0) {
+#pragma unroll
+      for (int i = k + 1; i < N; ++i) {
+        const bool sw = (p == i);
+#pragma unroll
+        for (int j = k; j < N; ++j) {   // columns >= k only: lu_apply replays the swaps interleaved
+          const cd a = A[k][j], b = A[i][j];
+          A[k][j] = sw ? b : a;
+          A[i][j] = sw ? a : b;
+        }
+      }
+    }
+    const cd pv = best != 0.0 ? A[k][k] : mk(1.0, 0.0);
+    const double inv = 1.0 / (pv.r * pv.r + pv.i * pv.i);
+    const cd rinv = mk(pv.r * inv, -pv.i * inv);
+    A[k][k] = rinv;
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) {
+      const cd l = mul(A[i][k], rinv);
+      A[i][k] = l;
+#pragma unroll
+      for (int j = k + 1; j < N; ++j) A[i][j] = sub(A[i][j], mul(l, A[k][j]));
+    }
+  }
+  return ok;
+}
+template <int N>
+__device__ __forceinline__ void lu_apply(const cd (&A)[N][N], const int (&piv)[N], cd (&x)[N]) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    if (__builtin_amdgcn_ballot_w64(piv[k] != k) != 0) {
+#pragma unroll
+      for (int i = k + 1; i < N; ++i) {
+        const bool sw = (piv[k] == i);
+        const cd a = x[k], b = x[i];
+        x[k] = sw ? b : a;
+        x[i] = sw ? a : b;
+      }
+    }
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) x[i] = sub(x[i], mul(A[i][k], x[k]));
+  }
+#pragma unroll
+  for (int k = N - 1; k >= 0; --k) {
+    cd s = x[k];
+#pragma unroll
+    for (int j = k + 1; j < N; ++j) s = sub(s, mul(A[k][j], x[j]));
+    x[k] = mul(s, A[k][k]);
+  }
+}
+
 // Raw buffer access: the 128-bit resource lives in SGPRs, each lane supplies one 32-bit byte
 // offset and the per-array / per-component part is a scalar offset.  This keeps the many
 // (array, DOF, bin) addresses of the case solve from being materialised as 64-bit VGPR pairs,

@@ -989,4 +989,113 @@ __global__ __launch_bounds__(kSysThreads) void k_system_solve(int N, int nw, con
   }
 }
 
+// The array system per (case, bin) in registers (raft/raft_model.py:1021-1040, 1065: Z_sys =
+// blockdiag(fowt.Z) + K_array, Xi = inv(Z_sys) F).  One FOWT: a 6x6 LU.  Two FOWTs: the 12x12
+// system by its 6x6 blocks, Z_sys = [[A, K12], [K21, D]] (A = Z1 + K11, D = Z2 + K22):
+//   X = A^-1 K12,  S = D - K21 X,  x2 = S^-1 (f2 - K21 A^-1 f1),  x1 = A^-1 f1 - X x2
+// with A factored once for its 7 right-hand sides.  The same solution as the
+// 12 x 12 elimination up to rounding (the reference inverts Z_sys with LAPACK); a 12 x 12
+// complex matrix per lane would need 576 VGPRs.  One lane per bin, 64 lanes per block.
+template <int NF>
+__global__ __launch_bounds__(64) void k_system_solve_reg(int nw, const rh_c128* __restrict__ Z, const double* __restrict__ K,
+                                                         const rh_c128* __restrict__ F, rh_c128* __restrict__ Xi) {
+  constexpr int N = 6 * NF;
+  __shared__ double ks[N * N];   // K_array staged in LDS: uniform reads, no scalar-register pressure
+  for (int e = threadIdx.x; e < N * N; e += 64) ks[e] = K ? K[e] : 0.0;
+  __syncthreads();
+  const int b0 = blockIdx.x * 64 + threadIdx.x;
+  const bool live = b0 < nw;
+  const int b = live ? b0 : nw - 1;          // pad lanes solve the last bin and store nothing
+  const size_t ic = blockIdx.y;
+  Z += ic * (size_t)NF * nw * 36;
+  F += ic * (size_t)N * nw;
+  Xi += ic * (size_t)N * nw;
+  int zo;                        // a zero the compiler cannot see through: the K reads stay where
+  asm volatile("s_mov_b32 %0, 0" : "=s"(zo));   // they are used instead of being hoisted into registers
+  const double* ksz = ks + zo;
+  auto kk = [&](int i, int j) { return ksz[i * N + j]; };
+  auto zload = [&](int f, cd (&A)[6][6]) {   // (0 + Z_f) + K_ff, the reference's order of additions
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const cd z = ld(Z + ((size_t)f * nw + b) * 36 + 6 * i + j);
+        A[i][j] = mk(z.r + kk(6 * f + i, 6 * f + j), z.i);
+      }
+  };
+  if constexpr (NF == 1) {
+    cd A[6][6], x[6];
+    zload(0, A);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] = ld(F + (size_t)i * nw + b);
+    lu_solve<6>(A, x);
+    if (live)
+#pragma unroll
+      for (int i = 0; i < 6; ++i) st(Xi + (size_t)i * nw + b, x[i]);
+  } else {
+    // X = A^-1 K12 goes column by column to a lane-private LDS slab [36][re, im][64 lanes], so
+    // A (factored) and S never occupy registers together
+    __shared__ double xs[36 * 2 * 64];
+    const int ln = threadIdx.x;
+    cd y[6];
+    {
+      cd A[6][6];
+      int pa[6];
+      zload(0, A);
+      lu_factor<6>(A, pa);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) y[i] = ld(F + (size_t)i * nw + b);
+      lu_apply<6>(A, pa, y);                  // y = A^-1 f1
+#pragma unroll 1
+      for (int j = 0; j < 6; ++j) {
+        cd c[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c[i] = mk(kk(i, 6 + j), 0.0);
+        lu_apply<6>(A, pa, c);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          xs[((6 * i + j) * 2) * 64 + ln] = c[i].r;
+          xs[((6 * i + j) * 2 + 1) * 64 + ln] = c[i].i;
+        }
+      }
+    }
+    auto X = [&](int i, int j) { return mk(xs[((6 * i + j) * 2) * 64 + ln], xs[((6 * i + j) * 2 + 1) * 64 + ln]); };
+    cd S[6][6], g[6];
+    int ps[6];
+    zload(1, S);                              // S = D - K21 X
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        cd t = mk(0, 0);
+#pragma unroll
+        for (int m = 0; m < 6; ++m) t = add(t, scl(X(m, j), kk(6 + i, m)));
+        S[i][j] = sub(S[i][j], t);
+      }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {             // g = f2 - K21 A^-1 f1
+      cd t = mk(0, 0);
+#pragma unroll
+      for (int m = 0; m < 6; ++m) t = add(t, scl(y[m], kk(6 + i, m)));
+      g[i] = sub(ld(F + (size_t)(6 + i) * nw + b), t);
+    }
+    lu_factor<6>(S, ps);
+    lu_apply<6>(S, ps, g);                    // x2
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {             // x1 = A^-1 f1 - X x2
+      cd t = y[i];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) t = sub(t, mul(X(i, m), g[m]));
+      y[i] = t;
+    }
+    if (live) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        st(Xi + (size_t)i * nw + b, y[i]);
+        st(Xi + (size_t)(6 + i) * nw + b, g[i]);
+      }
+    }
+  }
+}
+
 }  // namespace rh

@@ -156,22 +156,25 @@ __device__ __forceinline__ double wave_sum63(double v) {
 
 // Every table the loops read is staged here: a global load inside the node loops would share
 // the vector-memory counter with the prefetched wave-table loads and force them to drain.
-__host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB) {
-  return sizeof(double) * ((size_t)12 * kLT * NB      // XiLast [6][512 NB] complex
-                           + (size_t)nn * 3 * kLW     // per-wave node sums
+__host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB, int LT = kLT) {
+  const int LW = LT / 64;
+  return sizeof(double) * ((size_t)12 * LT * NB      // XiLast [6][512 NB] complex
+                           + (size_t)nn * 3 * LW     // per-wave node sums
                            + (size_t)nn * 36          // per-node B_drag contributions
                            + (size_t)nn * 9           // Bmat
                            + (size_t)nn * 5           // member-factored drag coefficients
                            + (size_t)nn               // node axial coordinate t
                            + (size_t)nm * 18          // member cq, c1, c2
-                           + (size_t)2 * kLT * NB     // w and zeta per (padded) bin
-                           + 36 + 108 + kLW * 6 + 36  // B_drag, M|B|C image, std partials, B_lin+B_drag
-                           + kLW)                     // convergence-margin partials
+                           + (size_t)2 * LT * NB     // w and zeta per (padded) bin
+                           + 36 + 108 + LW * 6 + 36  // B_drag, M|B|C image, std partials, B_lin+B_drag
+                           + LW)                     // convergence-margin partials
          + sizeof(int) * ((size_t)nm + 2);            // member node ranges
 }
 
-template <int NB>
-__global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
+// LT threads per case: 512 (8 waves), or 256 for nw <= 256 (two cases per CU; C4 has 240 bins)
+template <int NB, int LT = kLT>
+__global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
+  constexpr int LW = LT / 64;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wv_s = __builtin_amdgcn_readfirstlane(wv);   // wave index in an SGPR
@@ -189,26 +192,26 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
   const bool has_fx = a.c.fext != nullptr;
   const Buf bFx = mkbuf(has_fx ? a.c.fext + c6 : nullptr, has_fx ? 6u * nw16 : 0u);
 
-  constexpr int NWP = kLT * NB;                    // padded bins held in LDS
+  constexpr int NWP = LT * NB;                    // padded bins held in LDS
   cd* xl = reinterpret_cast<cd*>(smem);            // [6][NWP]
-  double* red = smem + 12 * NWP;                   // [nn*3][kLW]
-  double* bm = red + nn * 3 * kLW;                 // [nn][9]
+  double* red = smem + 12 * NWP;                   // [nn*3][LW]
+  double* bm = red + nn * 3 * LW;                 // [nn][9]
   double* al = bm + nn * 9;                        // [nn][5]
   double* bd = al + nn * 5;                        // [36]
   double* mbc = bd + 36;                           // [108] M, B_lin, C
-  double* sred = mbc + 108;                        // [kLW][6]
-  double* bsum = sred + kLW * 6;                   // [36] B_lin + B_drag of this iteration
+  double* sred = mbc + 108;                        // [LW][6]
+  double* bsum = sred + LW * 6;                   // [36] B_lin + B_drag of this iteration
   double* bdn = bsum + 36;                         // [36][nn]
   double* nt = bdn + 36 * nn;                      // [nn]
   double* mbf = nt + nn;                           // [18][nm]
   double* lw = mbf + 18 * nm;                      // [NWP] w per bin (pad bins: w[nw-1])
   double* lz = lw + NWP;                           // [NWP] zeta per bin (pad bins: 0)
-  double* mred = lz + NWP;                         // [kLW] per-wave max of tolCheck
-  int* mstart = reinterpret_cast<int*>(mred + kLW);  // [nm+1]
+  double* mred = lz + NWP;                         // [LW] per-wave max of tolCheck
+  int* mstart = reinterpret_cast<int*>(mred + LW);  // [nm+1]
   load_mbc(d, mbc, tid);
-  for (int n = tid; n < nn; n += kLT) nt[n] = node[RH_NF_T * nn + n];
-  for (int e = tid; e < 18 * nm; e += kLT) mbf[e] = d.memb[e];   // RH_MF_CQ0..C20 are fields 0..17
-  for (int e = tid; e <= nm; e += kLT) mstart[e] = d.mstart[e];
+  for (int n = tid; n < nn; n += LT) nt[n] = node[RH_NF_T * nn + n];
+  for (int e = tid; e < 18 * nm; e += LT) mbf[e] = d.memb[e];   // RH_MF_CQ0..C20 are fields 0..17
+  for (int e = tid; e <= nm; e += LT) mstart[e] = d.mstart[e];
 
   // Per-bin scalars live in LDS, not in registers: nothing per-thread stays live across the
   // phases, so the register-heavy solve of phase C does not push other values to scratch.
@@ -221,7 +224,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
     const rh_c128* XI0 = a.c.Xi_init ? a.c.Xi_init + c6 : nullptr;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int b = tid + kLT * j;
+      const int b = tid + LT * j;
       const bool okb = b < nw;
       const double w = d.w[okb ? b : nw - 1];
       const double zz = sea_amplitude(spec, Hs, Tp, gam, w, d.dw);
@@ -257,8 +260,8 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
       double bz[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        vb[j] = voff(tid + kLT * j);
-        bz[j] = lz[tid + kLT * j];
+        vb[j] = voff(tid + LT * j);
+        bz[j] = lz[tid + LT * j];
       }
       cd Bq[NB], B1[NB], B2[NB], E1[NB], E2[NB];
       auto member_terms = [&](int m) {
@@ -271,7 +274,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
         }
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-          const int b = tid + kLT * j;
+          const int b = tid + LT * j;
           cd X[6];
 #pragma unroll
           for (int c = 0; c < 6; ++c) X[c] = xl[c * NWP + b];
@@ -334,7 +337,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
             load_node(K[r], nr + kRingA);
             const int ln = lane_here();
             const double tot = tbfly3(s0, s1, s2, ln);
-            if (ln < 3) red[(nr * 3 + tbfly3_index(ln)) * kLW + wv_s] = tot;
+            if (ln < 3) red[(nr * 3 + tbfly3_index(ln)) * LW + wv_s] = tot;
           }
         }
       }
@@ -343,14 +346,14 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
     PROF_T(ta1);
     PROF_ADD(1, ta1 - ta0);
     // ---------------- B: node drag matrices and B_drag ----------------------------------
-    for (int n = tid; n < nn; n += kLT) {
+    for (int n = tid; n < nn; n += LT) {
       double r3[3];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const double* R = red + (size_t)(n * 3 + c) * kLW;
+        const double* R = red + (size_t)(n * 3 + c) * LW;
         double s = 0;
 #pragma unroll
-        for (int w = 0; w < kLW; ++w) s += R[w];
+        for (int w = 0; w < LW; ++w) s += R[w];
         r3[c] = s;
       }
       // sum|vrel_q|^2 = sum|s_q|^2 |q|^2 ; circular: |vrel_p|^2 = |s_1|^2|p1|^2 + |s_2|^2|p2|^2
@@ -392,7 +395,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
     for (int j = 0; j < NB; ++j) {
       // per-bin scalars picked without dynamic register indexing (the loop is not unrolled,
       // so only one bin's LU is ever live)
-      const int bj = tid + kLT * j;
+      const int bj = tid + LT * j;
       const unsigned vj = voff(bj);
       const bool okj = bj < nw;
       // drag excitation of bin j before the zeta factor, member-factored:
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
       tc_exc += tc1 - tc0;
 #endif
       if (!okj) continue;
-      const int b = tid + kLT * j;
+      const int b = tid + LT * j;
       const unsigned v = vj;
       const double w = lw[b], z = lz[b];
 #pragma unroll
@@ -527,7 +530,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
     const int all_ok = __syncthreads_and(my_ok ? 1 : 0);
     if (a.o.margin && tid == 0) {   // mred is rewritten only after the next phase-A barrier
       double mx = mred[0];
-      for (int w = 1; w < kLW; ++w) mx = fmax(mx, mred[w]);
+      for (int w = 1; w < LW; ++w) mx = fmax(mx, mred[w]);
       margin = closer_call(margin, mx - tol);
     }
     const int any_nan = __syncthreads_or(my_nan ? 1 : 0);
@@ -560,11 +563,11 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
   }
   if (a.o.B_drag && tid < 36) a.o.B_drag[(size_t)ic * 36 + tid] = bd[tid];
   if (a.o.Bmat)
-    for (int e = tid; e < nn * 9; e += kLT) a.o.Bmat[(size_t)ic * nn * 9 + e] = bm[e];
+    for (int e = tid; e < nn * 9; e += LT) a.o.Bmat[(size_t)ic * nn * 9 + e] = bm[e];
   if (a.o.Z) {   // final impedance fowt.Z (raft/raft_model.py:1013) from the last B_drag, streamed
 #pragma unroll 1
     for (int j = 0; j < NB; ++j) {
-      const int b = tid + kLT * j;
+      const int b = tid + LT * j;
       if (b >= nw) continue;
       const double w = lw[b], w2 = -(w * w);
       rh_c128* Zo = a.o.Z + ((size_t)ic * nw + b) * 36;
@@ -579,7 +582,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
   double ss[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int b = tid + kLT * j;
+    const int b = tid + LT * j;
     if (b >= nw) continue;
     const double z = lz[b];
 #pragma unroll
@@ -601,7 +604,7 @@ __global__ __launch_bounds__(kLT, 1) void k_solve_lds(CaseArgs a) {
     __syncthreads();
     if (tid < 6) {
       double s = 0;
-      for (int w = 0; w < kLW; ++w) s += sred[w * 6 + tid];
+      for (int w = 0; w < LW; ++w) s += sred[w * 6 + tid];
       a.o.std[(size_t)ic * 6 + tid] = sqrt(0.5 * s);
     }
   }
