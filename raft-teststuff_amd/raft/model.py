@@ -484,7 +484,26 @@ class Model:
             gm.append(float(one("wave_gamma", 0)))
         return hd, sp, Hs, Tp, gm
 
-    def analyzeArrayBatch(self, cases, tol=0.01, host=True, marks=None):
+    def prepareArrayBatch(self, cases):
+        """The per-batch inputs of analyzeArrayBatch resident on the device: the (case, FOWT)
+        case table with its wave tables (solver.prepare_batch), the FOWT descriptors and the
+        array stiffness.  Reusable for repeated solves of the same sea states."""
+        import torch
+        nf, n = self.nFOWT, len(cases)
+        dds = [f.device_design() for f in self.fowtList]
+        if len(set(d.nn for d in dds)) != 1:
+            raise NotImplementedError("analyzeArrayBatch: FOWTs with different submerged node counts")
+        hd, sp, Hs, Tp, gm = self._case_columns(cases)
+        rep = lambda v: [x for x in v for _ in range(nf)]          # case-major, FOWT-minor
+        cs = CaseSet(np.tile(np.arange(nf, dtype=np.int32), n), rep(hd), rep(sp), rep(Hs), rep(Tp), rep(gm))
+        dev = dds[0].device
+        from .solver import prepare_batch
+        Ka = self.array_stiffness()
+        return dict(n=n, dds=dds, cs=cs, prep=prepare_batch(dds, cs), dev=dev,
+                    arr=(N.RhDesign * nf)(*[d.struct() for d in dds]),
+                    K=None if Ka is None else torch.tensor(Ka, dtype=torch.float64, device=dev).contiguous())
+
+    def analyzeArrayBatch(self, cases=None, tol=0.01, host=True, marks=None, prepared=None):
         """The coupled-array response of many single-sea-state cases (raft/raft_model.py:852-1065
         for nFOWT > 1) in four device calls instead of per-case, per-FOWT host round trips:
           1. every (case, FOWT) drag fixed point in one rh_solve_cases launch;
@@ -494,32 +513,25 @@ class Model:
              case and bin (rh_system_solve_batch);
           4. per-FOWT motion PSD / RMS (rh_motion_stats).
         Returns Xi [n, 6N, nw], iters / status [n, N], psd [n, N, 6, nw], std [n, N, 6], zeta.
+        prepared: prepareArrayBatch(cases) of an earlier call (then `cases` is not needed).
         marks: optional two timing events recorded around the fixed-point launch (bench)."""
         import torch
-        nf, n, nw = self.nFOWT, len(cases), self.nw
-        dds = [f.device_design() for f in self.fowtList]
-        if len(set(d.nn for d in dds)) != 1:
-            raise NotImplementedError("analyzeArrayBatch: FOWTs with different submerged node counts")
-        hd, sp, Hs, Tp, gm = self._case_columns(cases)
-        rep = lambda v: [x for x in v for _ in range(nf)]          # case-major, FOWT-minor
-        cs = CaseSet(np.tile(np.arange(nf, dtype=np.int32), n), rep(hd), rep(sp), rep(Hs), rep(Tp), rep(gm))
-        dev = dds[0].device
-        from .solver import prepare_batch
-        prep = prepare_batch(dds, cs)
+        P = prepared if prepared is not None else self.prepareArrayBatch(cases)
+        nf, n, nw = self.nFOWT, P["n"], self.nw
+        dds, cs, prep, dev = P["dds"], P["cs"], P["prep"], P["dev"]
         if marks:
             marks[0].record(torch.cuda.current_stream(dev))
         res = solve_batch(dds, cs, self.nIter, self.XiStart, tol, want=("zeta", "Bmat", "Z"), prepared=prep)
         if marks:
             marks[1].record(torch.cuda.current_stream(dev))
         F = torch.empty([n * nf, 6, nw], dtype=torch.complex128, device=dev)
-        arr = (N.RhDesign * nf)(*[d.struct() for d in dds])
+        arr = P["arr"]
         s = N.stream_handle(torch, dev)
         ctx = N.context(self.device)
         N.check(N.lib().rh_wave_excitation(ctx, arr, nf, n * nf, N.ptr(prep["design"]), N.ptr(prep["head"]),
                                            N.ptr(res["zeta"]), N.ptr(res["Bmat"].contiguous()), N.ptr(F), s),
                 "rh_wave_excitation")
-        Ka = self.array_stiffness()
-        K = None if Ka is None else torch.tensor(Ka, dtype=torch.float64, device=dev).contiguous()
+        K = P["K"]
         X = torch.empty([n, 6 * nf, nw], dtype=torch.complex128, device=dev)
         N.check(N.lib().rh_system_solve_batch(ctx, n, nf, nw, N.ptr(res["Z"]), N.ptr(K), N.ptr(F), N.ptr(X), s),
                 "rh_system_solve_batch")

@@ -1,0 +1,16 @@
+"""The C4 leg of bench.py alone (2-FOWT farm, 512 sea states per step): run under
+rocprofv3 --kernel-trace --stats to split the step into kernels and host gaps."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "raft-teststuff_amd"))
+
+if __name__ == "__main__":
+    import torch
+    import bench
+    torch.cuda.set_device(0)
+    r = bench.bench_c4(0, int(sys.argv[1]) if len(sys.argv) > 1 else 10, 1, 0, None)
+    print(json.dumps({k: r[k] for k in ("value", "ms_per_step", "device_ms_per_step")} | {"kernel_ms": r["roofline"]["kernel_ms"]}))
