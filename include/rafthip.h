@@ -370,6 +370,14 @@ int rh_qtf_hermitian_fill(rh_ctx* ctx, int n2, rh_c128* qtf, rh_stream stream);
 int rh_force_2nd(rh_ctx* ctx, int n2, const double* w2, const rh_c128* qtf, int nw, const double* w, double dw,
                  const double* S0, double* f, double* f_mean, rh_stream stream);
 
+/* Second-order force spectrum, 'spectrum' interpolation mode (raft/raft_fowt.py:1760-1784,
+ * 1809-1810): S = interp(w2, w, S0) (0 outside w), force spectrum on the QTF grid
+ * Sf [6][n2] (device workspace, written), then f [6][nw] = sqrt(2 dw interp(w - w[0],
+ * w2 - w2[0], Sf)) shifted by one bin (the reference returns it as complex with zero imaginary
+ * part), f_mean [6]. */
+int rh_force_2nd_spectrum(rh_ctx* ctx, int n2, const double* w2, const rh_c128* qtf, int nw, const double* w,
+                          double dw, const double* S0, double* Sf, double* f, double* f_mean, rh_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -399,3 +399,29 @@ def hydro_force_2nd(qtf, w1_2nd, w, S0, dw):
     f[:, 0:-1] = f[:, 1:]
     f[:, -1] = 0
     return fm, f
+
+
+def hydro_force_2nd_spectrum(qtf, w1_2nd, w, S0, dw):
+    """calcHydroForce_2ndOrd 'spectrum' mode (raft/raft_fowt.py:1760-1784, 1809-1810): the
+    force spectrum on the QTF grid from the resampled wave spectrum, then resampled to w."""
+    nw1 = len(w1_2nd)
+    nw = len(w)
+    S = np.interp(w1_2nd, w, S0, left=0, right=0)
+    mu = w1_2nd - w1_2nd[0]
+    d1 = w1_2nd[1] - w1_2nd[0]
+    f = np.zeros([6, nw], dtype=complex)
+    fm = np.zeros(6)
+    for d in range(6):
+        Q = qtf[:, :, 0, d]
+        Sf = np.zeros(nw1)
+        for imu in range(1, nw1):
+            Saux = np.zeros(nw1)
+            Saux[0:nw1 - imu] = S[imu:]
+            Qaux = np.zeros(nw1, dtype=complex)
+            Qaux[0:nw1 - imu] = np.diag(Q, imu)
+            Sf[imu] = 8 * np.sum(S * Saux * np.abs(Qaux) ** 2) * d1
+        fm[d] = 2 * np.sum(S * np.diag(Q.real, 0)) * d1
+        f[d, :] = np.sqrt(2 * np.interp(w - w[0], mu, Sf, left=0, right=0) * dw)
+    f[:, 0:-1] = f[:, 1:]
+    f[:, -1] = 0
+    return fm, f

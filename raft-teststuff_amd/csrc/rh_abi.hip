@@ -552,4 +552,18 @@ int rh_force_2nd(rh_ctx* ctx, int n2, const double* w2, const rh_c128* qtf, int 
   return RH_OK;
 }
 
+int rh_force_2nd_spectrum(rh_ctx* ctx, int n2, const double* w2, const rh_c128* qtf, int nw, const double* w,
+                          double dw, const double* S0, double* Sf, double* f, double* f_mean, rh_stream stream) {
+  if (!ctx || !w2 || !qtf || !w || !S0 || !Sf || !f || !f_mean)
+    return fail(RH_EINVAL, "rh_force_2nd_spectrum: null argument");
+  if (n2 < 2 || nw < 2 || !(dw > 0)) return fail(RH_EINVAL, "rh_force_2nd_spectrum: bad sizes");
+  RH_HIP(hipSetDevice(ctx->device));
+  const hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(rh::k_force2nd_spec, dim3(n2), dim3(256), 0, s, n2, w2, qtf, nw, w, S0, Sf, f_mean);
+  RH_HIP(hipGetLastError());
+  hipLaunchKernelGGL(rh::k_force2nd_spec_out, dim3((6 * nw + 255) / 256), dim3(256), 0, s, n2, w2, nw, w, dw, Sf, f);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
 }  // extern "C"

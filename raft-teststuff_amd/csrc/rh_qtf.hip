@@ -939,4 +939,96 @@ __global__ __launch_bounds__(256) void k_force2nd(int n2, const double* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// second-order force spectrum, 'spectrum' interpolation mode (raft/raft_fowt.py:1760-1784)
+// ---------------------------------------------------------------------------------------
+// np.interp(x, xp, fp, left=0, right=0) for increasing xp: j with xp[j] <= x < xp[j+1];
+// x == xp[j] (and x == xp[n-1]) returns fp[j] exactly, else slope (x - xp[j]) + fp[j].
+__device__ __forceinline__ double np_interp0(double x, const double* xp, const double* fp, int n, int stride = 1) {
+  if (!(x >= xp[0]) || x > xp[n - 1]) return 0.0;
+  int lo = 0, hi = n - 1;                 // invariant xp[lo] <= x, and x < xp[hi] or hi == n-1
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (xp[mid] <= x) lo = mid; else hi = mid;
+  }
+  if (x == xp[n - 1]) return fp[(size_t)(n - 1) * stride];
+  const double y0 = fp[(size_t)lo * stride];
+  if (xp[lo] == x) return y0;
+  const double y1 = fp[(size_t)hi * stride];
+  const double slope = (y1 - y0) / (xp[hi] - xp[lo]);
+  return slope * (x - xp[lo]) + y0;
+}
+
+// Stage 1, block per difference-frequency index mu of the QTF grid: S = interp(w2, w, S0) on
+// the fly, Sf[d][mu] = 8 sum_i S_i S_{i+mu} |Q_d(i, i+mu)|^2 dw2 (mu >= 1, Sf[d][0] = 0) and the
+// mean drift f_mean[d] = 2 sum_i S_i Re Q_d(i, i) dw2 (mu == 0).  Upper half of the QTF only.
+__global__ __launch_bounds__(256) void k_force2nd_spec(int n2, const double* __restrict__ w2, const rh_c128* __restrict__ qtf,
+                                                        int nw, const double* __restrict__ w,
+                                                        const double* __restrict__ S0, double* __restrict__ Sf,
+                                                        double* __restrict__ fmean) {
+  __shared__ double red[4][6];
+  const int mu = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const double dw2 = w2[1] - w2[0];
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = tid; i + mu < n2; i += 256) {
+    const int j = i + mu;
+    const double Si = np_interp0(w2[i], w, S0, nw);
+    const rh_c128* q = qtf + ((size_t)i * n2 + j) * 6;
+    if (mu == 0) {
+#pragma unroll
+      for (int d = 0; d < 6; ++d) acc[d] += Si * ld(q + d).r;
+    } else {
+      const double ss = Si * np_interp0(w2[j], w, S0, nw);
+#pragma unroll
+      for (int d = 0; d < 6; ++d) acc[d] += ss * abs2(ld(q + d));
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 6; ++d) {
+    const double s = wave_sum(acc[d]);
+    if (lane == 0) red[wv][d] = s;
+  }
+  __syncthreads();
+  if (tid < 6) {
+    const double s = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    if (mu == 0) {
+      fmean[tid] = 2 * s * dw2;
+      Sf[(size_t)tid * n2] = 0.0;
+    } else {
+      Sf[(size_t)tid * n2 + mu] = 8 * s * dw2;
+    }
+  }
+}
+
+// Stage 2, thread per (dof, output bin): Sf_interp = interp(w - w[0], w2 - w2[0], Sf, 0, 0),
+// f = sqrt(2 Sf_interp dw), shifted by one bin with a zero last bin (:1781-1784, 1809-1810).
+__global__ __launch_bounds__(256) void k_force2nd_spec_out(int n2, const double* __restrict__ w2, int nw,
+                                                            const double* __restrict__ w, double dw,
+                                                            const double* __restrict__ Sf, double* __restrict__ fout) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 6 * nw) return;
+  const int d = t / nw, b = t % nw;
+  if (b == nw - 1) {
+    fout[t] = 0.0;
+    return;
+  }
+  // the grid mu = w2 - w2[0], formed per probe (a binary search reads log2(n2) entries)
+  const double x = w[b + 1] - w[0], w20 = w2[0];
+  double v = 0.0;
+  if (x >= 0.0 && x <= w2[n2 - 1] - w20) {
+    int lo = 0, hi = n2 - 1;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (w2[mid] - w20 <= x) lo = mid; else hi = mid;
+    }
+    const double* S = Sf + (size_t)d * n2;
+    const double xl = w2[lo] - w20, xh = w2[hi] - w20;
+    if (x == w2[n2 - 1] - w20) v = S[n2 - 1];
+    else if (xl == x) v = S[lo];
+    else v = (S[hi] - S[lo]) / (xh - xl) * (x - xl) + S[lo];
+  }
+  fout[t] = sqrt(2 * v * dw);
+}
+
 }  // namespace rh

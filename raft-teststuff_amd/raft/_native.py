@@ -112,6 +112,8 @@ def lib():
                 "rh_set_qtf_path": [_p, ctypes.c_int],
                 "rh_qtf_hankel": [_p, ctypes.c_int, _p, ctypes.c_int, _p, _p, _p],
                 "rh_force_2nd": [_p, ctypes.c_int, _p, _p, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p],
+                "rh_force_2nd_spectrum": [_p, ctypes.c_int, _p, _p, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p,
+                                          _p],
             }.items():
                 fn = getattr(L, name)
                 fn.argtypes = args

@@ -477,12 +477,13 @@ class FOWT:
 
     def calcHydroForce_2ndOrd(self, beta, S0, iCase=None, iWT=None, interpMode="qtf"):
         """Difference-frequency force amplitudes and mean drift from the QTF
-        (raft/raft_fowt.py:1728-1818, interpMode 'qtf') on the device.  Returns
-        (f_mean [6], f [6, nw]) like the reference."""
+        (raft/raft_fowt.py:1728-1818) on the device.  interpMode 'qtf' (the default: the QTF
+        resampled to (w, w), then the force spectrum) or 'spectrum' (the force spectrum on the
+        QTF grid, then resampled; f is complex with zero imaginary part, as the reference's).
+        Returns (f_mean [6], f [6, nw]) like the reference."""
         import torch
-        if interpMode != "qtf":
-            raise NotImplementedError("calcHydroForce_2ndOrd: only interpMode='qtf' (the reference default) is "
-                                      "accelerated")
+        if interpMode not in ("qtf", "spectrum"):
+            raise ValueError(f"calcHydroForce_2ndOrd: interpMode must be 'qtf' or 'spectrum', not {interpMode!r}")
         h2 = getattr(self, "heads_2nd", None)
         from_file = self.potSecOrder == 2
         if h2 is None or (not from_file and getattr(self, "_qtf_dev", None) is None):
@@ -493,12 +494,13 @@ class FOWT:
         if beta > h2[-1]:
             print(f"Warning in calcHydroForce_2ndOrd: angle {beta} is more than the maximum incidence angle in the "
                   f"QTF. An incidence of {h2[-1]} will be considered for 2nd order loads.")
-        from .qtf import force_2nd
+        from .qtf import force_2nd, force_2nd_spectrum
         dd = self.device_design()
         qd, qt = self._file_qtf_device(beta) if from_file else (self._qtf_qd, self._qtf_dev)
         S = S0 if isinstance(S0, torch.Tensor) else torch.tensor(np.asarray(S0, dtype=float), dtype=torch.float64,
                                                                   device=dd.device)
-        fm, f = force_2nd(qd, qt, dd.w, self.dw, S.to(dd.device).contiguous())
+        kern = force_2nd if interpMode == "qtf" else force_2nd_spectrum
+        fm, f = kern(qd, qt, dd.w, self.dw, S.to(dd.device).contiguous())
         self._f2nd_dev = f
         f_mean, f_h = fm.cpu().numpy(), f.cpu().numpy()
         if self.outFolderQTF is not None:

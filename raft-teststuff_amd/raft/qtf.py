@@ -210,3 +210,17 @@ def force_2nd(qdev, qtf, w, dw, S0):
                                  float(dw), N.ptr(S0), N.ptr(f), N.ptr(fm), N.stream_handle(torch, qdev.dev)),
             "rh_force_2nd")
     return fm, f
+
+
+def force_2nd_spectrum(qdev, qtf, w, dw, S0):
+    """rh_force_2nd_spectrum ('spectrum' mode, raft/raft_fowt.py:1760-1784): (f_mean [6],
+    f [6, nw] complex with zero imaginary part, as the reference returns it) device tensors."""
+    torch = qdev.torch
+    nw = int(w.numel())
+    f = torch.empty([6, nw], dtype=torch.float64, device=qdev.dev)
+    fm = torch.empty([6], dtype=torch.float64, device=qdev.dev)
+    Sf = torch.empty([6, qdev.n2], dtype=torch.float64, device=qdev.dev)
+    N.check(N.lib().rh_force_2nd_spectrum(N.context(qdev.dev_index), qdev.n2, N.ptr(qdev.w2), N.ptr(qtf), nw,
+                                          N.ptr(w), float(dw), N.ptr(S0), N.ptr(Sf), N.ptr(f), N.ptr(fm),
+                                          N.stream_handle(torch, qdev.dev)), "rh_force_2nd_spectrum")
+    return fm, torch.complex(f, torch.zeros_like(f))

@@ -507,7 +507,31 @@ def golden_qtf12d():
     print("wrote qtf12d.npz", file=sys.stderr)
 
 
+def golden_f2nd_spectrum():
+    """calcHydroForce_2ndOrd(interpMode='spectrum') (raft/raft_fowt.py:1760-1784), the
+    non-default mode: the reference method applied to the QTFs already in the fixtures (the
+    C3 slender-body QTF at n2=42, and the .12d file QTF with two of its cases' spectra)."""
+    from types import SimpleNamespace
+
+    import raft.raft_fowt as rf
+    C3 = dict(np.load(os.path.join(HERE, "c3_qtf.npz")))
+    Q12 = dict(np.load(os.path.join(HERE, "qtf12d.npz")))
+    out = {}
+    runs = [("c3", C3["out_qtf"], np.array([0.0]), C3["w1_2nd"], C3["w"], C3["out_S"][0], 0.0),
+            ("q12_b0", Q12["qtf"], Q12["heads_2nd"], Q12["w1_2nd"], Q12["w"], Q12["out_S"][0][0], 0.0),
+            ("q12_s1", Q12["qtf"], Q12["heads_2nd"], Q12["w1_2nd"], Q12["w"], Q12["out_S"][1][0], 0.0)]
+    for tag, qtf, heads, w1, w, S0, beta in runs:
+        obj = SimpleNamespace(nDOF=6, nw=len(w), w=w, dw=float(w[1] - w[0]), qtf=qtf, heads_2nd=heads, w1_2nd=w1,
+                              outFolderQTF=None)
+        fm, f = rf.FOWT.calcHydroForce_2ndOrd(obj, beta, S0, interpMode="spectrum")
+        out.update({f"{tag}_beta": np.float64(beta), f"{tag}_S0": S0, f"{tag}_fmean": fm, f"{tag}_f": f})
+    np.savez_compressed(os.path.join(HERE, "f2nd_spectrum.npz"), **out)
+    print("wrote f2nd_spectrum.npz", file=sys.stderr)
+
+
 def main(which):
+    if "spectrum" in which:
+        golden_f2nd_spectrum()
     if "qtf12d" in which:
         golden_qtf12d()
     if "qtf" in which:

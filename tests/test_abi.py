@@ -29,7 +29,8 @@ def test_header_declares_the_boundary():
     fns = declared_functions()
     for must in ["rh_ctx_create", "rh_ctx_destroy", "rh_last_error", "rh_wave_tables", "rh_solve_cases",
                  "rh_heading_response", "rh_linearize", "rh_drag_excitation", "rh_sea_state", "rh_motion_stats",
-                 "rh_system_solve", "rh_version", "rh_qtf_workspace_bytes", "rh_qtf_slender", "rh_force_2nd"]:
+                 "rh_system_solve", "rh_version", "rh_qtf_workspace_bytes", "rh_qtf_slender", "rh_force_2nd",
+                 "rh_force_2nd_spectrum"]:
         assert must in fns
 
 

@@ -226,3 +226,18 @@ def test_tile_sharded_qtf_equals_single_device(T):
         acc += part
     qd.hermitian_fill(acc)
     np.testing.assert_array_equal(acc.cpu().numpy(), f.qtf[:, :, 0, :])
+
+
+def test_force_spectrum_mode_matches_reference(T):
+    """calcHydroForce_2ndOrd(interpMode='spectrum') on the device (rh_force_2nd_spectrum)
+    against the reference method on the same QTF and spectrum (f2nd_spectrum.npz)."""
+    G = load_golden("f2nd_spectrum")
+    m, f = make(T)
+    f.calcHydroExcitation(_case(T), memberList=f.memberList)
+    f.calcQTF_slenderBody(0, Xi0=T["out_Xi0"])
+    fm, fd = f.calcHydroForce_2ndOrd(f.beta[0], G["c3_S0"], interpMode="spectrum")
+    assert fd.dtype == complex and np.all(fd.imag == 0) and np.all(fd[:, -1] == 0)
+    assert rel(fd, G["c3_f"]) < RTOL, rel(fd, G["c3_f"])
+    np.testing.assert_allclose(fm, G["c3_fmean"], rtol=RTOL, atol=RTOL * np.abs(G["c3_fmean"]).max())
+    with pytest.raises(ValueError):
+        f.calcHydroForce_2ndOrd(f.beta[0], G["c3_S0"], interpMode="bogus")

@@ -68,3 +68,15 @@ def test_force_spectrum_from_file_qtf(T, tmp_path):
     assert rel(fd, T["out_Fhydro_2nd"][0][0].real) < RTOL
     np.testing.assert_allclose(fm, T["out_Fhydro_2nd_mean"][0][0], rtol=RTOL,
                                atol=RTOL * np.abs(T["out_Fhydro_2nd_mean"][0][0]).max())
+
+
+@pytest.mark.parametrize("tag", ["q12_b0", "q12_s1"])
+def test_force_spectrum_mode_from_file_qtf(T, tmp_path, tag):
+    """interpMode='spectrum' on the .12d QTF against the reference method (f2nd_spectrum.npz)."""
+    G = load_golden("f2nd_spectrum")
+    m, f = make(T, str(tmp_path / "q"))
+    case = json.loads(str(T["cases_json"]))[0]
+    f.calcHydroExcitation(dict(case), memberList=f.memberList)
+    fm, fd = f.calcHydroForce_2ndOrd(0.0, G[f"{tag}_S0"], interpMode="spectrum")
+    assert rel(fd, G[f"{tag}_f"]) < RTOL, rel(fd, G[f"{tag}_f"])
+    np.testing.assert_allclose(fm, G[f"{tag}_fmean"], rtol=RTOL, atol=RTOL * np.abs(G[f"{tag}_fmean"]).max())

@@ -57,3 +57,16 @@ def test_oracle_second_order_solve_matches_reference(T):
     assert list(r["iters_pair"]) == list(T["out_iters_pair"])
     assert _rel(r["Xi"], T["out_Xi"]) < 1e-12
     assert _rel(r["Xi0"], T["out_Xi0"]) < 1e-12
+
+
+@pytest.mark.parametrize("tag", ["c3", "q12_b0", "q12_s1"])
+def test_oracle_force_2nd_spectrum_matches_reference(tag):
+    """interpMode='spectrum' (raft/raft_fowt.py:1760-1784) against the reference method run on
+    the fixture QTFs (tests/golden/f2nd_spectrum.npz, make_golden.py golden_f2nd_spectrum)."""
+    G = load_golden("f2nd_spectrum")
+    src = load_golden("c3_qtf") if tag == "c3" else load_golden("qtf12d")
+    qtf = src["out_qtf"] if tag == "c3" else src["qtf"]
+    fm, f = Q.hydro_force_2nd_spectrum(qtf, src["w1_2nd"], src["w"], G[f"{tag}_S0"], float(src["dw"]))
+    np.testing.assert_allclose(fm, G[f"{tag}_fmean"], rtol=1e-12, atol=1e-12 * np.abs(fm).max())
+    assert G[f"{tag}_f"].dtype == complex and f.dtype == complex
+    assert _rel(f, G[f"{tag}_f"]) < 1e-12
