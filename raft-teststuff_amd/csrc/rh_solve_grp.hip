@@ -95,6 +95,7 @@ __global__ __launch_bounds__(kGT, 1) void k_solve_grp(CaseArgs a, const int* __r
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wv_s = __builtin_amdgcn_readfirstlane(wv);
+  PROF_T(tp0);
   const int g = xcd_remap(blockIdx.x, ngroup);
   const int s0 = gstart[g];
   const int ncg = min(gstart[g + 1] - s0, CG);
@@ -168,8 +169,12 @@ __global__ __launch_bounds__(kGT, 1) void k_solve_grp(CaseArgs a, const int* __r
     iters[c] = nloop;
   }
   __syncthreads();
+  PROF_T(tp1);
+  PROF_ADD(0, tp1 - tp0);
 
   for (int it = a.c.first_iter; it < nloop && done != all; ++it) {
+    PROF_T(ta0);
+    PROF_ADD(7, 1);
     // ---------------- A: per-node sums of squared relative-velocity components ----------
     // (raft/raft_fowt.py:1205-1220), member-factored as in k_solve_lds
 #pragma unroll 1
@@ -259,6 +264,8 @@ __global__ __launch_bounds__(kGT, 1) void k_solve_grp(CaseArgs a, const int* __r
       }
     }
     __syncthreads();
+    PROF_T(ta1);
+    PROF_ADD(1, ta1 - ta0);
     // ---------------- B: node drag matrices and B_drag, per unfinished case ---------------
     if (tid == 0) *flg = 0;
     for (int e = tid; e < CG * nn; e += kGT) {
@@ -301,6 +308,11 @@ __global__ __launch_bounds__(kGT, 1) void k_solve_grp(CaseArgs a, const int* __r
       }
     }
     __syncthreads();
+    PROF_T(ta2);
+    PROF_ADD(2, ta2 - ta1);
+#ifdef RH_PROF
+    unsigned long long tc_exc = 0, tc_sol = 0;
+#endif
     // ---------------- C: excitation, Z(w), LU solve, convergence flags ------------------
     int bad = 0;   // per thread: bit 3c = not converged, 3c+1 = NaN, 3c+2 = singular
 #pragma unroll 1
@@ -308,6 +320,7 @@ __global__ __launch_bounds__(kGT, 1) void k_solve_grp(CaseArgs a, const int* __r
       const int bj = tid + kGT * j;
       const unsigned vj = voff(bj);
       const bool okj = bj < nw;
+      PROF_T(tc0);
       cd fe[6];
 #pragma unroll
       for (int k = 0; k < 6; ++k) fe[k] = bld(bFe, vj, k * nw16);
@@ -371,6 +384,10 @@ __global__ __launch_bounds__(kGT, 1) void k_solve_grp(CaseArgs a, const int* __r
         }
         if (nn > 0) fold();
       }
+      PROF_T(tc1);
+#ifdef RH_PROF
+      tc_exc += tc1 - tc0;
+#endif
       if (!okj) continue;
       const int b = bj;
       const double w = lw[b];
@@ -442,7 +459,13 @@ __global__ __launch_bounds__(kGT, 1) void k_solve_grp(CaseArgs a, const int* __r
         f |= (ok ? 0 : 1) | (nan ? 2 : 0);
         bad |= f << (3 * c);
       }
+#ifdef RH_PROF
+      tc_sol += clock64() - tc1;
+#endif
     }
+    PROF_ADD(3, tc_exc);
+    PROF_ADD(4, tc_sol);
+    PROF_T(ta3);
     // block-wide OR of the flag bits: one LDS atomic per wave and bit group
     {
       int wbits = 0;
@@ -452,6 +475,8 @@ __global__ __launch_bounds__(kGT, 1) void k_solve_grp(CaseArgs a, const int* __r
       if (lane == 0 && wbits) atomicOr(flg, wbits);
     }
     __syncthreads();
+    PROF_T(ta4);
+    PROF_ADD(5, ta4 - ta3);
     const int fl = *flg;
 #pragma unroll
     for (int c = 0; c < CG; ++c) {
@@ -467,6 +492,7 @@ __global__ __launch_bounds__(kGT, 1) void k_solve_grp(CaseArgs a, const int* __r
   }
 
   // ---------------- outputs, per case ------------------------------------------------------
+  PROF_T(te0);
 #pragma unroll
   for (int c = 0; c < CG; ++c) {
     if (c >= ncg) continue;
@@ -528,6 +554,8 @@ __global__ __launch_bounds__(kGT, 1) void k_solve_grp(CaseArgs a, const int* __r
       a.o.std[(size_t)i * 6 + k] = sqrt(0.5 * s);
     }
   }
+  PROF_T(te1);
+  PROF_ADD(6, te1 - te0);
 }
 
 }  // namespace rh
