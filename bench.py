@@ -397,7 +397,7 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    B = DesignBatch(variants, statics={"C_moor": C_moor}, device=device, pool=pool, light=True)
+    B = DesignBatch(variants, statics={"C_moor": C_moor}, device=device, pool=pool, native=True)
     cs = B.case_set(local_idx, cases_all[lo:hi])
     from raft.solver import prepare_batch
     prep = prepare_batch(B.dds, cs)                  # device wave tables per (design, heading)

@@ -378,6 +378,28 @@ int rh_force_2nd(rh_ctx* ctx, int n2, const double* w2, const rh_c128* qtf, int 
 int rh_force_2nd_spectrum(rh_ctx* ctx, int n2, const double* w2, const rh_c128* qtf, int nw, const double* w,
                           double dw, const double* S0, double* Sf, double* f, double* f_mean, rh_stream stream);
 
+/* ---- native per-design host preparation (host code; no device calls) -------------------
+ * Members, statics, added mass and the device-table layout of many single-FOWT designs on
+ * host threads: the per-design work of Model/FOWT setup before a case loop
+ * (raft/raft_model.py:30-170, raft/raft_fowt.py:291-565, 848-880; raft/raft_member.py:23-1050),
+ * here in C++ (raft-teststuff_amd/csrc/rh_prep.h) so that a design sweep (C5) pays no
+ * interpreter time per design.  spec: one float64 record per design, design i at
+ * spec[spec_off[i] .. spec_off[i+1]) (format: rh_prep.h; writer: raft/native_prep.py).
+ * w, k [nw]: the shared frequency grid and wave numbers.  nthreads <= 0: all host cores.
+ * Designs with MacCamy-Fuchs members are refused (RH_EINVAL): the Python path prepares them. */
+typedef struct rh_prep rh_prep;
+int rh_prep_designs(int ndesign, const double* spec, const long long* spec_off, int nw, const double* w,
+                    const double* k, int nthreads, rh_prep** out);
+/* info [ndesign][5] = (packed offset, packed length, mstart offset, nn, nm), then the totals
+ * info[5 nd] = packed doubles, info[5 nd + 1] = mstart ints.  Per design the packed block is
+ * w[nw], k[nw], node[RH_NF_COUNT][max(nn,1)], memb[RH_MF_COUNT][max(nm,1)], M[36], B[36], C[36]
+ * (the layout of raft/prep.py host_tables). */
+int rh_prep_layout(const rh_prep* p, long long* info);
+/* packed [total], mstart [total]; statics (optional) [ndesign][5][36] = M_struc, B_struc,
+ * C_struc, C_hydro, A_hydro_morison. */
+int rh_prep_copy(const rh_prep* p, double* packed, int* mstart, double* statics);
+void rh_prep_free(rh_prep* p);
+
 #ifdef __cplusplus
 }
 #endif

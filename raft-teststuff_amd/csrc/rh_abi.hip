@@ -15,6 +15,7 @@
 #include "rh_qtf_mfma.hip"
 #include "rh_solve.hip"
 #include "rh_solve_grp.hip"
+#include "rh_prep.h"       // host-only: native per-design preparation (rh_prep_designs)
 
 struct rh_ctx {
   int device = 0;
@@ -565,5 +566,77 @@ int rh_force_2nd_spectrum(rh_ctx* ctx, int n2, const double* w2, const rh_c128* 
   RH_HIP(hipGetLastError());
   return RH_OK;
 }
+
+
+// ---------------------------------------------------------------- native design preparation
+int rh_prep_designs(int ndesign, const double* spec, const long long* spec_off, int nw, const double* w,
+                    const double* k, int nthreads, rh_prep** out) {
+  if (!out) return fail(RH_EINVAL, "rh_prep_designs: null out");
+  *out = nullptr;
+  if (ndesign < 0 || (ndesign > 0 && (!spec || !spec_off)) || nw < 2 || !w || !k)
+    return fail(RH_EINVAL, "rh_prep_designs: bad arguments (ndesign=%d, nw=%d)", ndesign, nw);
+  auto* p = new rh_prep();
+  p->res.resize(ndesign);
+  int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
+  nt = std::max(1, std::min({nt, 64, std::max(ndesign, 1)}));
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    for (int i = next++; i < ndesign; i = next++)
+      rhp::prep_one(spec + spec_off[i], spec_off[i + 1] - spec_off[i], nw, w, k, p->res[i]);
+  };
+  if (nt == 1) {
+    work();
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back(work);
+    for (auto& t : th) t.join();
+  }
+  for (int i = 0; i < ndesign; ++i)
+    if (!p->res[i].ok) {
+      const std::string e = p->res[i].err;
+      delete p;
+      return fail(RH_EINVAL, "rh_prep_designs: design %d: %s", i, e.c_str());
+    }
+  long long o = 0, mo = 0;
+  for (auto& r : p->res) {
+    p->off.push_back(o);
+    p->moff.push_back(mo);
+    o += (long long)r.packed.size();
+    mo += (long long)r.mstart.size();
+  }
+  p->off.push_back(o);
+  p->moff.push_back(mo);
+  *out = p;
+  return RH_OK;
+}
+
+int rh_prep_layout(const rh_prep* p, long long* info) {
+  if (!p || !info) return fail(RH_EINVAL, "rh_prep_layout: null argument");
+  const int nd = (int)p->res.size();
+  for (int i = 0; i < nd; ++i) {
+    long long* r = info + 5 * i;
+    r[0] = p->off[i];
+    r[1] = p->off[i + 1] - p->off[i];
+    r[2] = p->moff[i];
+    r[3] = p->res[i].nn;
+    r[4] = p->res[i].nm;
+  }
+  info[5 * nd] = p->off[nd];
+  info[5 * nd + 1] = p->moff[nd];
+  return RH_OK;
+}
+
+int rh_prep_copy(const rh_prep* p, double* packed, int* mstart, double* statics) {
+  if (!p || !packed || !mstart) return fail(RH_EINVAL, "rh_prep_copy: null argument");
+  for (size_t i = 0; i < p->res.size(); ++i) {
+    const auto& r = p->res[i];
+    std::copy(r.packed.begin(), r.packed.end(), packed + p->off[i]);
+    std::copy(r.mstart.begin(), r.mstart.end(), mstart + p->moff[i]);
+    if (statics) std::copy(r.statics, r.statics + 5 * 36, statics + 5 * 36 * i);
+  }
+  return RH_OK;
+}
+
+void rh_prep_free(rh_prep* p) { delete p; }
 
 }  // extern "C"

@@ -114,10 +114,15 @@ def lib():
                 "rh_force_2nd": [_p, ctypes.c_int, _p, _p, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p],
                 "rh_force_2nd_spectrum": [_p, ctypes.c_int, _p, _p, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p,
                                           _p],
+                "rh_prep_designs": [ctypes.c_int, _p, _p, ctypes.c_int, _p, _p, ctypes.c_int, ctypes.POINTER(_p)],
+                "rh_prep_layout": [_p, _p],
+                "rh_prep_copy": [_p, _p, _p, _p],
             }.items():
                 fn = getattr(L, name)
                 fn.argtypes = args
                 fn.restype = ctypes.c_int
+            L.rh_prep_free.argtypes = [_p]
+            L.rh_prep_free.restype = None
             L.rh_version.restype = ctypes.c_int
             L.rh_group_cases.argtypes = []
             L.rh_group_cases.restype = ctypes.c_int

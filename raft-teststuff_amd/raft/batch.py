@@ -15,6 +15,7 @@ import time
 
 import numpy as np
 
+from .hydro_math import get_from_dict
 from .model import Model
 from .solver import CaseSet, solve_batch
 
@@ -28,22 +29,28 @@ class DesignBatch:
     r6      : platform pose for the linearisation (default: the reference position)
     """
 
-    def __init__(self, designs, statics=None, r6=None, device=0, pool=None, light=False):
+    def __init__(self, designs, statics=None, r6=None, device=0, pool=None, light=False, native=False):
         """pool: optional multiprocessing pool (see host_pool) that prepares the designs on
         the host in parallel; results are identical to the serial path.
         light: keep only what the device side needs of each design (HostDesign: its tables,
         grid and site scalars) instead of the full Model; from a pool this ships ~40 KB per
-        design instead of ~150 KB of Python objects (the parent's unpickling was the cost)."""
+        design instead of ~150 KB of Python objects (the parent's unpickling was the cost).
+        native: prepare every design in librafthip on host threads (raft/native_prep.py,
+        rh_prep_designs; implies light): the pool, if any, only flattens the design dicts."""
         t0 = time.perf_counter()
         if isinstance(statics, dict) or statics is None:
             statics = [statics] * len(designs)
         if len(statics) != len(designs):
             raise ValueError("statics: one dict for all designs or one per design")
-        jobs = [(d, st, r6, device, light) for d, st in zip(designs, statics)]
-        if pool is not None and len(jobs) > 1:
-            self.models = pool.map(prepare_design, jobs, chunksize=max(1, len(jobs) // (4 * pool._processes)))
+        self._prepared = None
+        if native:
+            self.models = self._native(designs, statics, r6, device, pool)
         else:
-            self.models = [prepare_design(j) for j in jobs]
+            jobs = [(d, st, r6, device, light) for d, st in zip(designs, statics)]
+            if pool is not None and len(jobs) > 1:
+                self.models = pool.map(prepare_design, jobs, chunksize=max(1, len(jobs) // (4 * pool._processes)))
+            else:
+                self.models = [prepare_design(j) for j in jobs]
         self.fowts = [m if isinstance(m, HostDesign) else m.fowtList[0] for m in self.models]
         m0 = self.models[0]
         for m in self.models[1:]:
@@ -57,14 +64,49 @@ class DesignBatch:
         self.dds = self._upload(device)
         self.upload_seconds = time.perf_counter() - t0
 
+    def _native(self, designs, statics, r6, device, pool):
+        """rh_prep_designs over every design (raft/native_prep.py); returns HostDesign-like
+        records holding views of the one packed host array."""
+        from .hydro_math import wave_numbers
+        from .native_prep import PreparedDesigns
+        w = Model.frequency_grid(designs[0])
+        depth = get_from_dict(designs[0]["site"], "water_depth", dtype=float)
+        for d in designs[1:]:
+            if get_from_dict(d["site"], "water_depth", dtype=float) != depth or \
+                    not np.array_equal(Model.frequency_grid(d), w):
+                raise ValueError("all designs of a batch must share the frequency grid and the site")
+        k = wave_numbers(w, depth)
+        jobs = [(d, None if r6 is None else np.asarray(r6, dtype=float), st) for d, st in zip(designs, statics)]
+        if pool is not None and len(jobs) > 1:
+            specs = pool.map(_spec_job, jobs, chunksize=max(1, len(jobs) // (4 * pool._processes)))
+        else:
+            specs = [_spec_job(j) for j in jobs]
+        import os
+        nt = pool._processes if pool is not None else min(16, len(os.sched_getaffinity(0)))
+        P = self._prepared = PreparedDesigns(specs, w, k, nthreads=nt)
+        st0 = designs[0].get("settings", {})
+        nIter = get_from_dict(st0, "nIter", default=15, dtype=int)
+        XiStart = get_from_dict(st0, "XiStart", default=0.1, dtype=float)
+        return [NativeDesign(P, i, d, w, k, depth, nIter, XiStart, device) for i, d in enumerate(designs)]
+
     def _upload(self, device):
         """Every design's device tables in one host->device copy (plus one for the member
         ranges); each DeviceDesign holds views of its slices."""
         import torch
         from .prep import DeviceDesign, _torch
         _torch()
-        hs = [f.host_tables() for f in self.fowts]
         dev = torch.device("cuda", device)
+        if self._prepared is not None:     # native: already one packed host array
+            P = self._prepared
+            packed = torch.from_numpy(P.packed).to(dev)
+            mst = torch.from_numpy(P.mstart).to(dev)
+            dds = []
+            for i, f in enumerate(self.fowts):
+                o, n, mo, nn, nm = (int(x) for x in P.info[i])
+                f._dd = DeviceDesign(f, device=device, packed=packed[o:o + n], mstart=mst[mo:mo + nm + 1])
+                dds.append(f._dd)
+            return dds
+        hs = [f.host_tables() for f in self.fowts]
         packed = torch.tensor(np.concatenate([h["packed"] for h in hs]), dtype=torch.float64, device=dev)
         mst = torch.tensor(np.concatenate([h["mstart"] for h in hs]).astype(np.int32), dtype=torch.int32, device=dev)
         dds, off, moff = [], 0, 0
@@ -149,6 +191,28 @@ class HostDesign:
         st = dict(self.__dict__)
         st["_dd"] = None
         return st
+
+
+def _spec_job(job):
+    from .native_prep import design_spec
+    d, r6, st = job
+    return design_spec(d, r6=r6, statics=st)
+
+
+class NativeDesign(HostDesign):
+    """HostDesign of a natively prepared design (rh_prep_designs): its tables are views of
+    the batch's packed host array."""
+
+    def __init__(self, P, i, design, w, k, depth, nIter, XiStart, device):
+        site = design["site"]
+        self.nw, self.w, self.k, self.dw = len(w), w, k, w[1] - w[0]
+        self.depth = depth
+        self.rho_water = get_from_dict(site, "rho_water", default=1025.0)
+        self.g = get_from_dict(site, "g", default=9.81)
+        self.nIter, self.XiStart = nIter, XiStart
+        self.device_index = device
+        self._host = P.host_tables(i)
+        self._dd = None
 
 
 def _warm_worker(grids):

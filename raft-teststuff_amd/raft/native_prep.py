@@ -1,0 +1,235 @@
+"""Native per-design host preparation (rh_prep_designs, csrc/rh_prep.h): the design sweep's
+host path without per-design interpreter work.
+
+A design dict is flattened into one float64 spec record (design_spec: the parsed member,
+rotor and statics inputs, with the reference's input rules of raft/member.py and
+raft/hydro_math.get_from_dict); librafthip then builds members, statics, added mass and the
+device tables of every design on host threads (the work of Model/FOWT setup,
+raft/raft_model.py:30-170, raft/raft_fowt.py:291-565, 848-880, that raft/batch.py
+prepare_design does in Python).  The Python path stays the parity reference
+(tests/test_native_prep.py compares every table and matrix).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .hydro_math import get_from_dict
+
+MAGIC = 7301
+STATIC_KEYS = ("M_struc", "B_struc", "C_struc", "C_hydro", "C_moor")
+
+
+def _vec(d, key, n, default=None, index=None):
+    """get_from_dict(d, key, shape=n, default=default, index=index) as a list of n floats
+    (raft/hydro_math.py get_from_dict: scalars are tiled; with `index`, a 1-D list gives its
+    index-th entry tiled and a 2-D list its index-th column)."""
+    if key not in d:
+        if default is None:
+            raise ValueError(f"Key '{key}' not found in input file...")
+        return [float(default)] * n
+    val = d[key]
+    if not isinstance(val, (list, tuple, np.ndarray)):
+        return [float(val)] * n
+    if len(val) != n:
+        raise ValueError(f"Value for key '{key}' is not the expected size of {n} and is instead: {val}")
+    if index is None:
+        return [float(v) for v in val]
+    if not isinstance(val[0], (list, tuple, np.ndarray)):
+        if 0 <= index < len(val):
+            return [float(val[index])] * n
+        raise ValueError(f"Value for index '{index}' is not within the size of {val} (len={len(val)})")
+    return [float(v[index]) for v in val]
+
+
+def _pairs(d, key, n):
+    """get_from_dict(d, key, shape=[n, 2]) flattened (rectangular side lengths)."""
+    val = d[key]
+    if not isinstance(val, (list, tuple, np.ndarray)):
+        return [float(val)] * (2 * n)
+    a = np.asarray(val, dtype=float)
+    if a.shape == (n, 2):
+        return a.ravel().tolist()
+    if a.ndim == 1 and len(a) == 2:
+        return a.tolist() * n
+    raise ValueError(f"Value for key '{key}' is not a compatible size for target size of {[n, 2]} and is instead: {val}")
+
+
+def _scalar(d, key, default):
+    if key not in d:
+        return default
+    val = d[key]
+    if isinstance(val, (list, tuple, np.ndarray)):
+        raise ValueError(f"Value for key '{key}' is expected to be a scalar but instead is: {val}")
+    return val
+
+
+def _member_spec(mi, heads, dlsMax_default, potModMaster, is_platform):
+    """One reference member entry (all its heading copies) as a list of spec values; the
+    parsing of raft/member.py Member.__init__ (raft/raft_member.py:23-96)."""
+    potMod = bool(_scalar(mi, "potMod", False))
+    dls = mi.get("dlsMax")
+    if is_platform:
+        if potModMaster in [1]:
+            potMod = False
+        elif potModMaster in [2, 3]:
+            potMod = True
+        if dls is None:
+            dls = dlsMax_default
+    dlsMax = 5.0 if dls is None else float(np.atleast_1d(dls)[0])
+    st = [float(x) for x in mi["stations"]]
+    n = len(st)
+    if n < 2:
+        raise ValueError("At least two stations entries must be provided")
+    if sorted(st) != st:
+        raise ValueError(f"Member {mi['name']}: the station list is not in ascending order.")
+    shape = str(mi["shape"])[0].lower()
+    if shape not in ("c", "r"):
+        raise ValueError("The only allowable shape strings are circular and rectangular")
+    circ = shape == "c"
+    mcf = bool(_scalar(mi, "MCF", False)) and circ
+    dd = _vec(mi, "d", n) if circ else _pairs(mi, "d", n)
+    has_t = "t" in mi
+    t = _vec(mi, "t", n) if has_t else []
+    fill = _vec(mi, "l_fill", n - 1, default=0)
+    for i in range(n - 1):
+        if fill[i] < 0:
+            raise Exception(f"Member {mi['name']}: ballast level in section {i+1} is negative.")
+        if fill[i] > st[i + 1] - st[i]:
+            raise Exception(f"Member {mi['name']}: ballast level in section {i+1} exceeds section length."
+                            + f" ({fill[i]} > {st[i+1] - st[i]}).")
+    rf = mi.get("rho_fill", 1025)
+    if not isinstance(rf, (list, tuple, np.ndarray)):
+        rho_fill = [float(rf)] * (n - 1)
+    elif len(rf) == n - 1:
+        rho_fill = [float(x) for x in rf]
+    else:
+        raise Exception(f"Member {mi['name']}: the number of provided ballast densities (rho_fill) must be 1 "
+                        "less than the number of stations.")
+    cs = mi.get("cap_stations", [])
+    cap_st = [float(x) for x in np.atleast_1d(cs)]
+    nc = len(cap_st)
+    cap_t = _vec(mi, "cap_t", nc) if nc else []
+    cap_d = _vec(mi, "cap_d_in", nc) if nc else []
+    head = [int(mi["type"]), 1.0 if circ else 0.0, 1.0 if potMod else 0.0, 1.0 if mcf else 0.0,
+            1.0 if str(mi["name"]) == "nacelle" else 0.0, n, nc, len(heads), 1.0 if has_t else 0.0,
+            float(_scalar(mi, "gamma", 0.0)), dlsMax, float(_scalar(mi, "rho_shell", 8500.))]
+    return (head + [float(x) for x in mi["rA"]] + [float(x) for x in mi["rB"]] + list(heads) + st + dd + t + fill
+            + rho_fill + _vec(mi, "Cd_q", n, 0.0) + _vec(mi, "Cd", n, 0.6, 0) + _vec(mi, "Cd", n, 0.6, 1)
+            + _vec(mi, "CdEnd", n, 0.6) + _vec(mi, "Ca_q", n, 0.0) + _vec(mi, "Ca", n, 0.97, 0)
+            + _vec(mi, "Ca", n, 0.97, 1) + _vec(mi, "CaEnd", n, 0.6) + cap_st + cap_t + cap_d)
+
+
+def design_spec(design, r6=None, statics=None, heading_adjust=0.0):
+    """The spec record of one single-FOWT design (layout: csrc/rh_prep.h).  statics: the
+    FOWT.setStatics entries that override the computed ones (and C_moor, MoorPy's stiffness)."""
+    site, plat = design["site"], design["platform"]
+    rho = get_from_dict(site, "rho_water", default=1025.0)
+    g = get_from_dict(site, "g", default=9.81)
+    potModMaster = get_from_dict(plat, "potModMaster", dtype=int, default=0)
+    dlsMax = get_from_dict(plat, "dlsMax", default=5.0)
+    blocks = []
+    nmemb = 0
+    for mi in plat["members"]:
+        hd = mi.get("heading", 0.0)
+        hd = hd if isinstance(hd, (list, tuple, np.ndarray)) else [hd]
+        blocks += _member_spec(mi, [float(h) + heading_adjust for h in hd], dlsMax, potModMaster, True)
+        nmemb += 1
+    rots = []
+    turb = design.get("turbine")
+    if turb:
+        nrot = get_from_dict(turb, "nrotors", dtype=int, shape=0, default=1)
+        for key in ("tower", "nacelle"):
+            ms = turb.get(key)
+            if ms is not None:
+                for mem in (ms if isinstance(ms, list) else [ms] * nrot):
+                    blocks += _member_spec(mem, [0.0], 5.0, 0, False)
+                    nmemb += 1
+        hhub = np.atleast_1d(get_from_dict(turb, "hHub", shape=-1, default=100.0))
+        if np.any(hhub < 0):
+            raise NotImplementedError("underwater rotors are outside the accelerated path")
+        if all(k in turb for k in ("mRNA", "IxRNA", "IrRNA", "xCG_RNA", "overhang", "shaft_tilt")):
+            # the RNA inputs (raft/statics.py RNA.__init__, raft/raft_rotor.py:42-111); the hub
+            # height correction r_rel[2] = hHub - q_z overhang is applied in rh_prep.h
+            if "rRNA" in turb:
+                rr = get_from_dict(turb, "rRNA", shape=[nrot, 3])
+            elif nrot > 1:
+                raise Exception("For designs with more than one rotor, the RNA reference point must be specified "
+                                "for each of them.")
+            else:
+                rr = [[0.0, 0.0, 100.0]]
+            cols = [_vec(turb, k, nrot) for k in ("mRNA", "IxRNA", "IrRNA", "xCG_RNA", "overhang")]
+            tilt, toe = _vec(turb, "shaft_tilt", nrot), _vec(turb, "shaft_toe", nrot, 0)
+            yaw = _vec(turb, "yaw_mode", nrot, 0)
+            hh = _vec(turb, "hHub", nrot) if "hHub" in turb else [0.0] * nrot
+            for ir in range(nrot):
+                rots.append([c[ir] for c in cols] + [tilt[ir] * np.pi / 180, toe[ir] * np.pi / 180, int(yaw[ir]),
+                                                     *[float(x) for x in rr[ir]], 1.0 if "hHub" in turb else 0.0,
+                                                     hh[ir]])
+        elif nrot:
+            if not statics or not all(k in statics for k in ("M_struc", "C_struc", "C_hydro")):
+                raise ValueError("turbine: mRNA, IxRNA, IrRNA, xCG_RNA, overhang and shaft_tilt are required")
+    statics = dict(statics or {})
+    moor = design.get("mooring")
+    if moor and "C_moor" not in statics:
+        # this FOWT's own mooring stiffness at the pose (raft/fowt.py setPosition with
+        # raft/mooring.py, MoorPy in the reference: raft/raft_fowt.py:166-189, 275-288)
+        from .mooring import MooringSystem
+        ms = MooringSystem.from_yaml(moor)
+        ms.transform(trans=[0.0, 0.0], rot=heading_adjust)
+        ms.initialize()
+        ms.set_body_positions([np.zeros(6) if r6 is None else np.asarray(r6, dtype=float)])
+        statics["C_moor"] = ms.coupled_stiffness_analytic()
+    hdr = [MAGIC, nmemb, len(rots), rho, g, *(np.zeros(6) if r6 is None else np.asarray(r6, dtype=float)),
+           *[1.0 if k in statics else 0.0 for k in STATIC_KEYS]]
+    given = [np.asarray(statics[k], dtype=float).ravel() for k in STATIC_KEYS if k in statics]
+    return np.concatenate([np.asarray(hdr, dtype=float), *given, np.asarray(blocks, dtype=float),
+                           np.asarray(rots, dtype=float).ravel()])
+
+
+class PreparedDesigns:
+    """Host tables of many designs from one rh_prep_designs call: `packed` (every design's
+    real-valued tables back to back, the layout of raft/prep.py host_tables), `mstart`,
+    and per design (offset, length, mstart offset, nn, nm) in `info`; `statics` [nd, 5, 6, 6]
+    = M_struc, B_struc, C_struc, C_hydro, A_hydro_morison."""
+
+    def __init__(self, specs, w, k, nthreads=0):
+        L = N.lib()
+        nd = len(specs)
+        off = np.zeros(nd + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(s) for s in specs])
+        flat = np.ascontiguousarray(np.concatenate(specs) if nd else np.zeros(0))
+        w = np.ascontiguousarray(w, dtype=float)
+        k = np.ascontiguousarray(k, dtype=float)
+        h = ctypes.c_void_p()
+        N.check(L.rh_prep_designs(nd, flat.ctypes.data, off.ctypes.data, len(w), w.ctypes.data, k.ctypes.data,
+                                  int(nthreads), ctypes.byref(h)), "rh_prep_designs")
+        try:
+            info = np.zeros(5 * nd + 2, dtype=np.int64)
+            N.check(L.rh_prep_layout(h, info.ctypes.data), "rh_prep_layout")
+            self.packed = np.empty(int(info[5 * nd]), dtype=float)
+            self.mstart = np.empty(int(info[5 * nd + 1]), dtype=np.int32)
+            self.statics = np.empty([nd, 5, 6, 6], dtype=float)
+            N.check(L.rh_prep_copy(h, self.packed.ctypes.data, self.mstart.ctypes.data, self.statics.ctypes.data),
+                    "rh_prep_copy")
+        finally:
+            L.rh_prep_free(h)
+        self.info = info[:5 * nd].reshape(nd, 5)
+        self.nw = len(w)
+
+    def __len__(self):
+        return len(self.info)
+
+    def host_tables(self, i):
+        """Design i's tables in the form of raft/prep.py host_tables (views of `packed`)."""
+        o, n, mo, nn, nm = (int(x) for x in self.info[i])
+        nw = self.nw
+        shapes = [("w", (nw,)), ("k", (nw,)), ("node", (N.NF_COUNT, max(nn, 1))), ("memb", (N.MF_COUNT, max(nm, 1))),
+                  ("M", (6, 6)), ("B", (6, 6)), ("C", (6, 6))]
+        layout, off = {}, 0
+        for name, shp in shapes:
+            layout[name] = (off, shp)
+            off += int(np.prod(shp))
+        assert off == n
+        return dict(packed=self.packed[o:o + n], layout=layout, imat=None, mstart=self.mstart[mo:mo + nm + 1],
+                    nn=nn, nm=nm, per_bin=False)

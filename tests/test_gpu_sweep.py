@@ -51,14 +51,18 @@ def _check_case(res, j, T, ic):
         np.testing.assert_allclose(res["std"][j, i], T[f"out_{dof}_std"][ic], rtol=RTOL, atol=RTOL * smax)
 
 
-def test_sweep_variants_one_launch_match_reference():
-    """Native per-design preparation + one launch over 3 designs x 2 sea states."""
+@pytest.mark.parametrize("native", [False, True])
+def test_sweep_variants_one_launch_match_reference(native):
+    """The product's per-design preparation (Python host path, or librafthip's
+    rh_prep_designs) + one launch over 3 designs x 2 sea states."""
     from raft.batch import DesignBatch
     designs, cmoor, idx, cases, refs = _sweep_inputs()
-    B = DesignBatch(designs, statics=cmoor)
-    for f, (T, _) in zip(B.fowts, [refs[0], refs[2], refs[4]]):
-        for k in ["M_struc", "C_struc", "C_hydro"]:
-            assert np.abs(getattr(f, k) - T[k]).max() <= 1e-12 * np.abs(T[k]).max(), k
+    B = DesignBatch(designs, statics=cmoor, native=native)
+    for i, (T, _) in enumerate([refs[0], refs[2], refs[4]]):
+        for j, k in enumerate(["M_struc", "B_struc", "C_struc", "C_hydro"]):
+            got = B._prepared.statics[i, j] if native else getattr(B.fowts[i], k)
+            if k in T:
+                assert np.abs(got - T[k]).max() <= 1e-12 * np.abs(T[k]).max(), k
     res = B.solve(idx, cases).host()
     for j, (T, ic) in enumerate(refs):
         _check_case(res, j, T, ic)

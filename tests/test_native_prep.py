@@ -1,0 +1,112 @@
+"""CPU: the native per-design preparation (rh_prep_designs, csrc/rh_prep.h) against the
+Python host path it restates (raft/batch.py prepare_design -> raft/member.py,
+raft/statics.py, raft/prep.py, itself pinned to the reference's statics goldens and solves).
+
+Sizes, member ranges and the frequency grid are expected bit for bit, every table field
+within 1e-14 of its largest entry (single entries may differ by an ulp where NumPy leaves
+the summation order of 3x3 products and norms to BLAS).  No GPU: librafthip loads and runs
+its host code only."""
+import numpy as np
+import pytest
+
+from conftest import load_design
+
+C_MOOR = np.diag([7e4, 7e4, 2e4, 1e7, 1e7, 1e8])
+
+
+def _python_tables(d, st, r6=None):
+    from raft.batch import prepare_design
+    m = prepare_design((d, st, r6, 0, False))
+    f = m.fowtList[0]
+    return f.host_tables(), f
+
+
+def _compare(h, n):
+    """Same sizes and member ranges, w and k bit for bit; every table field (node-table rows
+    one by one) within 1e-14 of its largest entry: rotated members reach their axes through
+    3x3 products and norms whose summation order NumPy leaves to BLAS, so single entries may
+    differ by an ulp."""
+    assert (h["nn"], h["nm"]) == (n["nn"], n["nm"])
+    np.testing.assert_array_equal(h["mstart"], n["mstart"])
+    for name, (o, shp) in h["layout"].items():
+        a = h["packed"][o:o + int(np.prod(shp))].reshape(shp)
+        no = n["layout"][name][0]
+        b = n["packed"][no:no + a.size].reshape(shp)
+        if name in ("w", "k"):
+            np.testing.assert_array_equal(a, b)
+            continue
+        rows = a if a.ndim == 2 and name in ("node", "memb") else a.reshape(1, -1)
+        brow = b if a.ndim == 2 and name in ("node", "memb") else b.reshape(1, -1)
+        for i, (x, y) in enumerate(zip(rows, brow)):
+            tol = 1e-14 * max(np.abs(x).max(), 1.0)   # unit vectors: rounding zeros (1e-48 vs 3e-33)
+            assert np.abs(x - y).max() <= tol, (name, i, np.abs(x - y).max(), tol)
+
+
+def _native(designs, statics, r6=None):
+    from raft.hydro_math import wave_numbers
+    from raft.model import Model
+    from raft.native_prep import PreparedDesigns, design_spec
+    w = Model.frequency_grid(designs[0])
+    k = wave_numbers(w, float(designs[0]["site"]["water_depth"]))
+    return PreparedDesigns([design_spec(d, r6=r6, statics=s) for d, s in zip(designs, statics)], w, k, nthreads=4)
+
+
+@pytest.mark.parametrize("name", ["VolturnUS-S_example", "VolturnUS-S_test", "OC3spar", "OC3spar_test"])
+def test_native_tables_and_statics_match_python(name):
+    d = load_design(name)
+    st = {"C_moor": C_MOOR}
+    h, f = _python_tables(d, st)
+    P = _native([d], [st])
+    _compare(h, P.host_tables(0))
+    for j, key in enumerate(["M_struc", "B_struc", "C_struc", "C_hydro", "A_hydro_morison"]):
+        ref = getattr(f, key)
+        assert np.abs(P.statics[0, j] - ref).max() <= 1e-14 * max(np.abs(ref).max(), 1e-300), key
+
+
+def test_native_sweep_variants_match_python():
+    """C5 parametersweep variants (raft/sweep.py), every one prepared natively in one call."""
+    from raft.sweep import sweep_multipliers, sweep_variant
+    base = load_design("VolturnUS-S_example")
+    base["settings"]["min_freq"] = 0.0002
+    designs = [sweep_variant(base, m) for m in sweep_multipliers(6, seed=5)]
+    st = {"C_moor": C_MOOR}
+    P = _native(designs, [st] * len(designs))
+    for i, d in enumerate(designs):
+        _compare(_python_tables(d, st)[0], P.host_tables(i))
+
+
+def test_native_pose_and_mooring_stiffness():
+    """A displaced, rotated pose (members, RNA and hydrostatics move) and the mooring
+    stiffness computed from the design's own mooring system (raft/mooring.py)."""
+    d = load_design("VolturnUS-S_example")
+    r6 = np.array([3.0, -2.0, 0.5, 0.02, -0.03, 0.1])
+    h, f = _python_tables(d, None, r6=r6)
+    P = _native([d], [None], r6=r6)
+    _compare(h, P.host_tables(0))
+
+
+def test_native_statics_given_override():
+    """Given M_struc / C_struc / C_hydro (setStatics) replace the computed ones."""
+    d = load_design("OC3spar")
+    rng = np.random.default_rng(3)
+    st = {k: rng.normal(size=(6, 6)) for k in ("M_struc", "C_struc", "C_hydro", "C_moor")}
+    h, f = _python_tables(d, st)
+    P = _native([d], [st])
+    _compare(h, P.host_tables(0))
+
+
+def test_native_refuses_maccamy_fuchs_and_bad_specs():
+    from raft import _native as N
+    from raft.native_prep import PreparedDesigns, design_spec
+    d = load_design("OC4semi-RAFT_QTF")
+    w = np.arange(1, 11) * 0.1
+    with pytest.raises(ValueError, match="MacCamy-Fuchs"):
+        PreparedDesigns([design_spec(d, statics={"C_moor": C_MOOR})], w, w)
+    s = design_spec(load_design("OC3spar"), statics={"C_moor": C_MOOR})
+    with pytest.raises(ValueError, match="spec record"):
+        PreparedDesigns([s[:-1]], w, w)
+    bad = s.copy()
+    bad[0] = 1.0
+    with pytest.raises(ValueError, match="magic"):
+        PreparedDesigns([bad], w, w)
+    assert N.lib().rh_prep_layout(None, None) == N.RH_EINVAL

@@ -20,10 +20,11 @@ if __name__ == "__main__":
     variants = [sweep_variant(base, mult[i]) for i in range(250)]
     idx, cases = sweep_cases(250, sea_state_grid())
     torch.zeros(1, device="cuda")
-    for rep in range(2):
+    for rep in range(3):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        B = DesignBatch(variants, statics={"C_moor": C_moor}, device=0, pool=pool, light=True)
+        B = DesignBatch(variants, statics={"C_moor": C_moor}, device=0, pool=pool,
+                        native=os.environ.get("C5_NATIVE", "1") == "1", light=True)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         cs = B.case_set(idx, cases)
