@@ -192,6 +192,12 @@ int rh_set_qtf_path(rh_ctx* ctx, int path);
 int rh_wave_tables(rh_ctx* ctx, const rh_design* d, const double* beta,
                    rh_c128* uhat, rh_c128* finer, rh_c128* kproj, rh_stream stream);
 
+/* rh_wave_tables for many designs in ONE launch: design i tabulates designs[i].nhead headings
+ * beta[i * hstride + h] (rad) into the tables its descriptor points at (uhat, finer, kproj,
+ * written).  The per-design part of a design sweep (C5) as a single grid. */
+int rh_wave_tables_batch(rh_ctx* ctx, const rh_design* designs, int ndesign, const double* beta, int hstride,
+                         rh_stream stream);
+
 /* Drag-linearisation fixed point + per-bin Z assemble / pivoted LU solve for a batch of
  * cases, one workgroup per case.  Replaces Model.solveDynamics' per-FOWT iteration
  * (raft/raft_model.py:877-1013) including FOWT.calcHydroLinearization (raft/raft_fowt.py:

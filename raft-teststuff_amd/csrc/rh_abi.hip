@@ -193,6 +193,28 @@ int rh_wave_tables(rh_ctx* ctx, const rh_design* d, const double* beta, rh_c128*
   return RH_OK;
 }
 
+int rh_wave_tables_batch(rh_ctx* ctx, const rh_design* designs, int ndesign, const double* beta, int hstride,
+                         rh_stream stream) {
+  if (!ctx || !designs || !beta) return fail(RH_EINVAL, "rh_wave_tables_batch: null argument");
+  if (ndesign < 1) return ndesign == 0 ? RH_OK : fail(RH_EINVAL, "rh_wave_tables_batch: ndesign=%d", ndesign);
+  int nwmax = 0, nhmax = 0;
+  for (int i = 0; i < ndesign; ++i) {
+    const rh_design& d = designs[i];
+    if (int r = check_design(d, false)) return r;
+    if (d.nhead < 1 || d.nhead > hstride)
+      return fail(RH_EINVAL, "rh_wave_tables_batch: design %d: nhead=%d outside [1, hstride=%d]", i, d.nhead, hstride);
+    if (!d.uhat || !d.finer || !d.kproj) return fail(RH_EINVAL, "rh_wave_tables_batch: design %d: null table", i);
+    nwmax = d.nw > nwmax ? d.nw : nwmax;
+    nhmax = d.nhead > nhmax ? d.nhead : nhmax;
+  }
+  RH_HIP(hipSetDevice(ctx->device));
+  const hipStream_t s = (hipStream_t)stream;
+  if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
+  dim3 grid((nwmax + 63) / 64, nhmax, ndesign);
+  hipLaunchKernelGGL(rh::k_wave_tables_batch, grid, dim3(64 * rh::kWtN), 0, s, ctx->d_designs, beta, hstride);
+  return designs_used(ctx, s);
+}
+
 int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_cases* cases,
                    const rh_solve_out* out, rh_stream stream) {
   if (!ctx || !designs || !cases || !out) return fail(RH_EINVAL, "rh_solve_cases: null argument");

@@ -83,14 +83,12 @@ __global__ __launch_bounds__(256) void k_sea_state(int nw, const double* __restr
 // loop: one design's tables (1000 bins) are 128 waves instead of 16.
 // ----------------------------------------------------------------------------------------
 constexpr int kWtN = 8;
-__global__ __launch_bounds__(64 * kWtN) void k_wave_tables(rh_design d, const double* __restrict__ beta,
-                                                            rh_c128* __restrict__ uhat, rh_c128* __restrict__ finer,
-                                                            rh_c128* __restrict__ kproj) {
-  __shared__ cd fs[kWtN][6][64];
+__device__ __forceinline__ void wave_tables_body(const rh_design& d, const double* __restrict__ beta, int h, int bx,
+                                                 rh_c128* __restrict__ uhat, rh_c128* __restrict__ finer,
+                                                 rh_c128* __restrict__ kproj, cd (&fs)[kWtN][6][64]) {
   const int lb = (int)threadIdx.x & 63, slot = (int)threadIdx.x >> 6;
-  const int h = blockIdx.y;
   const int nw = d.nw, nn = d.nn;
-  const int b0 = blockIdx.x * 64 + lb;
+  const int b0 = bx * 64 + lb;
   const bool okb = b0 < nw;
   const int b = okb ? b0 : nw - 1;           // pad lanes compute a valid bin and store nothing
   const double w = d.w[b], k = d.k[b], hd = d.depth;
@@ -183,6 +181,26 @@ __global__ __launch_bounds__(64 * kWtN) void k_wave_tables(rh_design d, const do
   rh_c128* Fo = finer + (size_t)h * 6 * nw + b;
 #pragma unroll
   for (int c = 0; c < 6; ++c) st(Fo + c * nw, F[c]);
+}
+
+__global__ __launch_bounds__(64 * kWtN) void k_wave_tables(rh_design d, const double* __restrict__ beta,
+                                                            rh_c128* __restrict__ uhat, rh_c128* __restrict__ finer,
+                                                            rh_c128* __restrict__ kproj) {
+  __shared__ cd fs[kWtN][6][64];
+  wave_tables_body(d, beta, blockIdx.y, blockIdx.x, uhat, finer, kproj, fs);
+}
+
+// Every design of a batch in one launch (rh_wave_tables_batch): blockIdx.z = design, its
+// headings beta[z * hstride + h] (h < its nhead), its tables at the pointers of its descriptor.
+// A design sweep's tables are then one grid of ndesign x nhead x bins/64 workgroups instead of
+// ndesign launches of 16 workgroups each.
+__global__ __launch_bounds__(64 * kWtN) void k_wave_tables_batch(const DevDesign* __restrict__ designs,
+                                                                  const double* __restrict__ beta, int hstride) {
+  __shared__ cd fs[kWtN][6][64];
+  const rh_design& d = designs[blockIdx.z].d;
+  if ((int)blockIdx.y >= d.nhead || (int)blockIdx.x * 64 >= d.nw) return;   // uniform per workgroup
+  wave_tables_body(d, beta + (size_t)blockIdx.z * hstride, blockIdx.y, blockIdx.x, const_cast<rh_c128*>(d.uhat),
+                   const_cast<rh_c128*>(d.finer), const_cast<rh_c128*>(d.kproj), fs);
 }
 
 // ----------------------------------------------------------------------------------------

@@ -84,6 +84,7 @@ def lib():
                 "rh_ctx_create": [ctypes.c_int, ctypes.POINTER(_p)],
                 "rh_ctx_destroy": [_p],
                 "rh_wave_tables": [_p, ctypes.POINTER(RhDesign), _p, _p, _p, _p, _p],
+                "rh_wave_tables_batch": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, _p, ctypes.c_int, _p],
                 "rh_solve_cases": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.POINTER(RhCases),
                                    ctypes.POINTER(RhSolveOut), _p],
                 "rh_heading_response": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.c_int, _p, _p, _p, _p,

@@ -139,6 +139,14 @@ class DesignBatch:
             gm.append(float(one(c, "wave_gamma", 0)))
         return CaseSet(np.asarray(design_idx, dtype=np.int32), hd, sp, Hs, Tp, gm)
 
+    def case_set_grid(self, design_idx, state_idx, sea_states):
+        """CaseSet of cases given as (design index, index into `sea_states`): a sweep's
+        design x sea-state product without one case dict per case."""
+        cs0 = self.case_set(np.zeros(len(sea_states), dtype=np.int32), sea_states)   # each sea state parsed once
+        si = np.asarray(state_idx, dtype=np.int64)
+        return CaseSet(np.asarray(design_idx, dtype=np.int32), cs0.heading[si], cs0.spectrum[si], cs0.Hs[si],
+                       cs0.Tp[si], cs0.gamma[si])
+
     def solve(self, design_idx, cases, tol=0.01, want=("psd", "std", "zeta", "B_drag"), prepared=None):
         """Drag fixed point + response of every case in one device call.  Returns the
         BatchResult (device tensors, stream-ordered): Xi [n,6,nw], iters, status, ..."""
@@ -216,6 +224,7 @@ class NativeDesign(HostDesign):
 
 
 def _warm_worker(grids):
+    from . import native_prep  # noqa: F401  (the spec writer of DesignBatch(native=True))
     from .hydro_math import wave_numbers
     for w, depth in grids:
         wave_numbers(w, depth)

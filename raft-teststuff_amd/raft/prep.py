@@ -133,8 +133,9 @@ class DeviceDesign:
             raise ValueError("DeviceDesign: packed slice does not match the design's tables")
         self._packed = packed if packed is not None else torch.tensor(h["packed"], dtype=torch.float64,
                                                                         device=self.device)
-        for name, (off, shape) in h["layout"].items():   # contiguous views of the one upload
-            setattr(self, name, self._packed[off:off + int(np.prod(shape))].view(*shape))
+        # w, k, node, memb, M, B, C: contiguous views of the one upload, made on first use
+        # (__getattr__); the descriptor takes their addresses from the layout directly
+        self._layout = h["layout"]
         imat = h["imat"]
         self.imat = torch.tensor(imat, dtype=torch.complex128, device=self.device) if imat is not None else None
         self.mstart = mstart if mstart is not None else torch.tensor(h["mstart"], dtype=torch.int32, device=self.device)
@@ -144,18 +145,39 @@ class DeviceDesign:
         self.finer = None
         self.kproj = None
 
+    def __getattr__(self, name):
+        lay = self.__dict__.get("_layout")
+        if lay is None or name not in lay:
+            raise AttributeError(name)
+        off, shape = lay[name]
+        v = self._packed[off:off + int(np.prod(shape))].view(*shape)
+        self.__dict__[name] = v
+        return v
+
+    def _addr(self, name):
+        return ctypes.c_void_p(self._packed.data_ptr() + 8 * self._layout[name][0])
+
     def struct(self):
+        """The rh_design descriptor of the current tables (cached until they change)."""
+        st = getattr(self, "_struct", None)
+        if st is not None and st[0] is self.kproj:
+            return st[1]
+        d = self._make_struct()
+        self._struct = (self.kproj, d)
+        return d
+
+    def _make_struct(self):
         d = N.RhDesign()
         d.nw, d.nn = self.nw, self.nn
         d.nhead = 0 if self.headings is None else len(self.headings)
         d.mb_per_bin = 1 if self.per_bin else 0
         d.dw, d.depth, d.rho, d.g = self.dw, self.depth, self.rho, self.g
         d.pdyn_rho_g = 1025.0 * 9.81   # getWaveKin defaults (raft/helpers.py:105, raft/raft_fowt.py:1109)
-        d.w, d.k, d.node = N.ptr(self.w), N.ptr(self.k), N.ptr(self.node)
-        d.nm, d.memb, d.mstart = self.nm, N.ptr(self.memb), N.ptr(self.mstart)
+        d.w, d.k, d.node = self._addr("w"), self._addr("k"), self._addr("node")
+        d.nm, d.memb, d.mstart = self.nm, self._addr("memb"), N.ptr(self.mstart)
         d.imat_mcf = N.ptr(self.imat)
         d.uhat, d.finer, d.kproj = N.ptr(self.uhat), N.ptr(self.finer), N.ptr(self.kproj)
-        d.M, d.B, d.C = N.ptr(self.M), N.ptr(self.B), N.ptr(self.C)
+        d.M, d.B, d.C = self._addr("M"), self._addr("B"), self._addr("C")
         return d
 
     def ensure_headings(self, betas):
@@ -191,3 +213,53 @@ class DeviceDesign:
         s = stream if stream is not None else N.stream_handle(self.torch, self.device)
         N.check(N.lib().rh_wave_tables(N.context(self.dev_index), ctypes.byref(d), N.ptr(self._beta_keep),
                                        N.ptr(self.uhat), N.ptr(self.finer), N.ptr(self.kproj), s), "rh_wave_tables")
+
+
+def tabulate_batch(designs, design_idx, betas):
+    """Wave tables of every (design, heading) pair a batch needs, in ONE rh_wave_tables_batch
+    launch, for designs that have none yet (a fresh design sweep).  Returns the heading
+    index of every case in its design's tables.  Tables of all designs share three device
+    allocations; each DeviceDesign holds views."""
+    torch = designs[0].torch
+    dev = designs[0].device
+    n = len(design_idx)
+    order = np.lexsort((betas, design_idx))
+    ds, bs = design_idx[order], betas[order]
+    new = np.ones(n, dtype=bool)
+    new[1:] = (ds[1:] != ds[:-1]) | (bs[1:] != bs[:-1])
+    grp = np.cumsum(new) - 1                       # unique (design, heading) pair per sorted case
+    ud, ub = ds[new], bs[new]
+    first = np.ones(len(ud), dtype=bool)
+    first[1:] = ud[1:] != ud[:-1]
+    start = np.maximum.accumulate(np.where(first, np.arange(len(ud)), 0))
+    head = np.empty(n, dtype=np.int32)
+    head[order] = (np.arange(len(ud)) - start)[grp]
+    di = ud[first]                                 # designs involved, with their heading runs
+    bounds = np.append(np.nonzero(first)[0], len(ud))
+    nh = np.diff(bounds)
+    hstride = int(nh.max())
+    sel = [designs[int(i)] for i in di]
+    nw = sel[0].nw
+    rows = [int(k) * max(d.nn, 1) * 3 * nw for d, k in zip(sel, nh)]
+    c128 = dict(dtype=torch.complex128, device=dev)
+    U = torch.empty([sum(rows)], **c128)
+    K = torch.empty([sum(rows)], **c128)
+    Fi = torch.empty([int(nh.sum()) * 6 * nw], **c128)
+    bm = np.zeros([len(sel), hstride])
+    ou = of = 0
+    for j, (d, k) in enumerate(zip(sel, nh)):
+        k = int(k)
+        hs = ub[bounds[j]:bounds[j + 1]]
+        bm[j, :k] = hs
+        d.headings = tuple(float(b) for b in hs)
+        shp = [k, max(d.nn, 1), 3, nw]
+        d.uhat, d.kproj = U[ou:ou + rows[j]].view(shp), K[ou:ou + rows[j]].view(shp)
+        d.finer = Fi[of:of + k * 6 * nw].view(k, 6, nw)
+        ou, of = ou + rows[j], of + k * 6 * nw
+    beta_t = torch.tensor(bm, dtype=torch.float64, device=dev)
+    for j, d in enumerate(sel):
+        d._beta_keep = beta_t[j, :int(nh[j])]
+    arr = (N.RhDesign * len(sel))(*[d.struct() for d in sel])
+    N.check(N.lib().rh_wave_tables_batch(N.context(sel[0].dev_index), arr, len(sel), N.ptr(beta_t), hstride,
+                                         N.stream_handle(torch, dev)), "rh_wave_tables_batch")
+    return head

@@ -29,9 +29,13 @@ class CaseSet:
         self.n = n
         self.design_idx = np.broadcast_to(np.asarray(design_idx, dtype=np.int32), (n,)).copy()
         self.heading = np.asarray(heading, dtype=float)
-        sp = np.broadcast_to(np.asarray(spectrum, dtype=object), (n,))
-        self.spectrum = np.array([s if isinstance(s, (int, np.integer)) else N.SPECTRUM_CODES[str(s)] for s in sp],
-                                 dtype=np.int32)
+        spa = np.asarray(spectrum)
+        if spa.dtype.kind in "iu":     # integer codes already
+            self.spectrum = np.broadcast_to(spa.astype(np.int32), (n,)).copy()
+        else:
+            sp = np.broadcast_to(np.asarray(spectrum, dtype=object), (n,))
+            self.spectrum = np.array([s if isinstance(s, (int, np.integer)) else N.SPECTRUM_CODES[str(s)] for s in sp],
+                                     dtype=np.int32)
         self.Hs = np.broadcast_to(np.asarray(Hs, dtype=float), (n,)).copy()
         self.Tp = np.broadcast_to(np.asarray(Tp, dtype=float), (n,)).copy()
         self.gamma = np.broadcast_to(np.asarray(gamma, dtype=float), (n,)).copy()
@@ -116,15 +120,19 @@ def prepare_batch(designs, cases):
     need.  Reusable across repeated solves of the same batch (bench steady state)."""
     torch = designs[0].torch
     dev = designs[0].device
-    head = np.zeros(cases.n, dtype=np.int32)
-    for di, d in enumerate(designs):
-        sel = np.nonzero(cases.design_idx == di)[0]
-        if len(sel) == 0:
-            continue
-        betas = cases.heading[sel] * DEG2RAD
-        head[sel] = d.ensure_headings(betas)
-    if cases.design_idx.min() < 0 or cases.design_idx.max() >= len(designs):
+    if cases.n and (cases.design_idx.min() < 0 or cases.design_idx.max() >= len(designs)):
         raise ValueError("design index out of range")
+    used = np.unique(cases.design_idx)
+    if len(used) > 1 and all(designs[int(i)].uhat is None for i in used):
+        # a fresh multi-design batch (a sweep): every table in one launch
+        from .prep import tabulate_batch
+        head = tabulate_batch(designs, cases.design_idx, cases.heading * DEG2RAD)
+    else:
+        head = np.zeros(cases.n, dtype=np.int32)
+        for di in used:
+            d = designs[int(di)]
+            sel = np.nonzero(cases.design_idx == di)[0]
+            head[sel] = d.ensure_headings(cases.heading[sel] * DEG2RAD)
     # design-major, then heading; within a (design, heading) run by sea state, so that the
     # cases solved in lock-step by one workgroup tend to need the same number of iterations
     order = np.lexsort((cases.Tp, cases.Hs, head, cases.design_idx)).astype(np.int32)

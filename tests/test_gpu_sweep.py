@@ -182,3 +182,35 @@ def test_farm_batch_matches_reference_and_oracle():
         x[:, 3:] *= 57.29577951308232
         np.testing.assert_allclose(r["psd"][:, i], 0.5 * np.abs(x) ** 2 / dw, rtol=1e-12, atol=1e-300)
         np.testing.assert_allclose(r["std"][:, i], np.sqrt(0.5 * np.sum(np.abs(x) ** 2, axis=2)), rtol=1e-12)
+
+
+def test_batched_wave_tables_equal_per_design_tables():
+    """rh_wave_tables_batch (one launch for a sweep) writes the same bits as rh_wave_tables
+    per design, for designs with different node counts and two headings each."""
+    import torch
+    from raft.batch import DesignBatch
+    from raft.hydro_math import DEG2RAD
+    from raft.sweep import sweep_multipliers, sweep_variant
+    base = load_design("VolturnUS-S_example")
+    designs = [sweep_variant(base, m) for m in sweep_multipliers(4, seed=11)]
+    st = {"C_moor": np.diag([7e4, 7e4, 2e4, 1e7, 1e7, 1e8])}
+    A = DesignBatch(designs, statics=st, native=True)
+    B = DesignBatch(designs, statics=st, native=True)
+    cases = [dict(wave_heading=h, wave_height=4.0, wave_period=10.0) for h in (30.0, 0.0)]
+    idx = np.repeat(np.arange(4), 2)
+    cs = A.case_set(idx, cases * 4)
+    from raft.solver import prepare_batch
+    pa = prepare_batch(A.dds, cs)                   # batched path (fresh designs)
+    for i, d in enumerate(B.dds):                    # per-design launches
+        d.ensure_headings(np.array([0.0, 30.0]) * DEG2RAD)
+    torch.cuda.synchronize()
+    assert len({d.nn for d in A.dds}) > 1
+    for i, (a, b) in enumerate(zip(A.dds, B.dds)):
+        for h, beta in enumerate(a.headings):
+            j = b.headings.index(beta)
+            for t in ("uhat", "kproj", "finer"):
+                assert torch.equal(getattr(a, t)[h], getattr(b, t)[j]), (i, h, t)
+    res_a = A.solve(None, cs, prepared=pa).host()
+    res_b = B.solve(None, cs).host()
+    np.testing.assert_array_equal(res_a["Xi"], res_b["Xi"])
+    np.testing.assert_array_equal(res_a["iters"], res_b["iters"])

@@ -4,6 +4,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "raft-teststuff_amd"))
@@ -27,7 +29,8 @@ if __name__ == "__main__":
                         native=os.environ.get("C5_NATIVE", "1") == "1", light=True)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        cs = B.case_set(idx, cases)
+        grid = sea_state_grid()
+        cs = B.case_set_grid(idx, np.arange(len(idx)) % len(grid), grid)
         t2 = time.perf_counter()
         prep = prepare_batch(B.dds, cs)
         torch.cuda.synchronize()

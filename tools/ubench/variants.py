@@ -29,6 +29,15 @@ EDITS = {
     "gNoPot": [("rh_qtf_mfma.hip", "  cgemm_steps(wk.Lp + ", "  if (nk < 0) cgemm_steps(wk.Lp + ")],
     "gNoMain": [("rh_qtf_mfma.hip", "  if (nk > 0)\n    cgemm_steps(", "  if (nk < 0)\n    cgemm_steps(")],
     "prof": [],          # unmodified source built with -DRH_PROF (phase cycle counters)
+    # phase C: the node's drag coefficients read from LDS one node ahead (registers)
+    "cPrefA": [("        int m = 0, mnext = nn > 0 ? mstart[1] : 0;\n",
+                "        int m = 0, mnext = nn > 0 ? mstart[1] : 0;\n"
+                "        double Ac0 = al[0], Ac1 = al[1], Ac2 = al[2], Ac3 = al[3], Ac4 = al[4];\n"),
+               ("          const double* A = al + 5 * n;\n"
+                "          const double A0 = A[0], A1 = A[1], A2 = A[2], A3 = A[3], A4 = A[4];\n",
+                "          const double A0 = Ac0, A1 = Ac1, A2 = Ac2, A3 = Ac3, A4 = Ac4;\n"
+                "          const double* An = al + 5 * (n + 1 < nn ? n + 1 : n);\n"
+                "          Ac0 = An[0]; Ac1 = An[1]; Ac2 = An[2]; Ac3 = An[3]; Ac4 = An[4];\n")],
     "noLU": [("      my_sing |= !lu_solve<6>(Z, F);", "      F[0] = add(F[0], Z[0][0]);")],
     "stXo": [("        st_nt(Xo + c * nw + b, x);", "        st(Xo + c * nw + b, x);")],
     "noXo": [("        st_nt(Xo + c * nw + b, x);", "        if (x.r == 1234.5) st(Xo + c * nw + b, x);")],
@@ -74,4 +83,5 @@ def build(name, edits, flags=()):
 if __name__ == "__main__":
     names = sys.argv[1:] or list(EDITS)
     for n in names:
-        build(n, EDITS[n], ["-DRH_PROF"] if n == "prof" else [])
+        base = n[:-5] if n.endswith("+prof") else n
+        build(n.replace("+", "_"), EDITS[base], ["-DRH_PROF"] if (n == "prof" or n.endswith("+prof")) else [])
