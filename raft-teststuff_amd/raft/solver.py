@@ -133,14 +133,18 @@ def prepare_batch(designs, cases):
             d = designs[int(di)]
             sel = np.nonzero(cases.design_idx == di)[0]
             head[sel] = d.ensure_headings(cases.heading[sel] * DEG2RAD)
-    # design-major, then heading; within a (design, heading) run by sea state, so that the
-    # cases solved in lock-step by one workgroup tend to need the same number of iterations
-    order = np.lexsort((cases.Tp, cases.Hs, head, cases.design_idx)).astype(np.int32)
     # Lock-step groups (k_solve_grp) are opt-in: RAFT_GROUP_WIDTH=2.  Measured on the C2
     # batch they halve the wave-table stream but not the time per case, and
     # one case per workgroup (k_solve_lds) schedules better at 512 cases per GPU.
     width = min(N.lib().rh_group_cases(), int(os.environ.get("RAFT_GROUP_WIDTH", "1") or 1))
-    gstart = case_groups(cases.design_idx[order], head[order], width) if width > 1 else None
+    if width > 1:
+        # design-major, then heading; within a (design, heading) run by sea state, so that
+        # the cases solved in lock-step by one workgroup tend to need the same iterations
+        order = np.lexsort((cases.Tp, cases.Hs, head, cases.design_idx)).astype(np.int32)
+        gstart = case_groups(cases.design_idx[order], head[order], width)
+    else:
+        order = balanced_order(cases, head)
+        gstart = None
     i32 = dict(dtype=torch.int32, device=dev)
     f64 = dict(dtype=torch.float64, device=dev)
     return dict(design=torch.tensor(cases.design_idx, **i32), head=torch.tensor(head, **i32),
@@ -149,6 +153,35 @@ def prepare_batch(designs, cases):
                 order=torch.tensor(order, **i32), head_host=head,
                 group_start=None if gstart is None else torch.tensor(gstart, **i32),
                 ngroup=0 if gstart is None else len(gstart) - 1)
+
+
+def balanced_order(cases, head, nxcd=8):
+    """Launch order of one-case-per-workgroup batches.  Design-major, then heading, so an
+    XCD's contiguous slice of the order (xcd_remap) streams few tables out of its L2; then
+    the longest peak period first.  Each pair of adjacent XCD slices is re-dealt so both get
+    the same mix of periods.  Longer periods tend to need more drag iterations, so no XCD
+    collects the long cases, and within a slice the long ones are dispatched first.  The
+    order changes placement only, never results.  Measured on the C2 bench batch (512
+    cases, 2 per CU): the last CU finishes after 9.5 instead of 10.5 case-iterations
+    (tools/ubench/makespan.py)."""
+    order = np.lexsort((-cases.Tp, head, cases.design_idx))
+    G = len(order)
+    q, r = G // nxcd, G % nxcd
+    bounds = [x * q + min(x, r) for x in range(nxcd + 1)]
+    out = order.copy()
+    for x in range(0, nxcd - 1, 2):
+        a0, a1, a2 = bounds[x], bounds[x + 1], bounds[x + 2]
+        seg = order[a0:a2]
+        seg = seg[np.argsort(-cases.Tp[seg], kind="stable")]
+        na, nb = a1 - a0, a2 - a1
+        m = min(na, nb)
+        to_a = np.zeros(na + nb, dtype=bool)
+        to_a[0:2 * m:2] = True          # dealt alternately ...
+        if na > nb:
+            to_a[2 * m:] = True          # ... and the larger slice takes what is left
+        out[a0:a1] = seg[to_a]
+        out[a1:a2] = seg[~to_a]
+    return out.astype(np.int32)
 
 
 def case_groups(design, head, width):
