@@ -29,6 +29,12 @@ EDITS = {
     "gNoPot": [("rh_qtf_mfma.hip", "  cgemm_steps(wk.Lp + ", "  if (nk < 0) cgemm_steps(wk.Lp + ")],
     "gNoMain": [("rh_qtf_mfma.hip", "  if (nk > 0)\n    cgemm_steps(", "  if (nk < 0)\n    cgemm_steps(")],
     "prof": [],          # unmodified source built with -DRH_PROF (phase cycle counters)
+    # nw <= 256 (C4): 128 threads x 2 bins per lane instead of 256 x 1 (half the reductions per bin)
+    "c4nb2": [("rh_abi.hip", "    const int nb = nw <= rh::kLT ? 1 : 2;\n", "    const int nb = (nw <= rh::kLT && nw > rh::kLT / 2) ? 1 : 2;\n"),
+              ("rh_abi.hip", "    const int lt = nw <= rh::kLT / 2 ? rh::kLT / 2 : rh::kLT;",
+               "    const int lt = nw <= rh::kLT / 2 ? rh::kLT / 4 : rh::kLT;"),
+              ("rh_abi.hip", "      if (lt < rh::kLT) hipLaunchKernelGGL((rh::k_solve_lds<1, rh::kLT / 2>), grid, block, lsm, s, a);",
+               "      if (lt < rh::kLT) hipLaunchKernelGGL((rh::k_solve_lds<2, rh::kLT / 4>), grid, block, lsm, s, a);")],
     # phase C: the node's drag coefficients read from LDS one node ahead (registers)
     "cPrefA": [("        int m = 0, mnext = nn > 0 ? mstart[1] : 0;\n",
                 "        int m = 0, mnext = nn > 0 ? mstart[1] : 0;\n"
