@@ -23,6 +23,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "raft-teststuff_amd"))
 
 NCASE = 512
+C5_CHUNKS = 5         # C5 design blocks: block k+1 is prepared on the host while block k solves
 PEAK_FP64 = 78.6e12   # MI355X FP64 dense peak (vector = matrix rate), FLOP/s
 # HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950
 # correction of MI355X_MICROARCH.md + WRITE_SIZE), written by tools/pmc_summary.py
@@ -376,12 +377,13 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
     """C5 (BASELINE.json configs[4]): 250 parametersweep-style VolturnUS-S_example variants
     (raft/sweep.py) x 40 sea states (Hs 2..10 x Tp 6..20) = 10,000 cases at nw = 1000.
     The design-major case list is split in contiguous blocks over the ranks; a rank prepares
-    only the designs its block touches (host members/statics/added mass + device tables),
-    solves its block in one launch and the per-case outputs (std, PSD, iterations) are
-    all-gathered over RCCL.  End-to-end time = prep + solve + gather (max over ranks);
-    solve-only = the launch alone, repeated `steps` times.  Strong scaling (fixed 10k)."""
+    only the designs its block touches, in C5_CHUNKS design blocks pipelined by
+    raft/batch.py solve_sweep (native host preparation of block k+1 while block k solves),
+    and the per-case outputs (std, PSD, iterations) are all-gathered over RCCL.  End-to-end
+    time = everything from the design dicts to the gathered outputs (max over ranks);
+    solve-only = the blocks' launches alone, repeated `steps` times.  Strong scaling (fixed 10k)."""
     import torch
-    from raft.batch import DesignBatch, sweep_cases, sweep_shard
+    from raft.batch import solve_sweep, sweep_cases, sweep_shard
     from raft.parallel import gather_cases
     from raft.sweep import sea_state_grid, sweep_multipliers, sweep_variant
     base, C_moor = c5_base()
@@ -393,30 +395,27 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
     variants = [sweep_variant(base, mult[i]) for i in range(dlo, dhi)]      # inputs: not timed
     local_idx = idx_all[lo:hi] - dlo
     want = ("psd", "std")
-    from raft.solver import prepare_batch
+    state_idx = np.arange(lo, hi) % len(grid)          # design-major product
     # two untimed passes first (the host workers' first tasks, allocator growth), as the
     # warmup steps of the C2 leg
     for _ in range(2):
-        W = DesignBatch(variants, statics={"C_moor": C_moor}, device=device, pool=pool, native=True)
-        W.solve(None, W.case_set_grid(local_idx, np.arange(lo, hi) % len(grid), grid), want=want)
-        del W
+        w_out, w_keep = solve_sweep(variants, {"C_moor": C_moor}, local_idx, state_idx, grid, device=device,
+                                    pool=pool, chunks=C5_CHUNKS, want=want)
+        torch.cuda.synchronize()
+        del w_out, w_keep
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    B = DesignBatch(variants, statics={"C_moor": C_moor}, device=device, pool=pool, native=True)
-    cs = B.case_set_grid(local_idx, np.arange(lo, hi) % len(grid), grid)   # design-major product
-    prep = prepare_batch(B.dds, cs)                  # device wave tables per (design, heading)
-    torch.cuda.synchronize()
-    t_prep = time.perf_counter() - t0
-    res = B.solve(None, cs, want=want, prepared=prep)
-    torch.cuda.synchronize()
-    t_solve1 = time.perf_counter() - t0 - t_prep
+    res, keep = solve_sweep(variants, {"C_moor": C_moor}, local_idx, state_idx, grid, device=device, pool=pool,
+                            chunks=C5_CHUNKS, want=want)
     out = gather_cases({"std": res["std"], "psd": res["psd"], "iters": res["iters"]}, n)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t_e2e = time.perf_counter() - t0
+    host_s = sum(B.host_seconds for B, _, _, _ in keep)
+    # solve only: the blocks' launches again, on their prepared tables
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     if world > 1:
@@ -425,26 +424,29 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
     t1 = time.perf_counter()
     for i in range(steps):
         ev[i][0].record(stream)
-        res = B.solve(None, cs, want=want, prepared=prep)
+        for B, cs, prep, _ in keep:
+            B.solve(None, cs, want=want, prepared=prep)
         ev[i][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t_solve = (time.perf_counter() - t1) / steps
-    ts = torch.tensor([t_e2e, t_prep, t_solve, B.host_seconds], dtype=torch.float64, device=f"cuda:{device}")
+    ts = torch.tensor([t_e2e, t_solve, host_s], dtype=torch.float64, device=f"cuda:{device}")
     if world > 1:
         dist.all_reduce(ts, op=dist.ReduceOp.MAX)
-    t_e2e, t_prep, t_solve, t_host = (float(x) for x in ts.cpu())
+    t_e2e, t_solve, t_host = (float(x) for x in ts.cpu())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     iters = out["iters"].cpu().numpy()
     return {"metric": "sweep cases/sec end-to-end (design prep + solve + gather)", "value": n / t_e2e,
             "unit": "cases/s", "scaling": "strong", "cases": n, "designs": C5_DESIGNS, "sea_states": len(grid),
-            "end_to_end_s": t_e2e, "prep_s": t_prep, "host_prep_s": t_host, "first_solve_s": t_solve1,
+            "end_to_end_s": t_e2e, "host_prep_s": t_host, "blocks": C5_CHUNKS,
             "solve_only_cases_per_s": n / t_solve, "solve_ms": t_solve * 1e3, "kernel_ms_rank0": kern_ms,
             "iterations_mean": float(iters.mean()),
             "config": {"workload": "C5: 250 VolturnUS-S_example parametersweep variants (5 variables U(0.75,1.25)) "
-                                   "x 40 sea states, nw=1000", "nw": B.nw,
-                       "parallelism": f"case-block-sharded x{world} + all-gather (std, PSD, iterations)",
+                                   "x 40 sea states, nw=1000", "nw": keep[0][0].nw,
+                       "parallelism": f"case-block-sharded x{world} + all-gather (std, PSD, iterations); "
+                                      f"{C5_CHUNKS} design blocks per rank, host preparation of block k+1 "
+                                      "overlapped with the solve of block k",
                        "host_prep_workers_per_rank": nproc}}
 
 

@@ -17,13 +17,24 @@
 #include "rh_solve_grp.hip"
 #include "rh_prep.h"       // host-only: native per-design preparation (rh_prep_designs)
 
+// One staging slot of the design descriptor array.  A context cycles through kDescSlots of
+// them, so a launch never waits for the descriptors of the previous one: the host blocks only
+// when it is kDescSlots launches ahead of the device (a pipelined sweep enqueues a block's
+// tables and solve while the previous block still runs, raft/batch.py solve_sweep).
+struct rh_desc_slot {
+  rh::DevDesign* d = nullptr;   // device copy of the descriptor array
+  rh::DevDesign* h = nullptr;   // pinned staging
+  int cap = 0;
+  hipEvent_t staged = nullptr;  // after the copy out of h
+  hipEvent_t used = nullptr;    // after the last kernel that reads d
+};
+constexpr int kDescSlots = 8;
+
 struct rh_ctx {
   int device = 0;
-  rh::DevDesign* d_designs = nullptr;   // device copy of the descriptor array
-  rh::DevDesign* h_designs = nullptr;   // pinned staging
-  int cap = 0;
-  hipEvent_t staged = nullptr;          // last copy out of h_designs
-  hipEvent_t used = nullptr;            // after the last kernel that reads d_designs
+  rh_desc_slot slot[kDescSlots];
+  int next = 0;                         // slot of the next staging
+  int cur = 0;                          // slot of the last staging
   // tuning / cross-check knobs (per context: the ABI has no mutable process globals)
   bool force_general = false;   // rh_set_solver(ctx, 1): always use k_solve_cases (parity cross-checks)
   bool no_group = false;        // rh_set_solver(ctx, 2): ignore group_start (one case per workgroup)
@@ -68,30 +79,38 @@ int check_design(const rh_design& d, bool need_tables) {
 }
 
 int stage_designs(rh_ctx* ctx, const rh_design* designs, int n, hipStream_t s) {
-  if (n > ctx->cap) {
-    if (ctx->staged) RH_HIP(hipEventSynchronize(ctx->staged));
-    RH_HIP(hipEventSynchronize(ctx->used));   // no kernel reads the old descriptor array any more
-    if (ctx->d_designs) RH_HIP(hipFree(ctx->d_designs));
-    if (ctx->h_designs) RH_HIP(hipHostFree(ctx->h_designs));
+  rh_desc_slot& sl = ctx->slot[ctx->next];
+  ctx->cur = ctx->next;
+  ctx->next = (ctx->next + 1) % kDescSlots;
+  if (n > sl.cap) {
+    RH_HIP(hipEventSynchronize(sl.staged));
+    RH_HIP(hipEventSynchronize(sl.used));   // no kernel reads this slot's old array any more
+    if (sl.d) RH_HIP(hipFree(sl.d));
+    if (sl.h) RH_HIP(hipHostFree(sl.h));
+    sl.d = sl.h = nullptr;
+    sl.cap = 0;
     int cap = n < 64 ? 64 : n;
-    RH_HIP(hipMalloc(&ctx->d_designs, sizeof(rh::DevDesign) * cap));
-    RH_HIP(hipHostMalloc(&ctx->h_designs, sizeof(rh::DevDesign) * cap, hipHostMallocDefault));
-    ctx->cap = cap;
+    RH_HIP(hipMalloc(&sl.d, sizeof(rh::DevDesign) * cap));
+    RH_HIP(hipHostMalloc(&sl.h, sizeof(rh::DevDesign) * cap, hipHostMallocDefault));
+    sl.cap = cap;
   }
-  if (ctx->staged) RH_HIP(hipEventSynchronize(ctx->staged));  // previous copy has left the staging buffer
-  // d_designs may still be read by a kernel of an earlier call on another stream: order the
-  // overwrite after it (a no-op on the same stream)
-  RH_HIP(hipStreamWaitEvent(s, ctx->used, 0));
-  for (int i = 0; i < n; ++i) ctx->h_designs[i].d = designs[i];
-  RH_HIP(hipMemcpyAsync(ctx->d_designs, ctx->h_designs, sizeof(rh::DevDesign) * n, hipMemcpyHostToDevice, s));
-  RH_HIP(hipEventRecord(ctx->staged, s));
+  RH_HIP(hipEventSynchronize(sl.staged));  // this slot's previous copy has left the staging buffer
+  // the slot's device array may still be read by a kernel of an earlier call on another
+  // stream: order the overwrite after it (a no-op on the same stream)
+  RH_HIP(hipStreamWaitEvent(s, sl.used, 0));
+  for (int i = 0; i < n; ++i) sl.h[i].d = designs[i];
+  RH_HIP(hipMemcpyAsync(sl.d, sl.h, sizeof(rh::DevDesign) * n, hipMemcpyHostToDevice, s));
+  RH_HIP(hipEventRecord(sl.staged, s));
   return RH_OK;
 }
 
-// after every launch that reads ctx->d_designs
+// the device descriptor array of the last staging
+rh::DevDesign* staged_designs(rh_ctx* ctx) { return ctx->slot[ctx->cur].d; }
+
+// after every launch that reads the staged descriptors
 int designs_used(rh_ctx* ctx, hipStream_t s) {
   RH_HIP(hipGetLastError());
-  RH_HIP(hipEventRecord(ctx->used, s));
+  RH_HIP(hipEventRecord(ctx->slot[ctx->cur].used, s));
   return RH_OK;
 }
 
@@ -154,10 +173,16 @@ int rh_ctx_create(int device, rh_ctx** out) {
   RH_HIP(hipSetDevice(device));
   rh_ctx* c = new rh_ctx;
   c->device = device;
-  hipError_t e = hipEventCreateWithFlags(&c->staged, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->used, hipEventDisableTiming);
+  hipError_t e = hipSuccess;
+  for (auto& sl : c->slot) {
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.staged, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.used, hipEventDisableTiming);
+  }
   if (e != hipSuccess) {
-    if (c->staged) (void)hipEventDestroy(c->staged);
+    for (auto& sl : c->slot) {
+      if (sl.staged) (void)hipEventDestroy(sl.staged);
+      if (sl.used) (void)hipEventDestroy(sl.used);
+    }
     delete c;
     return fail(RH_EHIP, "hipEventCreate: %s", hipGetErrorString(e));
   }
@@ -167,16 +192,18 @@ int rh_ctx_create(int device, rh_ctx** out) {
 
 int rh_ctx_destroy(rh_ctx* ctx) {
   if (!ctx) return RH_OK;
-  if (ctx->staged) {
-    (void)hipEventSynchronize(ctx->staged);
-    (void)hipEventDestroy(ctx->staged);
+  for (auto& sl : ctx->slot) {
+    if (sl.staged) {
+      (void)hipEventSynchronize(sl.staged);
+      (void)hipEventDestroy(sl.staged);
+    }
+    if (sl.used) {
+      (void)hipEventSynchronize(sl.used);
+      (void)hipEventDestroy(sl.used);
+    }
+    if (sl.d) (void)hipFree(sl.d);
+    if (sl.h) (void)hipHostFree(sl.h);
   }
-  if (ctx->used) {
-    (void)hipEventSynchronize(ctx->used);
-    (void)hipEventDestroy(ctx->used);
-  }
-  if (ctx->d_designs) (void)hipFree(ctx->d_designs);
-  if (ctx->h_designs) (void)hipHostFree(ctx->h_designs);
   delete ctx;
   return RH_OK;
 }
@@ -211,7 +238,7 @@ int rh_wave_tables_batch(rh_ctx* ctx, const rh_design* designs, int ndesign, con
   const hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
   dim3 grid((nwmax + 63) / 64, nhmax, ndesign);
-  hipLaunchKernelGGL(rh::k_wave_tables_batch, grid, dim3(64 * rh::kWtN), 0, s, ctx->d_designs, beta, hstride);
+  hipLaunchKernelGGL(rh::k_wave_tables_batch, grid, dim3(64 * rh::kWtN), 0, s, staged_designs(ctx), beta, hstride);
   return designs_used(ctx, s);
 }
 
@@ -243,7 +270,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
   rh::CaseArgs a;
-  a.designs = ctx->d_designs;
+  a.designs = staged_designs(ctx);
   a.c = *cases;
   a.o = *out;
   // Grouped path (rh_solve_grp.hip): kGroupCases cases of one (design, heading) per workgroup.
@@ -306,7 +333,7 @@ int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int 
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
-  rh::HeadArgs a{ctx->d_designs, ncase, design_idx, head, zeta, B_drag, Bmat, Xi, nullptr};
+  rh::HeadArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, B_drag, Bmat, Xi, nullptr};
   const size_t smem = sizeof(double) * (size_t)(nnmax * 9 + 36 + 108);
   dim3 grid((nw + kThreads - 1) / kThreads, ncase);
   hipLaunchKernelGGL(rh::k_heading_resp, grid, dim3(kThreads), smem, s, a);
@@ -328,7 +355,7 @@ int rh_wave_excitation(rh_ctx* ctx, const rh_design* designs, int ndesign, int n
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
-  rh::HeadArgs a{ctx->d_designs, ncase, design_idx, head, zeta, nullptr, Bmat, nullptr, F};
+  rh::HeadArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, nullptr, Bmat, nullptr, F};
   const size_t smem = sizeof(double) * (size_t)(nnmax * 9 + 36 + 108);
   dim3 grid((nw + kThreads - 1) / kThreads, ncase);
   hipLaunchKernelGGL(rh::k_heading_resp, grid, dim3(kThreads), smem, s, a);

@@ -154,6 +154,51 @@ class DesignBatch:
         return solve_batch(self.dds, cs, self.nIter, self.XiStart, tol, want=want, prepared=prepared)
 
 
+def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, pool=None, chunks=4, tol=0.01,
+                want=("psd", "std")):
+    """A design sweep solved in `chunks` design blocks, pipelined: while the device solves
+    block k, the host prepares block k+1 (native preparation, raft/native_prep.py), so the
+    host work hides behind the solve instead of preceding it.
+
+    design_idx / state_idx: per case, its design (index into `designs`, non-decreasing: the
+    design-major order of sweep_cases) and its sea state (index into `sea_states`).  Every
+    case is solved exactly as in one DesignBatch call (per-case arithmetic, so the results are
+    the same bits).  The uploads of a block go through a copy stream, so the host never
+    waits behind a running solve; its sweep tables and its solve run on the current stream
+    after an event on the uploads.  Returns (result dict of device tensors in case
+    order, stream-ordered on the current stream; the per-block DesignBatches, kept alive
+    with their tensors until the caller synchronises)."""
+    import torch
+    from .solver import prepare_batch
+    design_idx = np.asarray(design_idx, dtype=np.int64)
+    state_idx = np.asarray(state_idx, dtype=np.int64)
+    if np.any(np.diff(design_idx) < 0):
+        raise ValueError("solve_sweep: cases must be design-major (non-decreasing design index)")
+    nd = len(designs)
+    cuts = np.linspace(0, nd, max(1, min(chunks, nd)) + 1).round().astype(int)
+    dev = torch.device("cuda", device)
+    compute = torch.cuda.current_stream(dev)
+    copy = torch.cuda.Stream(dev)
+    parts, keep = [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        if b <= a:
+            continue
+        lo, hi = np.searchsorted(design_idx, [a, b])
+        with torch.cuda.stream(copy):
+            B = DesignBatch(designs[a:b], statics=statics if isinstance(statics, dict) or statics is None
+                            else statics[a:b], device=device, pool=pool, native=True)
+            cs = B.case_set_grid(design_idx[lo:hi] - a, state_idx[lo:hi], sea_states)
+            prep = prepare_batch(B.dds, cs, tables_stream=compute)
+            ready = torch.cuda.Event()
+            ready.record(copy)
+        compute.wait_event(ready)
+        res = B.solve(None, cs, tol=tol, want=want, prepared=prep)   # on the solve stream
+        parts.append(res)
+        keep.append((B, cs, prep, res))
+    out = {k: torch.cat([r[k] for r in parts], 0) for k in parts[0]}
+    return out, keep
+
+
 def prepare_design(job):
     """Host preparation of one single-FOWT design (members, statics, added mass and
     excitation coefficients at pose r6): the per-design part of runRAFT before the case loop

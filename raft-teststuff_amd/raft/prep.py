@@ -215,11 +215,12 @@ class DeviceDesign:
                                        N.ptr(self.uhat), N.ptr(self.finer), N.ptr(self.kproj), s), "rh_wave_tables")
 
 
-def tabulate_batch(designs, design_idx, betas):
+def tabulate_batch(designs, design_idx, betas, launch_stream=None):
     """Wave tables of every (design, heading) pair a batch needs, in ONE rh_wave_tables_batch
     launch, for designs that have none yet (a fresh design sweep).  Returns the heading
     index of every case in its design's tables.  Tables of all designs share three device
-    allocations; each DeviceDesign holds views."""
+    allocations; each DeviceDesign holds views.  launch_stream: run the launch there (after
+    this stream's uploads, through an event) instead of on the current stream."""
     torch = designs[0].torch
     dev = designs[0].device
     n = len(design_idx)
@@ -260,6 +261,13 @@ def tabulate_batch(designs, design_idx, betas):
     for j, d in enumerate(sel):
         d._beta_keep = beta_t[j, :int(nh[j])]
     arr = (N.RhDesign * len(sel))(*[d.struct() for d in sel])
-    N.check(N.lib().rh_wave_tables_batch(N.context(sel[0].dev_index), arr, len(sel), N.ptr(beta_t), hstride,
-                                         N.stream_handle(torch, dev)), "rh_wave_tables_batch")
+    if launch_stream is not None:
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        launch_stream.wait_event(ev)
+        s = ctypes.c_void_p(launch_stream.cuda_stream)
+    else:
+        s = N.stream_handle(torch, dev)
+    N.check(N.lib().rh_wave_tables_batch(N.context(sel[0].dev_index), arr, len(sel), N.ptr(beta_t), hstride, s),
+            "rh_wave_tables_batch")
     return head

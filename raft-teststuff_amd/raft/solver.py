@@ -115,9 +115,11 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     return out
 
 
-def prepare_batch(designs, cases):
+def prepare_batch(designs, cases, tables_stream=None):
     """Upload per-case parameters and make sure every design has the wave tables its cases
-    need.  Reusable across repeated solves of the same batch (bench steady state)."""
+    need.  Reusable across repeated solves of the same batch (bench steady state).
+    tables_stream: launch a fresh sweep's batched wave tables on that stream (the uploads
+    stay on the current one; raft/batch.py solve_sweep)."""
     torch = designs[0].torch
     dev = designs[0].device
     if cases.n and (cases.design_idx.min() < 0 or cases.design_idx.max() >= len(designs)):
@@ -126,7 +128,7 @@ def prepare_batch(designs, cases):
     if len(used) > 1 and all(designs[int(i)].uhat is None for i in used):
         # a fresh multi-design batch (a sweep): every table in one launch
         from .prep import tabulate_batch
-        head = tabulate_batch(designs, cases.design_idx, cases.heading * DEG2RAD)
+        head = tabulate_batch(designs, cases.design_idx, cases.heading * DEG2RAD, launch_stream=tables_stream)
     else:
         head = np.zeros(cases.n, dtype=np.int32)
         for di in used:

@@ -214,3 +214,23 @@ def test_batched_wave_tables_equal_per_design_tables():
     res_b = B.solve(None, cs).host()
     np.testing.assert_array_equal(res_a["Xi"], res_b["Xi"])
     np.testing.assert_array_equal(res_a["iters"], res_b["iters"])
+
+
+def test_pipelined_sweep_equals_one_batch():
+    """solve_sweep (design blocks prepared on the host while the previous block solves, uploads
+    on a copy stream) gives the same bits as one DesignBatch over the whole sweep."""
+    import torch
+    from raft.batch import DesignBatch, solve_sweep, sweep_cases
+    from raft.sweep import sea_state_grid, sweep_multipliers, sweep_variant
+    base = load_design("VolturnUS-S_example")
+    designs = [sweep_variant(base, m) for m in sweep_multipliers(7, seed=13)]
+    grid = sea_state_grid()[::5]
+    st = {"C_moor": np.diag([7e4, 7e4, 2e4, 1e7, 1e7, 1e8])}
+    idx, _ = sweep_cases(len(designs), grid)
+    sidx = np.arange(len(idx)) % len(grid)
+    out, keep = solve_sweep(designs, st, idx, sidx, grid, chunks=3, want=("std", "psd"))
+    B = DesignBatch(designs, statics=st, native=True)
+    ref = B.solve(None, B.case_set_grid(idx, sidx, grid), want=("std", "psd"))
+    torch.cuda.synchronize()
+    for k in ("Xi", "iters", "status", "std", "psd"):
+        assert torch.equal(out[k], ref[k]), k
