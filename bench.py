@@ -48,7 +48,10 @@ def pmc_traffic(*kernels):
     return total
 
 
-L2_PEAK = 34.5e12     # MI355X aggregate L2 bandwidth, B/s (MI355X_MICROARCH.md, L2 per XCD)
+# The L2 -> CU rate of the solve kernel's own kproj access pattern with no arithmetic beside it
+# (tools/ubench/l2_stream.hip on the box: 512 one-per-CU workgroups, 2.5 MB per heading, lane =
+# bin, buffer loads; profiles/r02_v5/l2_stream.txt): 49.5 TB/s.  The stream's ceiling, measured.
+L2_PEAK = 49.5e12
 
 
 def pmc_l2(kernel, kernel_ms):
@@ -65,6 +68,7 @@ def pmc_l2(kernel, kernel_ms):
             b = 128.0 * (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
             rate = b / (kernel_ms * 1e-3)
             return {"bytes": b, "TB_per_s": rate / 1e12, "peak_TB_per_s": L2_PEAK / 1e12, "frac": rate / L2_PEAK,
+                    "peak_note": "measured stream ceiling of this access pattern (tools/ubench/l2_stream.hip)",
                     "hit_rate": c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])}
     return None
 
@@ -219,8 +223,9 @@ def build_qtf(device):
 def bench_qtf(device, steps, warmup, world, rank, dist):
     """C3 throughput: one 400x400 QTF per step (upper triangle computed, Hermitian fill), 16 x 16
     pair tiles sharded over the ranks with one all-gather of packed pairs.  end_to_end_ms: a
-    cold QTF including the per-(design, grid, heading) tables (host geometry, device Hankel
-    table) and their upload."""
+    QTF of a new (design, grid, heading) in a warm process, including its tables (host
+    geometry, device Hankel table) and their upload; first_call_ms: the same for the first QTF
+    of the process, which also loads the QTF kernels."""
     import torch
     from raft.qtf import QtfDevice
     T, f, dd, X, M66, w2, k2 = build_qtf(device)
@@ -229,6 +234,13 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    qd = QtfDevice(f, w2, k2, 0.0, device)
+    q = qd.qtf(dd.w, X, M66, group=group)
+    torch.cuda.synchronize()
+    t_first = time.perf_counter() - t0     # first QTF of the process: includes loading its kernels
+    del qd, q
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()               # a new (design, grid, heading) in a warm process
     qd = QtfDevice(f, w2, k2, 0.0, device)
     t_tables = time.perf_counter() - t0
     q = qd.qtf(dd.w, X, M66, group=group)
@@ -255,10 +267,10 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt, t_e2e, t_tables], dtype=torch.float64, device=f"cuda:{device}")
+    t = torch.tensor([dt, t_e2e, t_tables, t_first], dtype=torch.float64, device=f"cuda:{device}")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt_max, e2e_max, tab_max = (float(x) for x in t.cpu())
+    dt_max, e2e_max, tab_max, first_max = (float(x) for x in t.cpu())
     ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     fpp = qtf_flops_per_pair(qd.nq, nkay, nwl)
     from raft.parallel import qtf_pairs_of
@@ -266,6 +278,7 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
     achieved = fpp * mine / (ms * 1e-3)
     out = {"metric": "QTF pairs/sec", "value": npair * steps / dt_max, "unit": "pairs/s", "steps": steps,
            "ms_per_qtf": dt_max / steps * 1e3, "end_to_end_ms": e2e_max * 1e3, "host_tables_ms": tab_max * 1e3,
+           "first_call_ms": first_max * 1e3,
            "scaling": "strong", "n_gpus": world, "n2": n2, "pairs_per_qtf": npair,
            "full_grid_equiv_per_s": n2 * n2 * steps / dt_max,
            "config": {"workload": "C3: OC4semi-RAFT_QTF slender-body QTF, 400x400 (w1,w2) grid, heading 0",

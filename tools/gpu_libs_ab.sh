@@ -1,0 +1,14 @@
+#!/bin/bash
+# Kernel A/B without the test suite: the C2 solve timed with each library given as an argument
+# (RAFTHIP_LIB), alternating three times.  Each GPU step has its own time limit.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out
+mkdir -p $OUT; cd $R
+: > $OUT/ab.log
+for rep in 1 2 3; do
+  for lib in "$@"; do
+    RAFTHIP_LIB=$R/$lib timeout -k 10 120 python tools/ubench/time_solve.py $(basename $lib) >> $OUT/ab.log 2>&1
+    rc=$?; if [ $rc -ne 0 ]; then echo "time_solve $lib rc=$rc"; tail -5 $OUT/ab.log; exit $rc; fi
+  done
+done
+grep -v amdgpu.ids $OUT/ab.log
