@@ -69,7 +69,15 @@ def read_qtf12d(src, rho, g, ULEN=1, nDOF=6):
         raise ValueError("Both frequency columns in the input QTF must contain the same values.")
     i1 = np.searchsorted(w1, data[:, 0])
     i2 = np.searchsorted(w2, data[:, 1])
-    ih = np.searchsorted(heads, np.deg2rad(data[:, 2]))
+    # The reference looks a row's heading up as np.where(heads_2nd == row[2]) (:1686): the
+    # heading column in DEGREES against heads_2nd in RADIANS.  Heading 0 matches; a heading
+    # with no radian value equal to its degree value finds nothing and indhead[0] raises
+    # IndexError.  Mirrored exactly, error included.
+    ih = np.minimum(np.searchsorted(heads, data[:, 2]), len(heads) - 1)
+    miss = heads[ih] != data[:, 2]
+    if miss.any():
+        raise IndexError("index 0 is out of bounds for axis 0 with size 0 (readQTF matches the .12d heading "
+                         f"{data[np.argmax(miss), 2]} deg against headings in radians, raft/raft_fowt.py:1686)")
     idof = np.round(data[:, 4] - 1).astype(int)
     factor = np.where(idof >= 3, rho * g * ULEN * ULEN, rho * g * ULEN)
     val = factor * (data[:, 7] + 1j * data[:, 8])

@@ -59,6 +59,21 @@ def test_reader_rejects_bidirectional_and_ragged():
         read_qtf12d(r, 1025, 9.81)
 
 
+def test_reader_heading_lookup_mirrors_reference():
+    """The reference matches the .12d heading column (degrees) against heads_2nd (radians,
+    raft/raft_fowt.py:1676, 1686): heading 0 reads, any other heading raises IndexError from
+    indhead[0].  Restated here on the reference's own loop semantics."""
+    T1, T2 = 2 * np.pi / 0.5, 2 * np.pi / 1.0
+    def rows(hd):
+        return [[T1, T2, hd, hd, 1, 0, 0, 1.0, 2.0], [T2, T1, hd, hd, 1, 0, 0, 1.0, -2.0]]
+    h, _, _, q = read_qtf12d(np.array(rows(0.0)), 1000.0, 10.0)
+    assert h.tolist() == [0.0] and q[0, 1, 0, 0] == 1e4 * (1 + 2j)
+    for heads in ([30.0], [0.0, 30.0]):
+        rows_h = np.array([r for hd in heads for r in rows(hd)])
+        with pytest.raises(IndexError):
+            read_qtf12d(rows_h, 1000.0, 10.0)
+
+
 def test_writer_reader_round_trip(T, tmp_path):
     """write_qtf12d (raft/raft_fowt.py:1700-1726, 5 significant digits) -> read_qtf12d."""
     q = T["qtf"]
