@@ -397,31 +397,40 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
     solve-only = the blocks' launches alone, repeated `steps` times.  Strong scaling (fixed 10k)."""
     import torch
     from raft.batch import solve_sweep, sweep_cases, sweep_shard
+    from raft.native_prep import sweep_specs
     from raft.parallel import gather_cases
-    from raft.sweep import sea_state_grid, sweep_multipliers, sweep_variant
+    from raft.sweep import sea_state_grid, sweep_multipliers
     base, C_moor = c5_base()
     mult = sweep_multipliers(C5_DESIGNS)
     grid = sea_state_grid()
     idx_all, cases_all = sweep_cases(C5_DESIGNS, grid)
     n = len(idx_all)
     lo, hi, dlo, dhi = sweep_shard(idx_all, rank, world)
-    variants = [sweep_variant(base, mult[i]) for i in range(dlo, dhi)]      # inputs: not timed
+    # inputs: the base design and this rank's multipliers.  Each block's spec records come from
+    # them inside the timed pipeline (native_prep.sweep_specs: the base record with the swept
+    # member fields rewritten), so no per-variant design dict is built or parsed.
+    statics = {"C_moor": C_moor}
+    designs = [base] * (dhi - dlo)               # site and frequency grid only
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) // max(1, world)))
+
+    def specs(a, b):
+        return sweep_specs(base, mult[dlo + a:dlo + b], statics=statics)
     local_idx = idx_all[lo:hi] - dlo
     want = ("psd", "std")
     state_idx = np.arange(lo, hi) % len(grid)          # design-major product
     # two untimed passes first (the host workers' first tasks, allocator growth), as the
     # warmup steps of the C2 leg
     for _ in range(2):
-        w_out, w_keep = solve_sweep(variants, {"C_moor": C_moor}, local_idx, state_idx, grid, device=device,
-                                    pool=pool, chunks=C5_CHUNKS, want=want)
+        w_out, w_keep = solve_sweep(designs, statics, local_idx, state_idx, grid, device=device, chunks=C5_CHUNKS,
+                                    want=want, specs=specs, threads=threads)
         torch.cuda.synchronize()
         del w_out, w_keep
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res, keep = solve_sweep(variants, {"C_moor": C_moor}, local_idx, state_idx, grid, device=device, pool=pool,
-                            chunks=C5_CHUNKS, want=want)
+    res, keep = solve_sweep(designs, statics, local_idx, state_idx, grid, device=device, chunks=C5_CHUNKS,
+                            want=want, specs=specs, threads=threads)
     out = gather_cases({"std": res["std"], "psd": res["psd"], "iters": res["iters"]}, n)
     torch.cuda.synchronize()
     if world > 1:
@@ -460,7 +469,9 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
                        "parallelism": f"case-block-sharded x{world} + all-gather (std, PSD, iterations); "
                                       f"{C5_CHUNKS} design blocks per rank, host preparation of block k+1 "
                                       "overlapped with the solve of block k",
-                       "host_prep_workers_per_rank": nproc}}
+                       "host_prep_threads_per_rank": threads,
+                       "design_input": "base design + per-variant multipliers; spec records built in the timed "
+                                       "pipeline (raft/native_prep.py sweep_specs)"}}
 
 
 def relaunch(nproc, argv):
@@ -530,7 +541,7 @@ def main():
     baselines = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         baselines = cpu_baselines()          # before this process initialises the GPU
-    pool, nproc = c5_pool(world) if not args.no_c5 else (None, 1)   # likewise
+    pool, nproc = None, 1     # C5 prepares designs on native host threads (no worker pool)
     import torch
     import torch.distributed as dist
     if world > 1:

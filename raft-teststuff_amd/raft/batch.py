@@ -29,22 +29,27 @@ class DesignBatch:
     r6      : platform pose for the linearisation (default: the reference position)
     """
 
-    def __init__(self, designs, statics=None, r6=None, device=0, pool=None, light=False, native=False):
+    def __init__(self, designs, statics=None, r6=None, device=0, pool=None, light=False, native=False, specs=None,
+                 threads=None):
         """pool: optional multiprocessing pool (see host_pool) that prepares the designs on
         the host in parallel; results are identical to the serial path.
         light: keep only what the device side needs of each design (HostDesign: its tables,
         grid and site scalars) instead of the full Model; from a pool this ships ~40 KB per
         design instead of ~150 KB of Python objects (the parent's unpickling was the cost).
         native: prepare every design in librafthip on host threads (raft/native_prep.py,
-        rh_prep_designs; implies light): the pool, if any, only flattens the design dicts."""
+        rh_prep_designs; implies light): the pool, if any, only flattens the design dicts.
+        specs: the designs' spec records, already flattened (native_prep.sweep_specs; implies
+        native); `designs` then only supplies the site and the frequency grid.
+        threads: host threads of the native preparation (default: the pool's size, else
+        min(16, this process's cores))."""
         t0 = time.perf_counter()
         if isinstance(statics, dict) or statics is None:
             statics = [statics] * len(designs)
         if len(statics) != len(designs):
             raise ValueError("statics: one dict for all designs or one per design")
         self._prepared = None
-        if native:
-            self.models = self._native(designs, statics, r6, device, pool)
+        if native or specs is not None:
+            self.models = self._native(designs, statics, r6, device, pool, specs, threads)
         else:
             jobs = [(d, st, r6, device, light) for d, st in zip(designs, statics)]
             if pool is not None and len(jobs) > 1:
@@ -64,7 +69,7 @@ class DesignBatch:
         self.dds = self._upload(device)
         self.upload_seconds = time.perf_counter() - t0
 
-    def _native(self, designs, statics, r6, device, pool):
+    def _native(self, designs, statics, r6, device, pool, specs=None, threads=None):
         """rh_prep_designs over every design (raft/native_prep.py); returns HostDesign-like
         records holding views of the one packed host array."""
         from .hydro_math import wave_numbers
@@ -72,17 +77,22 @@ class DesignBatch:
         w = Model.frequency_grid(designs[0])
         depth = get_from_dict(designs[0]["site"], "water_depth", dtype=float)
         for d in designs[1:]:
+            if d is designs[0]:
+                continue
             if get_from_dict(d["site"], "water_depth", dtype=float) != depth or \
                     not np.array_equal(Model.frequency_grid(d), w):
                 raise ValueError("all designs of a batch must share the frequency grid and the site")
         k = wave_numbers(w, depth)
-        jobs = [(d, None if r6 is None else np.asarray(r6, dtype=float), st) for d, st in zip(designs, statics)]
-        if pool is not None and len(jobs) > 1:
-            specs = pool.map(_spec_job, jobs, chunksize=max(1, len(jobs) // (4 * pool._processes)))
-        else:
-            specs = [_spec_job(j) for j in jobs]
+        if specs is None:
+            jobs = [(d, None if r6 is None else np.asarray(r6, dtype=float), st) for d, st in zip(designs, statics)]
+            if pool is not None and len(jobs) > 1:
+                specs = pool.map(_spec_job, jobs, chunksize=max(1, len(jobs) // (4 * pool._processes)))
+            else:
+                specs = [_spec_job(j) for j in jobs]
+        elif len(specs) != len(designs):
+            raise ValueError("DesignBatch: one spec record per design")
         import os
-        nt = pool._processes if pool is not None else min(16, len(os.sched_getaffinity(0)))
+        nt = threads or (pool._processes if pool is not None else min(16, len(os.sched_getaffinity(0))))
         P = self._prepared = PreparedDesigns(specs, w, k, nthreads=nt)
         st0 = designs[0].get("settings", {})
         nIter = get_from_dict(st0, "nIter", default=15, dtype=int)
@@ -155,7 +165,7 @@ class DesignBatch:
 
 
 def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, pool=None, chunks=4, tol=0.01,
-                want=("psd", "std")):
+                want=("psd", "std"), timings=None, specs=None, threads=None):
     """A design sweep solved in `chunks` design blocks, pipelined: while the device solves
     block k, the host prepares block k+1 (native preparation, raft/native_prep.py), so the
     host work hides behind the solve instead of preceding it.
@@ -167,7 +177,12 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
     waits behind a running solve; its sweep tables and its solve run on the current stream
     after an event on the uploads.  Returns (result dict of device tensors in case
     order, stream-ordered on the current stream; the per-block DesignBatches, kept alive
-    with their tensors until the caller synchronises)."""
+    with their tensors until the caller synchronises).  specs: optional spec records of the
+    designs (native_prep.sweep_specs), or a function (a, b) -> the records of designs [a, b),
+    called per block inside the pipeline (so their cost overlaps the previous block's solve).
+    timings: optional list that receives,
+    per block, the host seconds of (design preparation, case set + tables + uploads, solve
+    enqueue, DesignBatch host part, DesignBatch upload part)."""
     import torch
     from .solver import prepare_batch
     design_idx = np.asarray(design_idx, dtype=np.int64)
@@ -178,25 +193,44 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
     cuts = np.linspace(0, nd, max(1, min(chunks, nd)) + 1).round().astype(int)
     dev = torch.device("cuda", device)
     compute = torch.cuda.current_stream(dev)
-    copy = torch.cuda.Stream(dev)
+    copy = _copy_stream(dev)
     parts, keep = [], []
     for a, b in zip(cuts[:-1], cuts[1:]):
         if b <= a:
             continue
         lo, hi = np.searchsorted(design_idx, [a, b])
+        t0 = time.perf_counter()
         with torch.cuda.stream(copy):
+            sp = None if specs is None else (specs(a, b) if callable(specs) else specs[a:b])
             B = DesignBatch(designs[a:b], statics=statics if isinstance(statics, dict) or statics is None
-                            else statics[a:b], device=device, pool=pool, native=True)
+                            else statics[a:b], device=device, pool=pool, native=True, specs=sp, threads=threads)
+            t1 = time.perf_counter()
             cs = B.case_set_grid(design_idx[lo:hi] - a, state_idx[lo:hi], sea_states)
             prep = prepare_batch(B.dds, cs, tables_stream=compute)
             ready = torch.cuda.Event()
             ready.record(copy)
         compute.wait_event(ready)
+        t2 = time.perf_counter()
         res = B.solve(None, cs, tol=tol, want=want, prepared=prep)   # on the solve stream
+        if timings is not None:
+            timings.append((t1 - t0, t2 - t1, time.perf_counter() - t2, B.host_seconds, B.upload_seconds))
         parts.append(res)
         keep.append((B, cs, prep, res))
     out = {k: torch.cat([r[k] for r in parts], 0) for k in parts[0]}
     return out, keep
+
+
+_COPY_STREAMS = {}
+
+
+def _copy_stream(dev):
+    """One upload stream per device, kept across sweeps: the caching allocator keeps its
+    blocks per stream, so a fresh stream per call would allocate every upload buffer anew."""
+    import torch
+    key = dev.index
+    if key not in _COPY_STREAMS:
+        _COPY_STREAMS[key] = torch.cuda.Stream(dev)
+    return _COPY_STREAMS[key]
 
 
 def prepare_design(job):

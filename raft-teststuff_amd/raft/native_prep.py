@@ -123,6 +123,14 @@ def _member_spec(mi, heads, dlsMax_default, potModMaster, is_platform):
 def design_spec(design, r6=None, statics=None, heading_adjust=0.0):
     """The spec record of one single-FOWT design (layout: csrc/rh_prep.h).  statics: the
     FOWT.setStatics entries that override the computed ones (and C_moor, MoorPy's stiffness)."""
+    head, blocks, rots = _spec_parts(design, r6, statics, heading_adjust)
+    return np.concatenate([head, np.asarray([x for blk in blocks for x in blk], dtype=float),
+                           np.asarray(rots, dtype=float).ravel()])
+
+
+def _spec_parts(design, r6, statics, heading_adjust):
+    """design_spec in pieces: (header + given statics, one value list per member entry, rotor
+    rows); the member blocks follow the header back to back, in platform-member order."""
     site, plat = design["site"], design["platform"]
     rho = get_from_dict(site, "rho_water", default=1025.0)
     g = get_from_dict(site, "g", default=9.81)
@@ -133,7 +141,7 @@ def design_spec(design, r6=None, statics=None, heading_adjust=0.0):
     for mi in plat["members"]:
         hd = mi.get("heading", 0.0)
         hd = hd if isinstance(hd, (list, tuple, np.ndarray)) else [hd]
-        blocks += _member_spec(mi, [float(h) + heading_adjust for h in hd], dlsMax, potModMaster, True)
+        blocks.append(_member_spec(mi, [float(h) + heading_adjust for h in hd], dlsMax, potModMaster, True))
         nmemb += 1
     rots = []
     turb = design.get("turbine")
@@ -143,7 +151,7 @@ def design_spec(design, r6=None, statics=None, heading_adjust=0.0):
             ms = turb.get(key)
             if ms is not None:
                 for mem in (ms if isinstance(ms, list) else [ms] * nrot):
-                    blocks += _member_spec(mem, [0.0], 5.0, 0, False)
+                    blocks.append(_member_spec(mem, [0.0], 5.0, 0, False))
                     nmemb += 1
         hhub = np.atleast_1d(get_from_dict(turb, "hHub", shape=-1, default=100.0))
         if np.any(hhub < 0):
@@ -183,8 +191,41 @@ def design_spec(design, r6=None, statics=None, heading_adjust=0.0):
     hdr = [MAGIC, nmemb, len(rots), rho, g, *(np.zeros(6) if r6 is None else np.asarray(r6, dtype=float)),
            *[1.0 if k in statics else 0.0 for k in STATIC_KEYS]]
     given = [np.asarray(statics[k], dtype=float).ravel() for k in STATIC_KEYS if k in statics]
-    return np.concatenate([np.asarray(hdr, dtype=float), *given, np.asarray(blocks, dtype=float),
-                           np.asarray(rots, dtype=float).ravel()])
+    return np.concatenate([np.asarray(hdr, dtype=float), *given]), blocks, rots
+
+
+def sweep_specs(base, mults, r6=None, statics=None):
+    """The spec records of parametersweep variants of `base` (raft/sweep.py sweep_variant with
+    each row of `mults`), without building a design dict per variant: the base record is
+    flattened once, and per variant only the fields the sweep edits -- rA, rB and d of the
+    first four platform members (raft/sweep.py variant_members) -- are rewritten in place,
+    with the same parsing (_vec / _pairs) design_spec applies.  Equal, value for value, to
+    design_spec(sweep_variant(base, m)) (tests/test_native_prep.py)."""
+    from .sweep import variant_members
+    head, blocks, rots = _spec_parts(base, r6, statics, 0.0)
+    spec0 = np.concatenate([head, np.asarray([x for blk in blocks for x in blk], dtype=float),
+                            np.asarray(rots, dtype=float).ravel()])
+    plat = base["platform"]["members"]
+    slots, off = [], len(head)
+    for i, blk in enumerate(blocks):
+        if i < 4:
+            n, nh, circ = int(blk[5]), int(blk[7]), blk[1] != 0.0
+            o_r = off + 12                          # head (12), then rA (3), rB (3), heads, stations
+            o_d = o_r + 6 + nh + n
+            slots.append((o_r, o_d, n, circ))
+        off += len(blk)
+    if len(slots) < 4 or len(plat) < 4:
+        raise ValueError("sweep_specs: the sweep edits four platform members")
+    out = []
+    for m in np.atleast_2d(mults):
+        s = spec0.copy()
+        for (o_r, o_d, n, circ), mi in zip(slots, variant_members(base, m)):
+            s[o_r:o_r + 3] = [float(x) for x in mi["rA"]]
+            s[o_r + 3:o_r + 6] = [float(x) for x in mi["rB"]]
+            dd = _vec(mi, "d", n) if circ else _pairs(mi, "d", n)
+            s[o_d:o_d + len(dd)] = dd
+        out.append(s)
+    return out
 
 
 class PreparedDesigns:

@@ -36,9 +36,18 @@ def sweep_variant(design, mult):
     matters for its 3-level grid, not for an independent draw.  Mooring point moves
     (:62-66, :78-83) are skipped: the mooring stiffness is an input here."""
     d = copy.deepcopy(design)
+    d["platform"]["members"][:4] = variant_members(design, mult)
+    return d
+
+
+def variant_members(design, mult):
+    """The four platform members sweep_variant edits (copies, in member order), with its
+    assignments applied; everything else of the variant is the base design."""
     base = sweep_baseline(design)
     a, b, c, dd, e = (base[k] * float(f) for k, f in zip(SWEEP_VARIABLES, mult))
-    m = d["platform"]["members"]
+    # shallow copies suffice: every list edited below (rA, rB, the pontoon's d) is replaced by
+    # a fresh list before it is written
+    m = [dict(mm) for mm in design["platform"]["members"][:4]]
     for mm in m[:4]:
         mm["rA"] = [float(x) for x in mm["rA"]]
         mm["rB"] = [float(x) for x in mm["rB"]]
@@ -65,7 +74,7 @@ def sweep_variant(design, mult):
     m[2]["d"][1] = e
     m[2]["rA"][2] = m[0]["rA"][2] + e / 2
     m[2]["rB"][2] = m[1]["rA"][2] + e / 2
-    return d
+    return m
 
 
 def sweep_multipliers(n_designs, seed=20241016, lower=0.75, upper=1.25):

@@ -231,6 +231,12 @@ def test_pipelined_sweep_equals_one_batch():
     out, keep = solve_sweep(designs, st, idx, sidx, grid, chunks=3, want=("std", "psd"))
     B = DesignBatch(designs, statics=st, native=True)
     ref = B.solve(None, B.case_set_grid(idx, sidx, grid), want=("std", "psd"))
+    # the bench's path: spec records from the base and the multipliers, built per block
+    from raft.native_prep import sweep_specs
+    mult = sweep_multipliers(7, seed=13)
+    out2, keep2 = solve_sweep([base] * len(designs), st, idx, sidx, grid, chunks=3, want=("std", "psd"),
+                              specs=lambda a, b: sweep_specs(base, mult[a:b], statics=st), threads=4)
     torch.cuda.synchronize()
     for k in ("Xi", "iters", "status", "std", "psd"):
         assert torch.equal(out[k], ref[k]), k
+        assert torch.equal(out2[k], ref[k]), k

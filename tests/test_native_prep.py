@@ -75,6 +75,25 @@ def test_native_sweep_variants_match_python():
         _compare(_python_tables(d, st)[0], P.host_tables(i))
 
 
+def test_sweep_specs_equal_design_spec_of_variants():
+    """native_prep.sweep_specs (the base record with the swept fields rewritten, the C5 bench
+    path) equals design_spec of each sweep_variant dict, value for value; the base design is
+    left untouched."""
+    import copy
+    from raft.native_prep import design_spec, sweep_specs
+    from raft.sweep import sweep_multipliers, sweep_variant
+    base = load_design("VolturnUS-S_example")
+    base["settings"]["min_freq"] = 0.0002
+    keep = copy.deepcopy(base)
+    st = {"C_moor": C_MOOR}
+    mult = np.vstack([sweep_multipliers(40, seed=11), np.ones(5), np.full(5, 0.75), np.full(5, 1.25)])
+    fast = sweep_specs(base, mult, statics=st)
+    assert len(fast) == len(mult)
+    for m, s in zip(mult, fast):
+        np.testing.assert_array_equal(s, design_spec(sweep_variant(base, m), statics=st))
+    assert base == keep
+
+
 def test_native_pose_and_mooring_stiffness():
     """A displaced, rotated pose (members, RNA and hydrostatics move) and the mooring
     stiffness computed from the design's own mooring system (raft/mooring.py)."""
