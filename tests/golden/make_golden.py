@@ -529,7 +529,83 @@ def golden_f2nd_spectrum():
     print("wrote f2nd_spectrum.npz", file=sys.stderr)
 
 
+ROTOR_DESIGNS = {"IEA15MW": "tests/test_data/IEA15MW.yaml"}   # VolturnUS-S_example carries the same turbine
+
+
+def rotor_cases():
+    """Wind conditions of the rotor goldens: below / at / above rated and parked-region
+    speeds, misaligned inflow, every yaw mode, turbulence as an intensity and as IEC
+    class strings (NTM / ETM / EWM)."""
+    out = []
+    for U in (5.0, 10.59, 15.0, 25.0):
+        for hd, th, ym, ti in ((0.0, 0.0, 0, 0.1), (30.0, 0.0, 0, "IB_NTM"), (-20.0, 10.0, 1, "IIC_ETM"),
+                               (45.0, 0.0, 2, "IA_EWM"), (10.0, 25.0, 3, 0.14)):
+            out.append(dict(wind_speed=U, wind_heading=hd, turbine_heading=th, turbulence=ti, yaw_mode=ym))
+    return out
+
+
+def golden_rotor():
+    """Rotor aero-servo linearisation (raft/raft_rotor.py): the reference's Rotor run with the
+    scripted CCBlade stand-in of tests/golden/fake_ccblade.py (CCBlade itself is a third-party
+    dependency that is not installed).  Pins RAFT's own rotor code: the CCBlade inputs it builds
+    (polars on the angle-of-attack grid, PCHIP over the span, blade tables) and Rotor.calcAero /
+    IECKaimal for aeroServoMod 1 and 2.  Writes rotor_<design>.npz and the turbine dicts."""
+    import raft.raft_rotor as RR
+    from raft.helpers import getFromDict
+    sys.path.insert(0, HERE)
+    from fake_ccblade import FakeAirfoil, FakeCCBlade
+    RR.CCBlade, RR.CCAirfoil = FakeCCBlade, FakeAirfoil
+    # the reference's calcAero allocates with np.complex_, an alias NumPy 2 removed; it names
+    # complex128 (the same dtype), so restore the alias for the run
+    if not hasattr(np, "complex_") or np.__dict__.get("complex_") is None:
+        np.complex_ = np.complex128
+    for name, rel in ROTOR_DESIGNS.items():
+        d = load_design(os.path.join(REF, rel))
+        turb = d["turbine"]
+        turb["nrotors"] = 1
+        site = d["site"]
+        turb["rho_air"] = getFromDict(site, "rho_air", shape=0, default=1.225)
+        turb["mu_air"] = getFromDict(site, "mu_air", shape=0, default=1.81e-05)
+        turb["shearExp_air"] = getFromDict(site, "shearExp_air", shape=0, default=0.12)
+        turb["rho_water"] = getFromDict(site, "rho_water", shape=0, default=1025.0)
+        turb["mu_water"] = getFromDict(site, "mu_water", shape=0, default=1.0e-03)
+        turb["shearExp_water"] = getFromDict(site, "shearExp_water", shape=0, default=0.12)
+        with open(os.path.join(HERE, "designs", name + "_turbine.json"), "w") as f:
+            json.dump(turb, f, indent=1, default=str)
+        w = np.arange(0.01, 0.3 + 0.005, 0.01) * 2 * np.pi
+        out = {"w": w}
+        cases = rotor_cases()
+        for mod in (1, 2):
+            t = json.loads(json.dumps(turb, default=str))
+            t["aeroServoMod"] = mod
+            rot = RR.Rotor(t, w, 0)
+            if mod == 1:
+                for k, v in rot.ccblade.args.items():
+                    out["cc_" + k] = np.asarray(v)
+                out["Ca_interp"] = rot.Ca_interp
+                out["r_thick_interp"] = rot.r_thick_interp
+                out["cpmin_interp"] = rot.cpmin_interp
+            for ic, c in enumerate(cases):
+                rot.yaw_mode = c["yaw_mode"]
+                case = {k: v for k, v in c.items() if k != "yaw_mode"}
+                rot.setPosition(np.array([0.0, 0.0, 0.0, 0.0, 0.02, 0.1]))
+                f0, f, a, b = rot.calcAero(dict(case))
+                U, V, W, Rot = rot.IECKaimal(dict(case))
+                tag = f"m{mod}_c{ic}"
+                out[tag + "_f0"], out[tag + "_f"], out[tag + "_a"], out[tag + "_b"] = f0, f, a, b
+                out[tag + "_kaimal"] = np.array([U, V, W, Rot])
+                out[tag + "_call"] = np.array(rot.ccblade.calls[-1])
+                out[tag + "_yaw"] = np.array([rot.yaw, rot.turbine_heading])
+                if mod == 2:
+                    out[tag + "_C"] = rot.C
+        out["cases"] = np.array(json.dumps(cases))
+        np.savez_compressed(os.path.join(HERE, f"rotor_{name}.npz"), **out)
+        print(f"wrote rotor_{name}.npz ({len(cases)} cases x 2 modes)", file=sys.stderr)
+
+
 def main(which):
+    if "rotor" in which:
+        golden_rotor()
     if "spectrum" in which:
         golden_f2nd_spectrum()
     if "qtf12d" in which:
