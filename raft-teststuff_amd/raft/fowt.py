@@ -6,10 +6,12 @@ argument meaning, return values and the side-effect attributes downstream code r
 the per-design preparation (members, node tables, linear matrices) and the device buffers.
 
 The statics (member inertia / hydrostatics / RNA) are computed on
-the host by raft/statics.py.  Not built here: MoorPy mooring (its
-stiffness C_moor is an input, FOWT.setStatics), rotor aerodynamics (CCBlade), BEM (pyHAMS)
-and BEM coefficient files (potFirstOrder=1).  External .12d QTFs (potSecOrder=2) are read on
-the host (qtf_io.read_qtf12d) and applied on the device (rh_force_2nd).
+the host by raft/statics.py, the mooring by raft/mooring.py, and an operating rotor's
+aero-servo coefficients by raft/rotor.py (its blade-element solve is CCBlade's, a dependency of
+the reference that has to be installed for wind > 0).  Not built here: BEM
+(pyHAMS), BEM coefficient files (potFirstOrder=1) and underwater rotors.  External .12d QTFs
+(potSecOrder=2) are read on the host (qtf_io.read_qtf12d) and applied on the device
+(rh_force_2nd).
 """
 import os
 import ctypes
@@ -17,12 +19,24 @@ import ctypes
 import numpy as np
 
 from . import _native as N
-from .hydro_math import DEG2RAD, get_from_dict, wave_numbers, translate_matrix_6to6
+from .hydro_math import DEG2RAD, alternator, get_from_dict, wave_numbers, translate_matrix_6to6
 from .member import Member
+from .rotor import Rotor
 from .statics import RNA, fowt_statics
 from .prep import DeviceDesign
 
 STATICS_KEYS = ["M_struc", "B_struc", "C_struc", "C_hydro", "W_struc", "W_hydro"]
+# turbine inputs a full Rotor (aerodynamics and control, raft/rotor.py) needs
+AERO_KEYS = ("blade", "airfoils", "wt_ops", "pitch_control", "torque_control", "gear_ratio", "I_drivetrain",
+             "nBlades", "Rhub", "precone")
+
+
+def transform_force(f_in, offset):
+    """transformForce with an offset only (raft/helpers.py:404-452): a force (and moment) at
+    `offset` as force and moment about the origin."""
+    f = np.array(f_in) if len(f_in) == 6 else np.hstack([f_in, [0, 0, 0]])
+    f[3:] += np.cross(offset, f[:3])
+    return f
 
 
 class _Zeros:
@@ -98,10 +112,18 @@ class FOWT:
                     self.memberList.append(Member(mem, self.nw))
             tcopy = dict(turb)
             tcopy["nrotors"] = self.nrotors
-            if all(k in tcopy for k in ("mRNA", "IxRNA", "IrRNA", "xCG_RNA", "overhang", "shaft_tilt")):
-                self.rnaList = [RNA(tcopy, ir, get_from_dict) for ir in range(self.nrotors)]
             hhub = np.atleast_1d(get_from_dict(turb, "hHub", shape=-1, default=100.0))
             self._rotor_submerged = bool(np.any(hhub < 0))
+            if all(k in tcopy for k in ("mRNA", "IxRNA", "IrRNA", "xCG_RNA", "overhang", "shaft_tilt")):
+                if not self._rotor_submerged and all(k in tcopy for k in AERO_KEYS):
+                    # full rotors (raft/rotor.py): the site's fluid properties are copied into
+                    # the turbine inputs as raft/raft_fowt.py:85-90 does
+                    for k, dflt in (("rho_air", 1.225), ("mu_air", 1.81e-05), ("shearExp_air", 0.12),
+                                    ("rho_water", 1025.0), ("mu_water", 1.0e-03), ("shearExp_water", 0.12)):
+                        tcopy[k] = get_from_dict(site, k, shape=0, default=dflt)
+                    self.rnaList = [Rotor(tcopy, self.w, ir) for ir in range(self.nrotors)]
+                else:
+                    self.rnaList = [RNA(tcopy, ir, get_from_dict) for ir in range(self.nrotors)]
             self._aero_mod = np.atleast_1d(get_from_dict(turb, "aeroServoMod", shape=-1, default=1))
         self.potSecOrder = get_from_dict(plat, "potSecOrder", dtype=int, default=0)
         if self.potSecOrder == 1:
@@ -138,6 +160,7 @@ class FOWT:
         self.B_gyro = np.zeros([6, 6, max(self.nrotors, 1)])
         self.A_aero = np.zeros([6, 6, self.nw, self.nrotors])
         self.B_aero = np.zeros([6, 6, self.nw, self.nrotors])
+        self.f_aero = np.zeros([6, self.nw, self.nrotors], dtype=complex)
         self._statics = None
         for k in ("M_struc", "B_struc", "C_struc", "C_hydro"):
             setattr(self, k, np.zeros([6, 6]))   # filled by calcStatics
@@ -147,6 +170,12 @@ class FOWT:
         self.nWaves = 1
 
     # ------------------------------------------------------------------ set-up
+    @property
+    def rotorList(self):
+        """The reference's name for the rotors (raft/raft_fowt.py:201): Rotor objects when the
+        turbine carries its aerodynamic inputs, else their RNA pose/inertia part."""
+        return self.rnaList
+
     def setPosition(self, r6):
         """raft/raft_fowt.py:260-288: members, rotors and this FOWT's mooring system; the
         mooring stiffness C_moor and mean force F_moor0 follow the new pose (unless a C_moor
@@ -246,19 +275,40 @@ class FOWT:
         return D
 
     def calcTurbineConstants(self, case, ptfm_pitch=0):
-        """raft/raft_fowt.py:773-845 restricted to what the accelerated path supports: rotor
-        aerodynamics (CCBlade) are out of scope, so only cases without aero loads run."""
+        """raft/raft_fowt.py:773-845: for every operating rotor with aeroServoMod > 0 at wind
+        speed > 0, the aero-servo added mass, damping and wind excitation of Rotor.calcAero
+        (raft/rotor.py; CCBlade evaluates the blades) moved from the hub to the platform
+        reference point (translateMatrix6to6DOF / transformForce with r_hub_rel), the mean aero
+        loads f_aero0 and the rotor's gyroscopic damping B_gyro.  Host work: 6x6 per bin."""
         status = get_from_dict(case, "turbine_status", shape=0, dtype=str, default="operating")
-        speed = get_from_dict(case, "wind_speed", shape=0, default=10.0)
+        had_aero = bool(np.any(self.A_aero) or np.any(self.B_aero) or np.any(self.B_gyro))
         self.A_aero = np.zeros([6, 6, self.nw, self.nrotors])
         self.B_aero = np.zeros([6, 6, self.nw, self.nrotors])
+        self.f_aero = np.zeros([6, self.nw, self.nrotors], dtype=complex)
         self.f_aero0 = np.zeros([6, self.nrotors])
         self.B_gyro = np.zeros([6, 6, max(self.nrotors, 1)])
         if self._rotor_submerged:
             raise NotImplementedError("underwater rotors (raft/raft_rotor.py) are outside the accelerated path")
-        if status == "operating" and self.nrotors > 0 and speed > 0.0 and np.any(np.asarray(self._aero_mod) > 0):
-            raise NotImplementedError("rotor aerodynamics (CCBlade, raft/raft_rotor.py:788-1005) are outside the "
-                                      "accelerated path: run with wind_speed=0 or a non-operating turbine")
+        if status == "operating":
+            speed = get_from_dict(case, "wind_speed", shape=0, default=10.0)
+            for ir in range(self.nrotors):
+                if not (int(np.atleast_1d(self._aero_mod)[ir]) > 0 and speed > 0.0):
+                    continue
+                rot = self.rnaList[ir] if ir < len(self.rnaList) else None
+                if not isinstance(rot, Rotor):
+                    raise NotImplementedError("rotor aerodynamics need the turbine's blade, airfoil, operating-point "
+                                              "and control inputs (raft/raft_rotor.py:37-374)")
+                f0, f, a, b = rot.calcAero(case)
+                for iw in range(self.nw):
+                    self.A_aero[:, :, iw, ir] = translate_matrix_6to6(a[:, :, iw], rot.r_hub_rel)
+                    self.B_aero[:, :, iw, ir] = translate_matrix_6to6(b[:, :, iw], rot.r_hub_rel)
+                    self.f_aero[:, iw, ir] = transform_force(f[:, iw], rot.r_hub_rel)
+                self.f_aero0[:, ir] = transform_force(f0, rot.r_hub_rel)
+                Omega_rpm = np.interp(speed, rot.Uhub, rot.Omega_rpm)
+                IO_rotor = rot.I_drivetrain * (rot.q * Omega_rpm * 2 * np.pi / 60)
+                self.B_gyro[3:, 3:, ir] = alternator(IO_rotor)
+        if had_aero or np.any(self.A_aero) or np.any(self.B_aero) or np.any(self.B_gyro):
+            self._dd = self._host = None          # the per-bin M and B of the device design change
 
     def calcHydroConstants(self):
         """raft/raft_fowt.py:848-880 (strip-theory members)."""
@@ -537,13 +587,71 @@ class FOWT:
             means[k] = mt * self.g * hArm * np.sin(self.Xi0[4])                      # :1965-1966, f_aero0 = 0
         return coef, means
 
+    def _aero_outputs(self, results, case):
+        """The channels operating rotors change (host arithmetic over nw values per rotor):
+        the tower-base moment with the aero reaction term and the mean thrust moment
+        (raft/raft_fowt.py:1950-1970), and the rotor azimuth / speed / torque / pitch response
+        through the control transfer function C of Rotor.calcAero (:1976-2045)."""
+        rms = lambda x: np.sqrt(0.5 * np.sum(np.abs(x) ** 2))                      # getRMS
+        psd = lambda x: np.sum(0.5 * np.abs(x) ** 2 / self.dw, axis=0)              # getPSD, 2-D
+        w, Xi = self.w, self.Xi
+        for ir, rot in enumerate(self.rnaList[:len(self.mtower)]):
+            if not (np.any(self.A_aero[..., ir]) or np.any(self.B_aero[..., ir]) or np.any(self.f_aero0[:, ir])):
+                continue
+            mt = self.mtower[ir] + rot.mRNA
+            zCG = (self.rCG_tow[ir][2] * self.mtower[ir] + rot.r_rel[2] * rot.mRNA) / mt
+            tower = self.memberList[self.nplatmems + ir]
+            zBase = tower.rA[2]
+            hArm = zCG - zBase
+            ICG = (translate_matrix_6to6(tower.M_struc, [0, 0, -zCG])[4, 4] + rot.mRNA * (rot.r_rel[2] - zCG) ** 2
+                   + rot.IrRNA)
+            aCG = -w ** 2 * (Xi[:, 0, :] + zCG * Xi[:, 4, :])
+            M_I = -mt * aCG * hArm - ICG * (-w ** 2 * Xi[:, 4, :])
+            M_w = mt * self.g * hArm * Xi[:, 4]
+            M_X = -(-w ** 2 * self.A_aero[0, 0, :, ir] + 1j * w * self.B_aero[0, 0, :, ir]) * (rot.r_rel[2] - zBase) ** 2 \
+                * Xi[:, 4, :]
+            dyn = M_I + M_w + 0.0 + M_X
+            avg = mt * self.g * hArm * np.sin(self.Xi0[4]) + transform_force(self.f_aero0[:, ir], [0, 0, -hArm])[4]
+            results["Mbase_avg"][ir] = avg
+            results["Mbase_std"][ir] = rms(dyn)
+            results["Mbase_PSD"][:, ir] = psd(dyn)
+            results["Mbase_max"][ir] = avg + 3 * results["Mbase_std"][ir]
+            results["Mbase_min"][ir] = avg - 3 * results["Mbase_std"][ir]
+        speed = get_from_dict(case, "wind_speed", shape=0, default=10.0)
+        for ir, rot in enumerate(self.rnaList):
+            if not (isinstance(rot, Rotor) and rot.aeroServoMod > 1 and speed > 0.0 and hasattr(rot, "C")):
+                continue
+            XiHub = Xi[:, 0, :] + rot.r_rel[2] * Xi[:, 4, :]
+            phi = np.zeros_like(XiHub, dtype=complex)
+            for ih in range(Xi.shape[0] - 1):
+                phi[ih] = rot.C * XiHub[ih]
+            phi[-1] = rot.C * (XiHub[-1] - rot.V_w / (1j * w))
+            omega_w = 1j * w * phi
+            torque_w = (1j * w * rot.kp_tau + rot.ki_tau) * phi
+            pitch_w = (1j * w * rot.kp_beta + rot.ki_beta) * phi
+            rpm = lambda x: x / 0.1047                                                  # radps2rpm (helpers.py:32)
+            results["omega_avg"][ir] = rot.Omega_case
+            results["omega_std"][ir] = rpm(rms(omega_w))
+            results["omega_max"][ir] = results["omega_avg"][ir] + 2 * results["omega_std"][ir]
+            results["omega_min"][ir] = results["omega_avg"][ir] - 2 * results["omega_std"][ir]
+            results["omega_PSD"][:, ir] = rpm(1) ** 2 * psd(omega_w)
+            results["torque_avg"][ir] = rot.aero_torque / rot.Ng
+            results["torque_std"][ir] = rms(torque_w)
+            results["torque_PSD"][:, ir] = psd(torque_w)
+            results["power_avg"][ir] = rot.aero_power
+            results["bPitch_avg"][ir] = rot.pitch_case
+            results["bPitch_std"][ir] = rms(pitch_w) * 57.29577951308232
+            results["bPitch_PSD"][:, ir] = 57.29577951308232 ** 2 * psd(pitch_w)
+            results["wind_PSD"] = 0.5 * np.abs(rot.V_w) ** 2 / self.dw
+
     def saveTurbineOutputs(self, results, case):
-        """raft/raft_fowt.py:1821-1974: platform motions (RMS, PSD, RA), nacelle acceleration
-        AxRNA_* and tower-base moment Mbase_* per rotor (rh_channel_stats on the device) and
-        wave_PSD.  Rotor-control channels (omega/torque/power/bPitch) are the reference's zeros
-        because aero-servo is inactive in every case the accelerated path runs (wind 0 or a
-        non-operating turbine, raft/raft_fowt.py:2006).  Mooring tensions (Tmoor_*) need a
-        mooring system (MoorPy in the reference)."""
+        """raft/raft_fowt.py:1821-2045: platform motions (RMS, PSD, RA), nacelle acceleration
+        AxRNA_* and tower-base moment Mbase_* per rotor (rh_channel_stats on the device; with an
+        operating rotor the aero reaction term and mean thrust moment are added on the host,
+        _aero_outputs) and wave_PSD.  Rotor-control channels (omega/torque/power/bPitch,
+        wind_PSD) come from the rotor's control transfer function when aeroServoMod > 1 and the
+        wind blows, else they are the reference's zeros.  Mooring tensions (Tmoor_*) need a
+        mooring system (raft/mooring.py; MoorPy in the reference)."""
         import torch
         self.Xi0 = self.r6 - np.array([self.x_ref, self.y_ref, 0, 0, 0, 0])
         stats = getattr(self, "_stats", None)
@@ -587,6 +695,7 @@ class FOWT:
             results[name] = np.zeros(nr)
         for name in ["omega_PSD", "torque_PSD", "bPitch_PSD"]:
             results[name] = np.zeros([self.nw, nr])
+        self._aero_outputs(results, case)
         if self.ms is not None and self.ms.lines:                                      # :1878-1898
             results.update(mooring_outputs(self.ms, self._xi_dev, self.w, self.device_index, self._xi_dev.shape[0]))
 

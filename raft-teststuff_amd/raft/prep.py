@@ -89,6 +89,13 @@ def linear_matrices(fowt):
         else np.zeros([6, 6])
     per_bin = bool(np.any(A_BEM) or np.any(B_BEM))
     C = (fowt.C_struc + fowt.C_moor) + fowt.C_hydro
+    A_aero, B_aero = getattr(fowt, "A_aero", None), getattr(fowt, "B_aero", None)
+    if A_aero is not None and np.ndim(A_aero) == 4 and (np.any(A_aero) or np.any(B_aero)):
+        # operating rotors: the reference's sums, in its order (raft/raft_model.py:887-889, 911-912)
+        M_turb, B_turb = np.sum(A_aero, axis=3), np.sum(B_aero, axis=3)
+        M = ((M_turb + fowt.M_struc[:, :, None]) + A_BEM) + fowt.A_hydro_morison[:, :, None]
+        B = ((B_turb + fowt.B_struc[:, :, None]) + B_BEM) + B_gyro[:, :, None]
+        return np.moveaxis(M, 2, 0).copy(), np.moveaxis(B, 2, 0).copy(), C, True
     if per_bin:
         M = (fowt.M_struc[:, :, None] + A_BEM) + fowt.A_hydro_morison[:, :, None]
         B = (fowt.B_struc[:, :, None] + B_BEM) + B_gyro[:, :, None]

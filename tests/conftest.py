@@ -115,3 +115,26 @@ def oracle_tables_of(fowt):
     for k in ["M_struc", "B_struc", "C_struc", "C_hydro", "C_moor", "A_hydro_morison"]:
         T[k] = np.array(getattr(fowt, k), dtype=float)
     return T
+
+
+def aero_model(T, mod, monkeypatch):
+    """VolturnUS-S_example with its full turbine (blade, polars, schedule, controls) and the
+    scripted CCBlade, statics from the golden (the reference's own), as golden_aero ran it."""
+    import raft
+    import raft.rotor as R
+    sys.path.insert(0, GOLDEN)
+    from fake_ccblade import FakeAirfoil, FakeCCBlade
+    monkeypatch.setattr(R, "ccblade_classes", lambda: (FakeCCBlade, FakeAirfoil))
+    d = load_design("VolturnUS-S_example")
+    with open(os.path.join(GOLDEN, "designs", "IEA15MW_turbine.json")) as f:
+        turb = json.load(f)
+    for k in ("blade", "airfoils", "wt_ops", "pitch_control", "torque_control", "gear_ratio", "I_drivetrain",
+              "nBlades", "Rhub", "precone"):
+        d["turbine"][k] = turb[k]
+    d["turbine"]["aeroServoMod"] = mod
+    m = raft.Model(d, statics=[statics_of(T)])
+    f = m.fowtList[0]
+    f.setPosition(T["r6"])
+    f.calcStatics()
+    f.calcHydroConstants()
+    return m, f

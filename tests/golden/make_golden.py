@@ -154,7 +154,7 @@ def case_dict(design, row):
     return c
 
 
-def golden_solve(tag, yaml_path, cases, settings=None, keep_Z=False):
+def golden_solve(tag, yaml_path, cases, settings=None, keep_Z=False, aero=False):
     settings = settings or {}
     if isinstance(yaml_path, dict):          # an in-memory design (C5 sweep variants)
         design = yaml_path
@@ -167,6 +167,9 @@ def golden_solve(tag, yaml_path, cases, settings=None, keep_Z=False):
     caseout = {k: [] for k in ["Xi", "iters", "conv", "B_drag", "F_iner", "F_drag", "zeta", "S", "seconds"]}
     if keep_Z:
         caseout["Z"] = []
+    if aero:
+        for k in ["A_aero", "B_aero", "f_aero0", "B_gyro"]:
+            caseout[k] = []
     metrics = []
     for c in cases:
         case = dict(c)
@@ -185,6 +188,9 @@ def golden_solve(tag, yaml_path, cases, settings=None, keep_Z=False):
         caseout["seconds"].append(dt)
         if keep_Z:
             caseout["Z"].append(fowt.Z.copy())
+        if aero:
+            for k in ["A_aero", "B_aero", "f_aero0", "B_gyro"]:
+                caseout[k].append(np.array(getattr(fowt, k)).copy())
         res = {}
         fowt.saveTurbineOutputs(res, case)
         metrics.append(res)
@@ -200,6 +206,13 @@ def golden_solve(tag, yaml_path, cases, settings=None, keep_Z=False):
     for ch in ["AxRNA", "Mbase"]:
         for st in ["avg", "std", "max", "min", "PSD"]:
             out[f"out_{ch}_{st}"] = np.array([m[f"{ch}_{st}"] for m in metrics])
+    if aero:   # rotor-control channels (raft/raft_fowt.py:1976-2045)
+        for ch in ["omega", "torque", "bPitch"]:
+            for st in ["avg", "std", "PSD"]:
+                out[f"out_{ch}_{st}"] = np.array([m[f"{ch}_{st}"] for m in metrics])
+        for k in ["omega_max", "omega_min", "power_avg", "wind_PSD"]:
+            if all(k in m for m in metrics):       # wind_PSD only with aeroServoMod > 1
+                out["out_" + k] = np.array([m[k] for m in metrics])
     out["out_metric_keys"] = np.array(sorted(metrics[0].keys()))
     out.update(rotor_inputs(fowt))
     out["nIter"] = np.int64(model.nIter)
@@ -207,6 +220,8 @@ def golden_solve(tag, yaml_path, cases, settings=None, keep_Z=False):
     keys = ["wave_spectrum", "wave_period", "wave_height", "wave_heading", "wave_gamma"]
     meta = [{k: (np.atleast_1d(c[k]).tolist() if k in c else None) for k in keys} for c in cases]
     out["cases_json"] = np.array(json.dumps(meta))
+    if aero:
+        out["cases_full_json"] = np.array(json.dumps(cases))
     np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
     print(f"wrote {tag}.npz", file=sys.stderr)
 
@@ -603,7 +618,29 @@ def golden_rotor():
         print(f"wrote rotor_{name}.npz ({len(cases)} cases x 2 modes)", file=sys.stderr)
 
 
+def golden_aero():
+    """Operating-rotor solves (wind > 0) of VolturnUS-S_example at its own nw = 200 grid, for
+    aeroServoMod 1 and 2, with the scripted CCBlade stand-in (tests/golden/fake_ccblade.py):
+    A_aero / B_aero / f_aero0 / B_gyro, Xi, iteration counts and every output channel."""
+    import raft.raft_rotor as RR
+    sys.path.insert(0, HERE)
+    from fake_ccblade import FakeAirfoil, FakeCCBlade
+    RR.CCBlade, RR.CCAirfoil = FakeCCBlade, FakeAirfoil
+    if not hasattr(np, "complex_") or np.__dict__.get("complex_") is None:
+        np.complex_ = np.complex128
+    cases = [dict(wind_speed=10.59, wind_heading=0.0, turbulence=0.1, turbine_status="operating", yaw_misalign=0,
+                  wave_spectrum="JONSWAP", wave_period=12.0, wave_height=6.0, wave_heading=0.0, wave_gamma=0.0),
+             dict(wind_speed=18.0, wind_heading=20.0, turbulence="IB_NTM", turbine_status="operating", yaw_misalign=0,
+                  wave_spectrum="JONSWAP", wave_period=8.0, wave_height=2.0, wave_heading=30.0, wave_gamma=0.0)]
+    for mod in (1, 2):
+        d = load_design(os.path.join(REF, "examples", "VolturnUS-S_example.yaml"))
+        d["turbine"]["aeroServoMod"] = mod
+        golden_solve(f"aero_mod{mod}", d, cases, aero=True)
+
+
 def main(which):
+    if "aero" in which:
+        golden_aero()
     if "rotor" in which:
         golden_rotor()
     if "spectrum" in which:

@@ -1,0 +1,53 @@
+"""GPU: operating-rotor solves (wind > 0) against the reference.
+
+tests/golden/make_golden.py golden_aero ran the reference's Model.solveDynamics and
+saveTurbineOutputs on VolturnUS-S_example (nw = 200) with its IEA-15MW rotor, aeroServoMod 1
+and 2, two wind/wave cases each, with the scripted CCBlade stand-in (tests/golden/
+fake_ccblade.py; CCBlade is a third-party dependency that is not installed).  The same stand-in
+drives this build: Rotor.calcAero's added mass and damping enter the device solve as per-bin
+M and B (k_solve_lds, mb_per_bin), so Xi, the iteration counts and every output channel,
+including the aero tower-base moment and the rotor speed / torque / pitch spectra, are checked."""
+import json
+
+import numpy as np
+import pytest
+
+from conftest import aero_model, load_golden
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-9
+
+
+def rel(a, b):
+    nb = np.linalg.norm(b)
+    return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
+
+
+@pytest.mark.parametrize("mod", [1, 2])
+def test_operating_rotor_solve_matches_reference(mod, monkeypatch):
+    T = load_golden(f"aero_mod{mod}")
+    m, f = aero_model(T, mod, monkeypatch)
+    for ic, case in enumerate(json.loads(str(T["cases_full_json"]))):
+        f.calcTurbineConstants(dict(case), ptfm_pitch=0)
+        Xi = m.solveDynamics(dict(case))
+        assert f.iterations == T["out_iters"][ic], (ic, f.iterations, T["out_iters"][ic])
+        assert rel(Xi, T["out_Xi"][ic]) < RTOL, rel(Xi, T["out_Xi"][ic])
+        assert rel(f.B_hydro_drag, T["out_B_drag"][ic]) < RTOL
+        res = {}
+        f.saveTurbineOutputs(res, case)
+        for dof in ["surge", "sway", "heave", "roll", "pitch", "yaw"]:
+            np.testing.assert_allclose(res[dof + "_std"], T[f"out_{dof}_std"][ic], rtol=RTOL)
+        for ch in ["AxRNA", "Mbase"]:
+            for st in ["avg", "std", "max", "min", "PSD"]:
+                ref = np.asarray(T[f"out_{ch}_{st}"][ic])
+                np.testing.assert_allclose(res[f"{ch}_{st}"], ref, rtol=RTOL, atol=RTOL * np.abs(ref).max(),
+                                           err_msg=f"{ch}_{st}")
+        for ch in ["omega", "torque", "bPitch"]:
+            for st in ["avg", "std", "PSD"]:
+                ref = np.asarray(T[f"out_{ch}_{st}"][ic])
+                np.testing.assert_allclose(res[f"{ch}_{st}"], ref, rtol=RTOL, atol=RTOL * max(np.abs(ref).max(), 1e-300),
+                                           err_msg=f"{ch}_{st}")
+        for k in ["omega_max", "omega_min", "power_avg", "wind_PSD"]:
+            if "out_" + k in T:
+                ref = np.asarray(T["out_" + k][ic])
+                np.testing.assert_allclose(res[k], ref, rtol=RTOL, atol=RTOL * max(np.abs(ref).max(), 1e-300), err_msg=k)

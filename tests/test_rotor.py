@@ -75,3 +75,19 @@ def test_calc_aero_needs_ccblade():
     assert rot.ccblade is None and rot.blade_r.size > 0
     with pytest.raises(NotImplementedError, match="CCBlade"):
         rot.calcAero(dict(wind_speed=10.0, wind_heading=0.0, turbulence=0.1))
+
+
+@pytest.mark.parametrize("mod", [1, 2])
+def test_turbine_constants_match_reference(mod, monkeypatch):
+    """FOWT.calcTurbineConstants at wind > 0 (raft/raft_fowt.py:773-845): A_aero, B_aero,
+    f_aero0 and B_gyro about the platform reference point, per golden_aero case."""
+    from conftest import aero_model, load_golden
+    T = load_golden(f"aero_mod{mod}")
+    m, f = aero_model(T, mod, monkeypatch)
+    for ic, case in enumerate(json.loads(str(T["cases_full_json"]))):
+        f.calcTurbineConstants(dict(case), ptfm_pitch=0)
+        for k in ("A_aero", "B_aero", "f_aero0", "B_gyro"):
+            ref = T["out_" + k][ic]
+            x = np.asarray(getattr(f, k))[..., :ref.shape[-1]] if k == "B_gyro" else getattr(f, k)
+            scale = max(np.abs(ref).max(), 1e-300)
+            assert np.abs(x - ref).max() <= 1e-12 * scale, (ic, k, np.abs(x - ref).max() / scale)
