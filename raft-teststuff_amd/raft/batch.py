@@ -165,7 +165,8 @@ class DesignBatch:
 
 
 def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, pool=None, chunks=4, tol=0.01,
-                want=("psd", "std"), timings=None, specs=None, threads=None):
+                want=("psd", "std"), timings=None, specs=None, threads=None, first=0.25,
+                last=0.5):
     """A design sweep solved in `chunks` design blocks, pipelined: while the device solves
     block k, the host prepares block k+1 (native preparation, raft/native_prep.py), so the
     host work hides behind the solve instead of preceding it.
@@ -180,6 +181,9 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
     with their tensors until the caller synchronises).  specs: optional spec records of the
     designs (native_prep.sweep_specs), or a function (a, b) -> the records of designs [a, b),
     called per block inside the pipeline (so their cost overlaps the previous block's solve).
+    first, last: the first and last blocks' sizes relative to the others (the device idles
+    while the first is prepared, and only the last block's solve runs after the host is done,
+    so small ones shorten the pipeline's fill and drain; 1 = equal blocks).
     timings: optional list that receives,
     per block, the host seconds of (design preparation, case set + tables + uploads, solve
     enqueue, DesignBatch host part, DesignBatch upload part)."""
@@ -190,7 +194,7 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
     if np.any(np.diff(design_idx) < 0):
         raise ValueError("solve_sweep: cases must be design-major (non-decreasing design index)")
     nd = len(designs)
-    cuts = np.linspace(0, nd, max(1, min(chunks, nd)) + 1).round().astype(int)
+    cuts = sweep_cuts(nd, chunks, first, last)
     dev = torch.device("cuda", device)
     compute = torch.cuda.current_stream(dev)
     copy = _copy_stream(dev)
@@ -218,6 +222,18 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
         keep.append((B, cs, prep, res))
     out = {k: torch.cat([r[k] for r in parts], 0) for k in parts[0]}
     return out, keep
+
+
+def sweep_cuts(nd, chunks, first=1.0, last=1.0):
+    """Block boundaries of a pipelined sweep over nd designs: `chunks` blocks, the first and
+    the last weighted `first` and `last` against 1 for the others."""
+    k = max(1, min(int(chunks), nd))
+    wts = np.ones(k)
+    if k > 1:
+        wts[0], wts[-1] = first, last
+    cuts = np.round(np.concatenate([[0.0], np.cumsum(wts)]) / wts.sum() * nd).astype(int)
+    cuts[-1] = nd
+    return np.maximum.accumulate(cuts)
 
 
 _COPY_STREAMS = {}

@@ -20,6 +20,25 @@ from .hydro_math import DEG2RAD, get_from_dict, wave_numbers
 from .solver import CaseSet, solve_batch
 
 
+class CaseMB:
+    """A per-case view of a DeviceDesign: the same node and wave tables, its own per-bin M and
+    B [nw, 6, 6] device tensors (an operating rotor's aero-servo terms for one case)."""
+
+    def __init__(self, base, M, B):
+        self.base, self._M, self._B = base, M, B
+
+    def __getattr__(self, name):
+        return getattr(self.__dict__["base"], name)
+
+    def ensure_headings(self, betas):
+        return self.base.ensure_headings(betas)
+
+    def struct(self):
+        d = N.RhDesign.from_buffer_copy(self.base.struct())
+        d.M, d.B, d.mb_per_bin = N.ptr(self._M), N.ptr(self._B), 1
+        return d
+
+
 class Model:
     def __init__(self, design, nTurbines=1, statics=None, device=0):
         """statics: optional per-FOWT dicts of calcStatics outputs (M_struc, C_struc, C_hydro,
@@ -458,16 +477,48 @@ class Model:
 
     def analyzeCasesBatch(self, cases, tol=0.01, want=("psd", "std", "zeta", "B_drag"), host=True):
         """Solve many single-sea-state cases in one device call (one workgroup per case).
-        cases: list of case dicts (wave_heading/spectrum/period/height/gamma).  Returns a dict
+        cases: list of case dicts (wave_heading/spectrum/period/height/gamma; with wind_speed
+        > 0 on an operating rotor, that case's aero-servo M and B from calcTurbineConstants).  Returns a dict
         of arrays: Xi [n,6,nw], iters, status, psd [n,6,nw], std [n,6], ...
         Arrays (nFOWT > 1) go through analyzeArrayBatch: Xi [n,6N,nw], iters [n,N], ..."""
         if self.nFOWT != 1:
             return self.analyzeArrayBatch(cases, tol=tol, host=host)
         fowt = self.fowtList[0]
         hd, sp, Hs, Tp, gm = self._case_columns(cases)
-        cs = CaseSet(np.zeros(len(cases), dtype=np.int32), hd, sp, Hs, Tp, gm)
-        res = solve_batch([fowt.device_design()], cs, self.nIter, self.XiStart, tol, want=want)
+        aero = [self._operating_rotor(fowt, c) for c in cases]
+        if not any(aero):
+            cs = CaseSet(np.zeros(len(cases), dtype=np.int32), hd, sp, Hs, Tp, gm)
+            res = solve_batch([fowt.device_design()], cs, self.nIter, self.XiStart, tol, want=want)
+            return res.host() if host else res
+        # operating rotors: each such case gets its own per-bin M and B (its rotors' aero-servo
+        # added mass and damping, FOWT.calcTurbineConstants) on the shared node and wave tables
+        import torch
+        from .prep import linear_matrices
+        fowt.calcTurbineConstants(dict(cases[0], wind_speed=0.0), ptfm_pitch=0)     # the aero-free design
+        base = fowt.device_design()
+        base.ensure_headings(np.unique(np.asarray(hd, dtype=float)) * DEG2RAD)
+        views, idx = [base], np.zeros(len(cases), dtype=np.int32)
+        for i, c in enumerate(cases):
+            if aero[i]:
+                fowt.calcTurbineConstants(dict(c), ptfm_pitch=0)
+                M, B, _, _ = linear_matrices(fowt)
+                f64 = dict(dtype=torch.float64, device=base.device)
+                views.append(CaseMB(base, torch.tensor(M, **f64).contiguous(), torch.tensor(B, **f64).contiguous()))
+                idx[i] = len(views) - 1
+        cs = CaseSet(idx, hd, sp, Hs, Tp, gm)
+        res = solve_batch(views, cs, self.nIter, self.XiStart, tol, want=want)
         return res.host() if host else res
+
+    @staticmethod
+    def _operating_rotor(fowt, case):
+        """Whether calcTurbineConstants gives this case aero terms (raft/raft_fowt.py:795-812).
+        A batch case without a wind_speed entry is a sea state alone (wind 0), as batch cases
+        have always been read here."""
+        if fowt.nrotors == 0:
+            return False
+        status = get_from_dict(case, "turbine_status", shape=0, dtype=str, default="operating")
+        speed = get_from_dict(case, "wind_speed", shape=0, default=0.0)
+        return status == "operating" and speed > 0.0 and bool(np.any(np.atleast_1d(fowt._aero_mod) > 0))
 
     @staticmethod
     def _case_columns(cases):

@@ -51,3 +51,31 @@ def test_operating_rotor_solve_matches_reference(mod, monkeypatch):
             if "out_" + k in T:
                 ref = np.asarray(T["out_" + k][ic])
                 np.testing.assert_allclose(res[k], ref, rtol=RTOL, atol=RTOL * max(np.abs(ref).max(), 1e-300), err_msg=k)
+
+
+def test_operating_rotor_cases_in_one_batch(monkeypatch):
+    """analyzeCasesBatch with operating rotors: every wind case of both aero goldens and the
+    wind-0 cases of c2_nw200 (same design and grid) in one launch; each case has its own
+    per-bin M and B (CaseMB) on the shared node and wave tables."""
+    cases, refs = [], []
+    T0 = None
+    for mod in (1, 2):
+        T = load_golden(f"aero_mod{mod}")
+        T0 = T0 or T
+        for ic, c in enumerate(json.loads(str(T["cases_full_json"]))):
+            cases.append((mod, c))
+            refs.append((T["out_Xi"][ic][0], T["out_iters"][ic]))
+    for mod in (1, 2):
+        m, f = aero_model(T0, mod, monkeypatch)
+        sel = [i for i, (md, _) in enumerate(cases) if md == mod]
+        W = load_golden("c2_nw200")
+        from conftest import golden_cases
+        calm = golden_cases(W)[:3]
+        res = m.analyzeCasesBatch([cases[i][1] for i in sel] + calm, want=("psd", "std"))
+        for j, i in enumerate(sel):
+            assert res["iters"][j] == refs[i][1], (i, res["iters"][j], refs[i][1])
+            assert rel(res["Xi"][j], refs[i][0]) < RTOL, rel(res["Xi"][j], refs[i][0])
+        for j in range(len(calm)):
+            k = len(sel) + j
+            assert res["iters"][k] == W["out_iters"][j]
+            assert rel(res["Xi"][k], W["out_Xi"][j][0]) < RTOL, rel(res["Xi"][k], W["out_Xi"][j][0])
