@@ -291,10 +291,12 @@ class FOWT:
             raise NotImplementedError("underwater rotors (raft/raft_rotor.py) are outside the accelerated path")
         if status == "operating":
             speed = get_from_dict(case, "wind_speed", shape=0, default=10.0)
+            mods = np.atleast_1d(self._aero_mod)
             for ir in range(self.nrotors):
-                if not (int(np.atleast_1d(self._aero_mod)[ir]) > 0 and speed > 0.0):
-                    continue
                 rot = self.rnaList[ir] if ir < len(self.rnaList) else None
+                mod = rot.aeroServoMod if isinstance(rot, Rotor) else mods[min(ir, len(mods) - 1)]
+                if not (mod > 0 and speed > 0.0):
+                    continue
                 if not isinstance(rot, Rotor):
                     raise NotImplementedError("rotor aerodynamics need the turbine's blade, airfoil, operating-point "
                                               "and control inputs (raft/raft_rotor.py:37-374)")

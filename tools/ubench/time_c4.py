@@ -14,3 +14,15 @@ if __name__ == "__main__":
     torch.cuda.set_device(0)
     r = bench.bench_c4(0, int(sys.argv[1]) if len(sys.argv) > 1 else 10, 1, 0, None)
     print(json.dumps({k: r[k] for k in ("value", "ms_per_step", "device_ms_per_step")} | {"kernel_ms": r["roofline"]["kernel_ms"]}))
+    from raft import _native as N
+    L = N.lib()
+    if hasattr(L, "rh_prof_read"):      # RH_PROF builds: phase cycles of the fixed-point launches
+        import ctypes
+        buf = (ctypes.c_ulonglong * 8)()
+        L.rh_prof_read(buf, 0)
+        v = list(buf)
+        nit = max(v[7], 1)
+        names = ["A/iter", "B/iter", "C-exc/iter", "C-solve/iter", "flags/iter"]
+        print("  cycles (s_memtime, wave 0, all launches): " + "  ".join(
+            f"{n}={x / nit:,.0f}" for n, x in zip(names, v[1:6])) + f"  prologue+epilogue total/iter={(v[0] + v[6]) / nit:,.0f}",
+            flush=True)
