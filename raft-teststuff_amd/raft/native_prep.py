@@ -257,6 +257,7 @@ class PreparedDesigns:
             L.rh_prep_free(h)
         self.info = info[:5 * nd].reshape(nd, 5)
         self.nw = len(w)
+        self._layouts = {}
 
     def __len__(self):
         return len(self.info)
@@ -264,13 +265,17 @@ class PreparedDesigns:
     def host_tables(self, i):
         """Design i's tables in the form of raft/prep.py host_tables (views of `packed`)."""
         o, n, mo, nn, nm = (int(x) for x in self.info[i])
-        nw = self.nw
-        shapes = [("w", (nw,)), ("k", (nw,)), ("node", (N.NF_COUNT, max(nn, 1))), ("memb", (N.MF_COUNT, max(nm, 1))),
-                  ("M", (6, 6)), ("B", (6, 6)), ("C", (6, 6))]
-        layout, off = {}, 0
-        for name, shp in shapes:
-            layout[name] = (off, shp)
-            off += int(np.prod(shp))
-        assert off == n
+        cached = self._layouts.get((nn, nm))
+        if cached is None:                          # one layout per (nodes, members) shape
+            nw = self.nw
+            shapes = [("w", (nw,)), ("k", (nw,)), ("node", (N.NF_COUNT, max(nn, 1))),
+                      ("memb", (N.MF_COUNT, max(nm, 1))), ("M", (6, 6)), ("B", (6, 6)), ("C", (6, 6))]
+            layout, off = {}, 0
+            for name, shp in shapes:
+                layout[name] = (off, shp)
+                off += int(np.prod(shp))
+            cached = self._layouts[(nn, nm)] = (layout, off)
+        layout, total = cached
+        assert total == n
         return dict(packed=self.packed[o:o + n], layout=layout, imat=None, mstart=self.mstart[mo:mo + nm + 1],
                     nn=nn, nm=nm, per_bin=False)
