@@ -79,3 +79,38 @@ def test_operating_rotor_cases_in_one_batch(monkeypatch):
             k = len(sel) + j
             assert res["iters"][k] == W["out_iters"][j]
             assert rel(res["Xi"][k], W["out_Xi"][j][0]) < RTOL, rel(res["Xi"][k], W["out_Xi"][j][0])
+
+
+def test_run_raft_with_operating_rotor(monkeypatch):
+    """runRAFT on VolturnUS-S_example with its own wind cases (16 m/s, class and intensity
+    turbulence) and the full rotor: mean offsets with the rotor thrust (solveStatics), then the
+    device solve with the aero M and B per bin.  MoorPy is absent, so no reference run covers
+    the offsets; the last case's response is checked against the CPU oracle on the same offset
+    tables, with the aero matrices as its per-bin added mass and damping."""
+    import os
+    import sys
+
+    import raft
+    import raft.rotor as R
+    from conftest import GOLDEN, load_design, oracle_tables_of
+    from oracle import raft_oracle as O
+    sys.path.insert(0, GOLDEN)
+    from fake_ccblade import FakeAirfoil, FakeCCBlade
+    monkeypatch.setattr(R, "ccblade_classes", lambda: (FakeCCBlade, FakeAirfoil))
+    d = load_design("VolturnUS-S_example")
+    with open(os.path.join(GOLDEN, "designs", "IEA15MW_turbine.json")) as fh:
+        turb = json.load(fh)
+    for k in ("blade", "airfoils", "wt_ops", "pitch_control", "torque_control", "gear_ratio", "I_drivetrain",
+              "nBlades", "Rhub", "precone"):
+        d["turbine"][k] = turb[k]
+    m = raft.runRAFT(d)
+    f = m.fowtList[0]
+    offs = np.array(m.results["mean_offsets"])
+    assert offs.shape[0] == 3 and offs[1, 0] > offs[0, 0] + 1.0      # thrust pushes the platform downwind
+    case = dict(zip(d["cases"]["keys"], d["cases"]["data"][-1]))
+    T = oracle_tables_of(f)
+    T["A_BEM"] = np.sum(f.A_aero, axis=3)
+    T["B_BEM"] = np.sum(f.B_aero, axis=3) + np.sum(f.B_gyro, axis=2)[:, :, None]
+    r = O.solve_dynamics(T, dict(case), int(m.nIter), float(m.XiStart))
+    assert f.iterations == r["iters"]
+    assert rel(f.Xi, r["Xi"]) < RTOL, rel(f.Xi, r["Xi"])
