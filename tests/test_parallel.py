@@ -80,6 +80,30 @@ def test_sweep_shard_covers_every_case_and_its_design():
             assert prepared.min() >= 1 and prepared.max() <= 2
 
 
+def test_sharded_sweep_spec_blocks_match_whole_sweep():
+    """bench_c5 under --gpus N: each rank builds its pipeline blocks' spec records from the
+    multipliers of its own design range (specs(a, b) = sweep_specs(base, mult[dlo + a:dlo + b]))
+    over raft/batch.py sweep_cuts; every design a rank solves gets the record the whole sweep
+    gives it."""
+    from raft.batch import sweep_cases, sweep_cuts, sweep_shard
+    from raft.native_prep import sweep_specs
+    from raft.sweep import sea_state_grid, sweep_multipliers
+    from conftest import load_design
+    base = load_design("VolturnUS-S_example")
+    st = {"C_moor": np.diag([7e4, 7e4, 2e4, 1e7, 1e7, 1e8])}
+    nd = 23
+    mult = sweep_multipliers(nd, seed=3)
+    whole = sweep_specs(base, mult, statics=st)
+    idx, _ = sweep_cases(nd, sea_state_grid()[:4])
+    for world in (1, 3, 8):
+        for r in range(world):
+            lo, hi, dlo, dhi = sweep_shard(idx, r, world)
+            cuts = sweep_cuts(dhi - dlo, 5, 0.25, 0.5)
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                for i, s in enumerate(sweep_specs(base, mult[dlo + a:dlo + b], statics=st)):
+                    np.testing.assert_array_equal(s, whole[dlo + a + i])
+
+
 def test_sweep_variant_restates_parametersweep():
     """The five variables land where raft/parametersweep.py:56-88 puts them; multipliers of 1
     leave the design unchanged."""
