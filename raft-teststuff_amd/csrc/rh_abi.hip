@@ -40,6 +40,9 @@ struct rh_ctx {
   bool no_group = false;        // rh_set_solver(ctx, 2): ignore group_start (one case per workgroup)
   int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
   bool qtf_direct = false;      // rh_set_qtf_path(ctx, 1): the per-pair kernel even on a sorted grid
+  // a second stream for k_qtf_kay, which runs beside k_qtf_lcoef + k_qtf_gemm (created on first use)
+  hipStream_t qtf_aux = nullptr;
+  hipEvent_t qtf_tables_done = nullptr, qtf_kay_done = nullptr;
 };
 
 namespace {
@@ -204,6 +207,12 @@ int rh_ctx_destroy(rh_ctx* ctx) {
     if (sl.d) (void)hipFree(sl.d);
     if (sl.h) (void)hipHostFree(sl.h);
   }
+  if (ctx->qtf_aux) {
+    (void)hipStreamSynchronize(ctx->qtf_aux);
+    (void)hipStreamDestroy(ctx->qtf_aux);
+  }
+  if (ctx->qtf_tables_done) (void)hipEventDestroy(ctx->qtf_tables_done);
+  if (ctx->qtf_kay_done) (void)hipEventDestroy(ctx->qtf_kay_done);
   delete ctx;
   return RH_OK;
 }
@@ -525,14 +534,32 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   if (gemm) {
     // w1-side coefficients, then the pair tiles: bilinear + potential GEMMs, then Kim & Yue
     // and the Hermitian fill (rh_qtf_mfma.hip)
-    hipLaunchKernelGGL(rh::k_qtf_lcoef, dim3(nb, 18 + q->nq + q->nmq), dim3(512), 0, s, *q, wk, M66);
-    RH_HIP(hipGetLastError());
     const int nt = n2p / 16, ntile = nt * (nt + 1) / 2;
     const int blocks = (ntile - rank + nrank - 1) / nrank;
     if (blocks > 0) {
+      // k_qtf_kay needs only the tables: it runs on the context's second stream beside
+      // k_qtf_lcoef + k_qtf_gemm (each alone fills ~1.3 waves of workgroups), and k_qtf_kay_sum
+      // joins the two on the caller's stream.  Every later use of the workspace on `s` is
+      // ordered after k_qtf_kay_sum, which waits for k_qtf_kay.
+      if (!ctx->qtf_aux) {
+        RH_HIP(hipStreamCreateWithFlags(&ctx->qtf_aux, hipStreamNonBlocking));
+        RH_HIP(hipEventCreateWithFlags(&ctx->qtf_tables_done, hipEventDisableTiming));
+        RH_HIP(hipEventCreateWithFlags(&ctx->qtf_kay_done, hipEventDisableTiming));
+      }
+      RH_HIP(hipEventRecord(ctx->qtf_tables_done, s));
+      RH_HIP(hipStreamWaitEvent(ctx->qtf_aux, ctx->qtf_tables_done, 0));
+      hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, ctx->qtf_aux, *q, wk, qtf, rank, nrank,
+                         mirror);
+      RH_HIP(hipGetLastError());
+      RH_HIP(hipEventRecord(ctx->qtf_kay_done, ctx->qtf_aux));
+    }
+    hipLaunchKernelGGL(rh::k_qtf_lcoef, dim3(nb, 18 + q->nq + q->nmq), dim3(512), 0, s, *q, wk, M66);
+    RH_HIP(hipGetLastError());
+    if (blocks > 0) {
       hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(2 * blocks), dim3(384), 0, s, *q, wk, qtf, rank, nrank);
       RH_HIP(hipGetLastError());
-      hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, s, *q, wk, qtf, rank, nrank, mirror);
+      RH_HIP(hipStreamWaitEvent(s, ctx->qtf_kay_done, 0));
+      hipLaunchKernelGGL(rh::k_qtf_kay_sum, dim3(blocks), dim3(256), 0, s, *q, wk, qtf, rank, nrank, mirror);
       RH_HIP(hipGetLastError());
     }
     return RH_OK;

@@ -61,13 +61,16 @@ struct QtfWork {
   double* KA;      // [nkr][24][n2p] Kim & Yue: (Re, Im) of the w1-side coefficients of sum omega_n
   double* KB;      // [nkr][24][n2p]                                      ... of sum n (n+1) omega_n
   double* KR;      // [nkr][24][n2p] (Im, Re) of conj(1 / D_n(k2 R))
+  double* KS;      // [ntile][12][256] Kim & Yue sum of each 16 x 16 pair tile (k_qtf_kay ->
+                   //                  k_qtf_kay_sum, so k_qtf_kay can run beside k_qtf_gemm)
 };
 
 __host__ __device__ inline size_t qtf_work_elems(const rh_qtf_design& q) {   // complex elements
   const size_t n2p = (size_t)qtf_n2p(q), kp = (size_t)qtf_kp(q), kq = (size_t)qtf_kq(q);
   return (size_t)q.nq * QT_COUNT * q.n2 + (size_t)q.nmq * WT_COUNT * q.n2 + (size_t)FT_COUNT * q.n2 +
          (size_t)q.nkr * q.n2 * 12 + ((size_t)q.nkr * q.n2 * kKayT + 1) / 2 +
-         7 * kp * n2p + 14 * kq * n2p + ((size_t)3 * q.nkr * kKayK * n2p + 1) / 2;
+         7 * kp * n2p + 14 * kq * n2p + ((size_t)3 * q.nkr * kKayK * n2p + 1) / 2 +
+         (size_t)(n2p / 16) * (n2p / 16 + 1) / 2 * 12 * 256 / 2;
 }
 
 // carve the workspace (same order as qtf_work_elems)
@@ -87,6 +90,7 @@ __host__ inline QtfWork qtf_carve(const rh_qtf_design& q, void* work) {
   wk.KA = reinterpret_cast<double*>(wk.Lp + 12 * kq * n2p);
   wk.KB = wk.KA + (size_t)q.nkr * kKayK * n2p;
   wk.KR = wk.KB + (size_t)q.nkr * kKayK * n2p;
+  wk.KS = wk.KR + (size_t)q.nkr * kKayK * n2p;
   return wk;
 }
 

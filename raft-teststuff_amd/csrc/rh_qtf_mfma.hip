@@ -896,6 +896,9 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
 // keeps per element sum sre and sum sre p over the member's rows, and adds
 // phase x [s0 pf; s x pf] (the rows' translateForce3to6DOF) to the tile's LDS sum in member
 // order.  The next row's operands are loaded while the current row is reduced.
+// row-major index of upper-triangle tile (T1, T2), T2 >= T1, of an nt x nt tile grid
+__device__ __forceinline__ int qtf_tile_id(int T1, int T2, int nt) { return T1 * nt - T1 * (T1 - 1) / 2 + (T2 - T1); }
+
 constexpr int kKayW = 4;
 constexpr int kKayThreads = 64 * kKayW;
 __global__ __launch_bounds__(kKayThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_qtf_kay(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf,
@@ -1038,6 +1041,26 @@ __global__ __launch_bounds__(kKayThreads) __attribute__((amdgpu_waves_per_eu(2))
       __syncthreads();
     }
   }
+  // the tile's Kim & Yue sums to the workspace; k_qtf_kay_sum adds them to the GEMM part
+  double* ks = wk.KS + (size_t)qtf_tile_id(T1, T2, nt) * 12 * 256;
+  for (int e = tid; e < 12 * 256; e += kKayThreads) ks[e] = (&acc[0][0])[e];
+}
+
+// The final sum of a QTF pair tile: the GEMM part k_qtf_gemm wrote plus the Kim & Yue part
+// k_qtf_kay left in the workspace (the same addition, in the same order, as when k_qtf_kay
+// finished the tile itself), then the Hermitian fill (raft/raft_fowt.py:1639-1640).
+__global__ __launch_bounds__(256) void k_qtf_kay_sum(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf,
+                                                     int rank, int nrank, int mirror) {
+  const int tid = (int)threadIdx.x;
+  const int n2 = q.n2, n2p = qtf_n2p(q), nt = n2p / 16;
+  int T1 = 0, t = rank + nrank * xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  while (t >= nt - T1) {   // block-uniform
+    t -= nt - T1;
+    ++T1;
+  }
+  const int T2 = T1 + t;
+  const int i1b = 16 * T1, i2b = 16 * T2;
+  const double* ks = wk.KS + (size_t)qtf_tile_id(T1, T2, nt) * 12 * 256;
   // one pair per thread
   const int a1 = i1b + (tid >> 4), a2 = i2b + (tid & 15);
   if (a1 >= n2 || a2 >= n2 || a2 < a1) return;
@@ -1046,7 +1069,7 @@ __global__ __launch_bounds__(kKayThreads) __attribute__((amdgpu_waves_per_eu(2))
   rh_c128* lo = qtf + ((size_t)a2 * n2 + a1) * 6;
 #pragma unroll
   for (int d = 0; d < 6; ++d) {
-    const cd Qd = add(ld(up + d), mk(acc[2 * d][e], acc[2 * d + 1][e]));
+    const cd Qd = add(ld(up + d), mk(ks[(2 * d) * 256 + e], ks[(2 * d + 1) * 256 + e]));
     if (!mirror) {
       st(up + d, Qd);
     } else if (a1 == a2) {   // qtf + conj(qtf).T - diag(conj(diag(qtf))) (:1639-1640)
