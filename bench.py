@@ -287,8 +287,8 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
            "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                         "frac": achieved / PEAK_FP64,
                         "traffic": pmc_traffic("k_qtf_freq", "k_qtf_tables", "k_qtf_lcoef", "k_qtf_gemm", "k_qtf_kay"),
-                        "kernel": "rh_qtf_slender%s: k_qtf_freq, k_qtf_tables, k_qtf_lcoef, k_qtf_gemm, k_qtf_kay "
-                                  "(every launch of a QTF on this rank)" % ("_rows" if world > 1 else ""),
+                        "kernel": "rh_qtf_slender%s: k_qtf_freq, k_qtf_tables, k_qtf_lcoef, k_qtf_gemm, k_qtf_kay (second "
+                                  "stream), k_qtf_kay_sum (every launch of a QTF on this rank)" % ("_rows" if world > 1 else ""),
                         "kernel_ms": ms, "flops_per_pair": fpp, "pairs_this_rank": mine,
                         "note": "FP64: the pair sum as MFMA GEMMs (k_qtf_gemm) + VALU Kim & Yue epilogue (DESIGN.md "
                                 "§4); peak = MI355X FP64 dense (matrix = vector rate); algorithmic FLOPs from SURVEY.md "

@@ -40,7 +40,7 @@ struct rh_ctx {
   bool no_group = false;        // rh_set_solver(ctx, 2): ignore group_start (one case per workgroup)
   int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
   bool qtf_direct = false;      // rh_set_qtf_path(ctx, 1): the per-pair kernel even on a sorted grid
-  // a second stream for k_qtf_kay, which runs beside k_qtf_lcoef + k_qtf_gemm (created on first use)
+  // a second stream for k_qtf_kay, which runs beside k_qtf_lcoef + k_qtf_gemm (rh_ctx_create)
   hipStream_t qtf_aux = nullptr;
   hipEvent_t qtf_tables_done = nullptr, qtf_kay_done = nullptr;
 };
@@ -181,7 +181,14 @@ int rh_ctx_create(int device, rh_ctx** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.staged, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.used, hipEventDisableTiming);
   }
+  // the QTF's second stream, made here so that a first QTF does not pay for it
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->qtf_aux, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->qtf_tables_done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->qtf_kay_done, hipEventDisableTiming);
   if (e != hipSuccess) {
+    if (c->qtf_aux) (void)hipStreamDestroy(c->qtf_aux);
+    if (c->qtf_tables_done) (void)hipEventDestroy(c->qtf_tables_done);
+    if (c->qtf_kay_done) (void)hipEventDestroy(c->qtf_kay_done);
     for (auto& sl : c->slot) {
       if (sl.staged) (void)hipEventDestroy(sl.staged);
       if (sl.used) (void)hipEventDestroy(sl.used);
@@ -541,11 +548,6 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
       // k_qtf_lcoef + k_qtf_gemm (each alone fills ~1.3 waves of workgroups), and k_qtf_kay_sum
       // joins the two on the caller's stream.  Every later use of the workspace on `s` is
       // ordered after k_qtf_kay_sum, which waits for k_qtf_kay.
-      if (!ctx->qtf_aux) {
-        RH_HIP(hipStreamCreateWithFlags(&ctx->qtf_aux, hipStreamNonBlocking));
-        RH_HIP(hipEventCreateWithFlags(&ctx->qtf_tables_done, hipEventDisableTiming));
-        RH_HIP(hipEventCreateWithFlags(&ctx->qtf_kay_done, hipEventDisableTiming));
-      }
       RH_HIP(hipEventRecord(ctx->qtf_tables_done, s));
       RH_HIP(hipStreamWaitEvent(ctx->qtf_aux, ctx->qtf_tables_done, 0));
       hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, ctx->qtf_aux, *q, wk, qtf, rank, nrank,
