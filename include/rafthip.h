@@ -346,7 +346,10 @@ long long rh_qtf_workspace_bytes(const rh_qtf_design* q);
 
 /* Slender-body QTF for one heading: Xi0 [6][nw] motion RAO on the first-order grid w [nw];
  * M66 [36] structural mass matrix (F1st, :1437-1439); qtf out [n2][n2][6] (full Hermitian
- * matrix, upper triangle computed, lower filled as :1639-1640).  work: device workspace. */
+ * matrix, upper triangle computed, lower filled as :1639-1640).  work: device workspace.
+ * On the MFMA path the Kim & Yue kernel runs on a second stream owned by ctx, joined back to
+ * `stream` by an event before the final kernel: the outputs are stream-ordered on `stream`, and
+ * a ctx must not run two QTFs at once on different streams. */
 int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
                    const double* M66, rh_c128* qtf, void* work, long long work_bytes, rh_stream stream);
 
