@@ -6,8 +6,10 @@ at min_freq 0.0002 Hz -> nw = 1000 bins, 53 submerged strip nodes (20 circular +
 (Hs~U(1,10) m, Tp~U(6,18) s, gamma 0 = IEC auto, heading in {0,30,60,90} deg), solved to
 converged RAO + motion PSD in one device call.  Inputs (design tables, case parameters)
 are resident in HBM before the timed region.  Multi-GPU: one process per GPU, every rank
-solves its own 512-case shard (weak scaling, no data-path collective); the only
-collective is the barrier/max-time reduction of the harness.
+solves its own 512-case shard (weak scaling, no collective inside the drag loop); each
+step's per-case outputs (std, PSD, iteration counts) are all-gathered over RCCL on a second
+stream while the next step solves (the final response-spectrum gather of north_star), and
+the line also reports the same steps without the gather.
 
 Prints ONE JSON line (rank 0).
 """
@@ -185,6 +187,44 @@ def cpu_baselines(qtf_seconds=10.0):
                      f"(vectorised over pairs, faster per pair than the reference's 19-23 ms) on {P} cores, "
                      f"{dq:.1f} s wall ({cores_note}); CPU {model}"}
     return case, qtf
+
+
+CPU_BASELINE_CACHE = os.path.join("/tmp", "raft_bench_cpu_baseline.json")
+
+
+def cpu_baselines_cached(harness=False):
+    """The CPU baseline legs for this run, measured before the process touches the GPU.
+    A `--gpus N` run started as one process measures them in the relaunch() parent (which never
+    touches the GPU) and hands them to rank 0 through CPU_BASELINE_CACHE; a torchrun-launched
+    N > 1 series (N = 1, 2, 4, 8 back to back on one node) reuses the measurement of an earlier
+    run on the same host from the last 24 h, and rank 0 measures it itself when there is none.
+    harness=True (--harness-check) writes a stub instead of timing the oracle."""
+    import socket
+    host = socket.gethostname()
+    try:
+        with open(CPU_BASELINE_CACHE) as fh:
+            d = json.load(fh)
+        if d.get("host") == host and time.time() - d.get("time", 0) < 86400 and d.get("stub", False) == harness:
+            return d["case"], d["qtf"]
+    except (OSError, ValueError, KeyError):
+        pass
+    if harness:
+        case = {"value": 0.0, "unit": "cases/s", "cores": 0, "kind": "stub", "sample": "harness check: no timing"}
+        qtf = dict(case, unit="pairs/s")
+    else:
+        case, qtf = cpu_baselines()
+    with open(CPU_BASELINE_CACHE, "w") as fh:
+        json.dump({"host": host, "time": time.time(), "stub": harness, "case": case, "qtf": qtf}, fh)
+    return case, qtf
+
+
+def pack_outputs(res):
+    """One contiguous f64 block [n, 6 + 6 nw + 1] of a batch's per-case outputs: std, PSD and
+    the iteration count (exact in f64): what the response-spectrum gather moves."""
+    import torch
+    n = res["std"].shape[0]
+    return torch.cat([res["std"].reshape(n, -1), res["psd"].reshape(n, -1),
+                      res["iters"].to(torch.float64).reshape(n, 1)], 1)
 
 
 def qtf_flops_per_pair(nsub, nkay, nwl):
@@ -480,6 +520,8 @@ def relaunch(nproc, argv):
     before this process touches the GPU, and return its exit code."""
     import socket
     import subprocess
+    if "--no-cpu-baseline" not in argv:
+        cpu_baselines_cached(harness="--harness-check" in argv)   # this process never touches the GPU
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
@@ -494,6 +536,9 @@ def harness_check(args, world, rank):
     stub steps, max-over-ranks time, one JSON line from rank 0.  tests/test_bench.py runs it."""
     import torch
     import torch.distributed as dist
+    base = None
+    if rank == 0 and not args.no_cpu_baseline:
+        base = cpu_baselines_cached(harness=True)
     if world > 1:
         dist.init_process_group("gloo")
     for _ in range(args.warmup):
@@ -501,17 +546,30 @@ def harness_check(args, world, rank):
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
+    gathered = 0
     for _ in range(args.steps):
         time.sleep(0.001 * (1 + rank))
+        if world > 1:   # the per-step output gather (a stub block of the real one's layout)
+            res = {"std": torch.zeros(4, 6, dtype=torch.float64), "psd": torch.zeros(4, 6, 8, dtype=torch.float64),
+                   "iters": torch.full((4,), 4 + rank, dtype=torch.int32)}
+            blk = pack_outputs(res)
+            out = torch.empty((world * blk.shape[0], blk.shape[1]), dtype=blk.dtype)
+            dist.all_gather_into_tensor(out, blk)
+            gathered += int((out[:, -1] >= 4).sum())
     if world > 1:
         dist.barrier()
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if rank == 0:
-        print(json.dumps({"metric": "harness check", "value": args.ncase * world * args.steps / float(t.item()),
-                          "unit": "cases/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": float(t.item()) / args.steps * 1e3, "ranks_seen": world}))
+        line = {"metric": "harness check", "value": args.ncase * world * args.steps / float(t.item()),
+                "unit": "cases/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": float(t.item()) / args.steps * 1e3, "ranks_seen": world}
+        if world > 1:
+            line["gather"] = {"cases_gathered_per_step": gathered // max(1, args.steps)}
+        if base is not None:
+            line["cpu_baseline"] = base[0]
+        print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
 
@@ -539,8 +597,8 @@ def main():
     if args.harness_check:
         return harness_check(args, world, rank)
     baselines = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        baselines = cpu_baselines()          # before this process initialises the GPU
+    if rank == 0 and not args.no_cpu_baseline:
+        baselines = cpu_baselines_cached()   # before this process initialises the GPU
     pool, nproc = None, 1     # C5 prepares designs on native host threads (no worker pool)
     import torch
     import torch.distributed as dist
@@ -570,26 +628,67 @@ def main():
             e.record(stream)
         return solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=want, prepared=prep)
 
+    comm = torch.cuda.Stream(device) if world > 1 else None
+
+    def gather_async(res, e_done):
+        """All-gather of this step's packed outputs on the comm stream, after the solve
+        (event e_done), overlapping the next step's solve on the compute stream."""
+        with torch.cuda.stream(comm):
+            comm.wait_event(e_done)
+            blk = pack_outputs(res)
+            out = torch.empty((world * blk.shape[0], blk.shape[1]), dtype=blk.dtype, device=blk.device)
+            g0 = torch.cuda.Event(enable_timing=True)
+            g0.record(comm)
+            work = dist.all_gather_into_tensor(out, blk, async_op=True)
+        for v in res.values():
+            v.record_stream(comm)
+        return work, out, g0
+
     for _ in range(args.warmup):
         res = step()
+        if world > 1:
+            e = torch.cuda.Event()
+            e.record(stream)
+            w, _, _ = gather_async(res, e)
+            w.wait()
     torch.cuda.synchronize()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def timed(gather):
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        pend = []
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            ev[i][0].record(stream)
+            r = step(ev[i][1])
+            ev[i][2].record(stream)
+            if gather:
+                pend.append(gather_async(r, ev[i][2]))
+        for work, _, _ in pend:
+            work.wait()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=f"cuda:{device}")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gms = None
+        if pend:
+            g1 = torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(comm):
+                g1.record(comm)
+            torch.cuda.synchronize()
+            gms = pend[-1][2].elapsed_time(g1)   # the last step's gather (nothing overlaps it)
+            out = pend[-1][1]
+            assert out.shape[0] == world * args.ncase and torch.all(out[:, -1] >= 1)
+        return float(t.item()), ev, r, gms
+
+    dt_ng, ev, res, _ = timed(False)
+    dt_max, gather_ms = dt_ng, None
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        res = step(ev[i][1])
-        ev[i][2].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{device}")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt_max = float(t.item())
+        dt_max, _, _, gather_ms = timed(True)
     tab_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     kern_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
 
@@ -631,6 +730,13 @@ def main():
         "iterations_mean": float(iters.mean()),
         "converged_frac": float((status == 1).mean()),
     }
+    if world > 1:
+        n_out = args.ncase * (6 + 6 * dd.nw + 1) * 8
+        line["gather"] = {"included_in_value": True, "value_without_gather": total_cases / dt_ng,
+                          "ms_per_step_without_gather": dt_ng / args.steps * 1e3,
+                          "last_gather_ms": gather_ms, "bytes_per_rank_per_step": n_out,
+                          "note": "per step: all_gather_into_tensor (RCCL) of every rank's std, PSD and iteration "
+                                  "counts on a second stream, overlapping the next step's solve"}
     if not args.no_qtf:
         line["qtf"] = bench_qtf(device, max(3, args.steps // 4), 1, world, rank, dist)
     if not args.no_c4:
@@ -641,7 +747,10 @@ def main():
         pool.close()
         pool.join()
     if baselines is not None:
-        line["cpu_baseline"] = baselines[0]
+        line["cpu_baseline"] = dict(baselines[0])
+        if world > 1:
+            line["cpu_baseline"]["note"] = ("measured on this host before the GPU work (relaunch() parent, or an "
+                                            "earlier run of this series within 24 h: " + CPU_BASELINE_CACHE + ")")
         if "qtf" in line:
             line["qtf"]["cpu_baseline"] = baselines[1]
     if rank == 0:

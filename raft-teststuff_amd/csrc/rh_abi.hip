@@ -15,6 +15,7 @@
 #include "rh_qtf_mfma.hip"
 #include "rh_solve.hip"
 #include "rh_solve_grp.hip"
+#include "rh_solve_pair.hip"
 #include "rh_prep.h"       // host-only: native per-design preparation (rh_prep_designs)
 
 // One staging slot of the design descriptor array.  A context cycles through kDescSlots of
@@ -38,6 +39,10 @@ struct rh_ctx {
   // tuning / cross-check knobs (per context: the ABI has no mutable process globals)
   bool force_general = false;   // rh_set_solver(ctx, 1): always use k_solve_cases (parity cross-checks)
   bool no_group = false;        // rh_set_solver(ctx, 2): ignore group_start (one case per workgroup)
+#ifndef RH_PAIR_OFF
+#define RH_PAIR_OFF 0
+#endif
+  bool no_pair = RH_PAIR_OFF;   // rh_set_solver(ctx, 3): k_solve_lds instead of k_solve_pair (cross-checks)
   int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
   bool qtf_direct = false;      // rh_set_qtf_path(ctx, 1): the per-pair kernel even on a sorted grid
   // a second stream for k_qtf_kay, which runs beside k_qtf_lcoef + k_qtf_gemm (rh_ctx_create)
@@ -48,6 +53,22 @@ struct rh_ctx {
 namespace {
 thread_local std::string g_err;
 constexpr int kGroupCases = 2;   // lock-step width of k_solve_grp
+#ifndef RH_PAIR_RA
+#define RH_PAIR_RA 2
+#endif
+#ifndef RH_PAIR_RC
+#define RH_PAIR_RC 4
+#endif
+constexpr int kPairRA = RH_PAIR_RA;   // k_solve_pair wave-table prefetch depth, phase A (nodes)
+constexpr int kPairRC = RH_PAIR_RC;   // ... phase C
+#ifndef RH_PAIR_HOLD
+#define RH_PAIR_HOLD 0
+#endif
+constexpr bool kPairHold = RH_PAIR_HOLD;   // k_solve_pair keeps the unrelaxed iterate in VGPRs
+#ifndef RH_PAIR_PB
+#define RH_PAIR_PB 2
+#endif
+constexpr int kPairPB = RH_PAIR_PB;   // bins per lane in phase A at 1024 threads
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -144,10 +165,12 @@ extern "C" int rh_prof_read(unsigned long long* out, int reset) {
 
 int rh_set_solver(rh_ctx* ctx, int which) {
   if (!ctx) return fail(RH_EINVAL, "rh_set_solver: null context");
-  if (which < 0 || which > 2)
-    return fail(RH_EINVAL, "rh_set_solver: which=%d (0 = auto, 1 = general kernel, 2 = ungrouped)", which);
+  if (which < 0 || which > 3)
+    return fail(RH_EINVAL, "rh_set_solver: which=%d (0 = auto, 1 = general kernel, 2 = ungrouped, 3 = k_solve_lds)",
+                which);
   ctx->force_general = which == 1;
-  ctx->no_group = which == 2;
+  ctx->no_group = which == 2 || which == 3;
+  ctx->no_pair = which == 3 || (which == 0 && RH_PAIR_OFF);
   return RH_OK;
 }
 
@@ -303,11 +326,25 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
       return designs_used(ctx, s);
     }
   }
-  // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case (256 for nw <= 256), nw <= 1024.
+  int nmmax = 0;
+  for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
+  // Default path (rh_solve_pair.hip): one bin per lane, pair-split LU, 4 waves per SIMD.
+  if (nw <= 1024 && !ctx->force_general && !ctx->no_pair) {
+    const int lt = nw <= 256 ? 256 : nw <= 512 ? 512 : 1024;
+    const int pb = lt == 1024 ? kPairPB : 1;
+    const size_t lsm = rh::solve_pair_smem(nnmax, nmmax, lt, pb);
+    if (lsm <= kMaxLds) {
+      dim3 grid(cases->ncase), block(lt);
+      if (lt == 256) hipLaunchKernelGGL((rh::k_solve_pair<256, 1, kPairRA, kPairRC, kPairHold>), grid, block, lsm, s, a);
+      else if (lt == 512) hipLaunchKernelGGL((rh::k_solve_pair<512, 1, kPairRA, kPairRC, kPairHold>), grid, block, lsm, s, a);
+      else hipLaunchKernelGGL((rh::k_solve_pair<1024, kPairPB, kPairRA, kPairRC, kPairHold>), grid, block, lsm, s, a);
+      return designs_used(ctx, s);
+    }
+  }
+  // Previous fast path (rh_solve.hip): XiLast in LDS, 512 threads per case (256 for nw <= 256),
+  // nw <= 1024; rh_set_solver(ctx, 3) selects it for cross-checks.
   if (nw <= 2 * rh::kLT && !ctx->force_general) {
     const int nb = nw <= rh::kLT ? 1 : 2;
-    int nmmax = 0;
-    for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
     const int lt = nw <= rh::kLT / 2 ? rh::kLT / 2 : rh::kLT;   // nw <= 256: 256 threads, two cases per CU
     const size_t lsm = rh::solve_lds_smem(nnmax, nmmax, nb, lt);
     if (lsm <= 160 * 1024) {

@@ -517,11 +517,16 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
       const bool okb = b0 < nw;
       const int b = okb ? b0 : nw - 1;
       const double w = d.w[b];
+      // zeta of bin j by a select chain: zt[j] with the loop index j would be a dynamic index
+      // into a register array (s_set_gpr_idx), which tools/isa_check.py refuses
+      double zj = zt[0];
+#pragma unroll
+      for (int jj = 1; jj < NB; ++jj) zj = j == jj ? zt[jj] : zj;
       cd F[6];
       drag_exc_members(d, al, Kp, nw, b, F);
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
-        cd f = add(scl(ld(Fe + c * nw + b), zt[j]), scl(F[c], zt[j]));   // F_lin + F_drag
+        cd f = add(scl(ld(Fe + c * nw + b), zj), scl(F[c], zj));   // F_lin + F_drag
         if (a.c.fext) f = add(f, ld(a.c.fext + ((size_t)ic * 6 + c) * nw + b));
         F[c] = f;
       }

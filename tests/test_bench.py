@@ -25,6 +25,10 @@ def test_gpus2_launches_two_ranks_one_line():
     assert len(lines) == 1, lines
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["steps"] == 3
+    # the per-step output gather and the CPU baseline (measured by the relaunch() parent before
+    # any rank starts; a stub in harness mode) both reach rank 0's line
+    assert d["gather"]["cases_gathered_per_step"] == 8
+    assert d["cpu_baseline"]["kind"] == "stub"
     # rank 1 sleeps twice as long per step: the reported time is the max over ranks
     assert d["ms_per_step"] >= 2.0
 

@@ -1,0 +1,116 @@
+"""ISA gate for librafthip's hot kernels (gfx950).
+
+Compiles raft-teststuff_amd/csrc/rh_abi.hip to device assembly and checks every kernel:
+  * no dynamic register indexing: `s_set_gpr_idx_*` or `v_movrel*` (a lane-dependent index into
+    a register array, lowered with a scalar index, faulted k_qtf_hankel on the box in round 2;
+    DESIGN.md §4) -> FAIL in any kernel;
+  * no scratch traffic inside an innermost loop of a hot kernel (the node loops of the solve
+    kernels, the pair loops of the QTF kernels): a spill reload there shares `vmcnt` with the
+    wave-table prefetch ring and drains it every node -> FAIL;
+  * scratch instructions elsewhere (prologue, solve, member boundaries) are counted and reported.
+Loops are found from the branch structure: a branch to a label that precedes it closes a loop
+[label, branch]; a loop that contains no other loop is innermost.
+
+Usage: python tools/isa_check.py [--asm file.s] [--out report.txt]   (exit status 1 on FAIL)
+"""
+import argparse
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "raft-teststuff_amd", "csrc", "rh_abi.hip")
+HOT = ("k_solve_pair", "k_solve_lds", "k_solve_cases", "k_solve_grp", "k_qtf_gemm", "k_qtf_kay", "k_qtf_pairs",
+       "k_qtf_lcoef", "k_qtf_tables")
+DYN_INDEX = re.compile(r"^\s*(s_set_gpr_idx\w*|v_movrel\w*)")
+SCRATCH = re.compile(r"^\s*(scratch_|buffer_\w+.*\boff(en)?\b.*s\[0:3\])")
+LABEL = re.compile(r"^(\.LBB\w+|\w+):")
+BRANCH = re.compile(r"^\s*s_(cbranch_\w+|branch)\s+(\.LBB\w+)")
+
+
+def compile_asm():
+    fd, path = tempfile.mkstemp(suffix=".s")
+    os.close(fd)
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--offload-device-only", "-S",
+                    "-o", path, SRC], check=True, capture_output=True)
+    return path
+
+
+def kernels(lines):
+    """{mangled name: [instruction lines]} for every kernel body (up to its s_endpgm)."""
+    out, name, body = {}, None, []
+    for ln in lines:
+        m = re.match(r"^(_Z\w+):", ln)
+        if m and name is None:
+            name, body = m.group(1), []
+            continue
+        if name is not None:
+            body.append(ln)
+            if re.match(r"^\s*s_endpgm", ln):
+                out[name] = body
+                name = None
+    return out
+
+
+def analyse(body):
+    labels = {}
+    for i, ln in enumerate(body):
+        m = LABEL.match(ln)
+        if m:
+            labels[m.group(1)] = i
+    loops = []
+    for i, ln in enumerate(body):
+        m = BRANCH.match(ln)
+        if m and m.group(2) in labels and labels[m.group(2)] <= i:
+            loops.append((labels[m.group(2)], i))
+    inner = [l for l in loops if not any(o != l and l[0] <= o[0] and o[1] <= l[1] for o in loops)]
+    dyn = [ln.strip() for ln in body if DYN_INDEX.match(ln)]
+    scr = [i for i, ln in enumerate(body) if SCRATCH.match(ln)]
+    scr_inner = [i for i in scr if any(a <= i <= b for a, b in inner)]
+    return {"dyn": dyn, "scratch": len(scr), "scratch_inner": len(scr_inner), "loops": len(loops), "inner": len(inner)}
+
+
+def demangle(n):
+    try:
+        return subprocess.run(["c++filt", n], capture_output=True, text=True).stdout.strip()
+    except OSError:
+        return n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--asm")
+    ap.add_argument("--out")
+    args = ap.parse_args()
+    path = args.asm or compile_asm()
+    with open(path) as fh:
+        ks = kernels(fh.read().split("\n"))
+    rows, fails = [], []
+    for name, body in sorted(ks.items()):
+        r = analyse(body)
+        dn = demangle(name)
+        hot = any(h in dn for h in HOT)
+        verdict = "ok"
+        if r["dyn"]:
+            verdict = "FAIL dynamic register indexing: " + "; ".join(sorted(set(r["dyn"])))
+        elif hot and r["scratch_inner"]:
+            verdict = f"FAIL {r['scratch_inner']} scratch instructions inside innermost loops"
+        if verdict != "ok":
+            fails.append(dn)
+        rows.append(f"{dn:70s} hot={int(hot)} loops={r['loops']:3d} inner={r['inner']:3d} "
+                    f"scratch={r['scratch']:4d} scratch_in_inner={r['scratch_inner']:3d}  {verdict}")
+    text = "# tools/isa_check.py: gfx950 device assembly of rh_abi.hip\n" + "\n".join(rows) + "\n"
+    text += f"# {len(ks)} kernels, {len(fails)} failing\n"
+    print(text)
+    if args.out:
+        with open(args.out, "w") as fh:
+            fh.write(text)
+    if not args.asm:
+        os.unlink(path)
+    return 1 if fails else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
