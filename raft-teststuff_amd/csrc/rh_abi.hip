@@ -39,10 +39,10 @@ struct rh_ctx {
   // tuning / cross-check knobs (per context: the ABI has no mutable process globals)
   bool force_general = false;   // rh_set_solver(ctx, 1): always use k_solve_cases (parity cross-checks)
   bool no_group = false;        // rh_set_solver(ctx, 2): ignore group_start (one case per workgroup)
-#ifndef RH_PAIR_OFF
-#define RH_PAIR_OFF 0
+#ifndef RH_PAIR_ON
+#define RH_PAIR_ON 0
 #endif
-  bool no_pair = RH_PAIR_OFF;   // rh_set_solver(ctx, 3): k_solve_lds instead of k_solve_pair (cross-checks)
+  bool use_pair = RH_PAIR_ON;   // rh_set_solver(ctx, 3): k_solve_pair instead of k_solve_lds (cross-checks)
   int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
   bool qtf_direct = false;      // rh_set_qtf_path(ctx, 1): the per-pair kernel even on a sorted grid
   // a second stream for k_qtf_kay, which runs beside k_qtf_lcoef + k_qtf_gemm (rh_ctx_create)
@@ -166,11 +166,11 @@ extern "C" int rh_prof_read(unsigned long long* out, int reset) {
 int rh_set_solver(rh_ctx* ctx, int which) {
   if (!ctx) return fail(RH_EINVAL, "rh_set_solver: null context");
   if (which < 0 || which > 3)
-    return fail(RH_EINVAL, "rh_set_solver: which=%d (0 = auto, 1 = general kernel, 2 = ungrouped, 3 = k_solve_lds)",
+    return fail(RH_EINVAL, "rh_set_solver: which=%d (0 = auto, 1 = general kernel, 2 = ungrouped, 3 = k_solve_pair)",
                 which);
   ctx->force_general = which == 1;
   ctx->no_group = which == 2 || which == 3;
-  ctx->no_pair = which == 3 || (which == 0 && RH_PAIR_OFF);
+  ctx->use_pair = which == 3 || (which == 0 && RH_PAIR_ON);
   return RH_OK;
 }
 
@@ -328,8 +328,9 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   }
   int nmmax = 0;
   for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
-  // Default path (rh_solve_pair.hip): one bin per lane, pair-split LU, 4 waves per SIMD.
-  if (nw <= 1024 && !ctx->force_general && !ctx->no_pair) {
+  // Opt-in path (rh_solve_pair.hip, rh_set_solver(ctx, 3)): one bin per lane, lane-pair LU,
+  // 4 waves per SIMD.  Parity-green but slower than k_solve_lds on C2.
+  if (nw <= 1024 && !ctx->force_general && ctx->use_pair) {
     const int lt = nw <= 256 ? 256 : nw <= 512 ? 512 : 1024;
     const int pb = lt == 1024 ? kPairPB : 1;
     const size_t lsm = rh::solve_pair_smem(nnmax, nmmax, lt, pb);
@@ -341,8 +342,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
       return designs_used(ctx, s);
     }
   }
-  // Previous fast path (rh_solve.hip): XiLast in LDS, 512 threads per case (256 for nw <= 256),
-  // nw <= 1024; rh_set_solver(ctx, 3) selects it for cross-checks.
+  // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case (256 for nw <= 256), nw <= 1024.
   if (nw <= 2 * rh::kLT && !ctx->force_general) {
     const int nb = nw <= rh::kLT ? 1 : 2;
     const int lt = nw <= rh::kLT / 2 ? rh::kLT / 2 : rh::kLT;   // nw <= 256: 256 threads, two cases per CU

@@ -31,6 +31,9 @@ constexpr int kLT = 512;          // threads per case workgroup
 constexpr int kLW = kLT / 64;     // waves per case workgroup
 constexpr int kRingA = 3;         // wave-table prefetch depth (nodes) of phase A
 constexpr int kRingC = 6;         // ... of phase C (one bin per pass: less work per node)
+#ifndef RH_LDS_LANE_BRANCH
+#define RH_LDS_LANE_BRANCH 0          // 1: the round-2 per-lane `continue` before the solve (A/B only)
+#endif
 
 // A scalar zero the compiler cannot fold (see its use in phase C).
 __device__ __forceinline__ int opaque_zero() {
@@ -459,7 +462,15 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
 #ifdef RH_PROF
       tc_exc += tc1 - tc0;
 #endif
+#if RH_LDS_LANE_BRANCH
       if (!okj) continue;
+#else
+      // No lane branch around the solve (a per-lane `continue` here let the compiler's spills
+      // run under a partial EXEC mask in the general kernel): only a wave whose
+      // every lane is past the grid skips it (uniform); pad lanes of the last wave solve the
+      // clamped last bin with a zero right-hand side (zeta = 0, x = 0 exactly) and store nothing.
+      if (!__builtin_amdgcn_ballot_w64(okj)) continue;
+#endif
       const int b = tid + LT * j;
       const unsigned v = vj;
       const double w = lw[b], z = lz[b];
@@ -470,7 +481,7 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
 #pragma unroll
         for (int c = 0; c < 6; ++c) fx[c] = bld(bFx, v, c * nw16);
 #pragma unroll
-        for (int c = 0; c < 6; ++c) F[c] = add(F[c], fx[c]);
+        for (int c = 0; c < 6; ++c) F[c] = add(F[c], mk(okj ? fx[c].r : 0.0, okj ? fx[c].i : 0.0));
       }
       cd Z[6][6];
       {
@@ -482,8 +493,9 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
         const double* zs = bsum + zo;
         const double w2 = -(w * w);
         if (d.mb_per_bin) {
-          const double* M = d.M + (size_t)b * 36;
-          const double* B = d.B + (size_t)b * 36;
+          const int bc = okj ? b : nw - 1;
+          const double* M = d.M + (size_t)bc * 36;
+          const double* B = d.B + (size_t)bc * 36;
 #pragma unroll
           for (int r = 0; r < 6; ++r) {
 #pragma unroll
@@ -500,20 +512,23 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
           }
         }
       }
-      my_sing |= !lu_solve<6>(Z, F);
+      const bool ok_lu = lu_solve<6>(Z, F);
+      my_sing |= okj && !ok_lu;
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
         const cd x = F[c];
         const cd xlast = xl[c * NWP + b];
-        my_nan |= (x.r != x.r) || (x.i != x.i);
+        my_nan |= okj && ((x.r != x.r) || (x.i != x.i));
         // tolCheck = |Xi - XiLast| / (|Xi| + tol) < tol  (raft/raft_model.py:961-962)
         // (magnitudes as sqrt(re^2 + im^2): within an ulp of np.abs's hypot, far cheaper)
         const double tt = sqrt(abs2(sub(x, xlast))) / (sqrt(abs2(x)) + tol);
-        my_ok = my_ok && (tt < tol);
-        my_tmax = fmax(my_tmax, tt);
-        st_nt(Xo + c * nw + b, x);   // streamed: only the last iteration's value is kept
-        if (XP) st(XP + c * nw + b, xlast);
-        // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged
+        my_ok = my_ok && (!okj || tt < tol);
+        my_tmax = okj ? fmax(my_tmax, tt) : my_tmax;
+        if (okj) {   // stores only
+          st_nt(Xo + c * nw + b, x);   // streamed: only the last iteration's value is kept
+          if (XP) st(XP + c * nw + b, xlast);
+        }
+        // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged (pads: 0)
         xl[c * NWP + b] = add(scl(xlast, 0.2), scl(x, 0.8));
       }
 #ifdef RH_PROF

@@ -180,7 +180,7 @@ __host__ __device__ inline size_t solve_pair_smem(int nn, int nm, int LT, int PB
                            + (size_t)nm * 18        // member cq, c1, c2
                            + (size_t)2 * LT         // w and zeta per (padded) bin
                            + 36 + 108 + LW * 6 + 36  // B_drag, M|B|C image, std partials, B_lin+B_drag
-                           + LW)                    // convergence-margin partials
+                           + LW + 1)                // convergence-margin partials, closest call
          + sizeof(int) * ((size_t)nm + 2);
 }
 
@@ -193,8 +193,15 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
   constexpr int TB = LT / PB;       // lanes per phase-A group (bins per pass)
   constexpr int LWA = TB / 64;      // waves per phase-A group
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int par = tid & 1;
+  const int tid = threadIdx.x;
+  // The wave index lives in an SGPR; every lane-dependent index below is recomputed from it
+  // and the lane id where it is used (tnow(): v_mbcnt behind asm volatile, so it is neither
+  // hoisted nor kept): a value kept live across the phases would be spilled around the
+  // register-heavy pair solves, and its reload inside a node loop would drain the wave-table
+  // prefetch ring (scratch loads share vmcnt with the buffer loads).
+  const int wv_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+  auto tnow = [&]() { return wv_s * 64 + lane_here(); };
+  PROF_T(tp0);
   const int slot = xcd_remap(blockIdx.x, a.c.ncase);
   const int ic = a.c.order ? a.c.order[slot] : slot;
   const rh_design& d = a.designs[a.c.design[ic]].d;
@@ -221,18 +228,17 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
   double* mbf = nt + nn;                           // [18][nm]
   double* lw = mbf + 18 * nm;                      // [LT] w per bin (pad bins: w[nw-1])
   double* lz = lw + LT;                            // [LT] zeta per bin (pad bins: 0)
-  double* mred = lz + LT;                          // [LW] per-wave max of tolCheck
-  int* mstart = reinterpret_cast<int*>(mred + LW);  // [nm+1]
+  double* mred = lz + LT;                          // [LW] per-wave max of tolCheck, [LW] closest call
+  int* mstart = reinterpret_cast<int*>(mred + LW + 1);  // [nm+1]
   load_mbc(d, mbc, tid);
   for (int n = tid; n < nn; n += LT) nt[n] = node[RH_NF_T * nn + n];
   for (int e = tid; e < 18 * nm; e += LT) mbf[e] = d.memb[e];
   for (int e = tid; e <= nm; e += LT) mstart[e] = d.mstart[e];
 
   auto voff = [&](int b) { return (unsigned)(b < nw ? b : nw - 1) * 16u; };
-  const int b = tid;                  // this lane's bin in phase C
-  const bool okb = b < nw;
-  const unsigned vb_own = voff(b);
   {
+    const int b = tid;                // this lane's bin in phase C
+    const bool okb = b < nw;
     const int spec = a.c.spectrum[ic];
     const double Hs = a.c.Hs[ic], Tp = a.c.Tp[ic], gam = a.c.gamma[ic];
     const rh_c128* XI0 = a.c.Xi_init ? a.c.Xi_init + c6 : nullptr;
@@ -242,8 +248,11 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
     lz[b] = okb ? zz : 0.0;
     if (okb && a.o.zeta) a.o.zeta[(size_t)ic * nw + b] = zz;
 #pragma unroll
-    for (int c = 0; c < 6; ++c)
-      xl[c * LT + b] = csel(okb, csel(XI0 != nullptr, ld(XI0 + c * nw + b), mk(a.c.XiStart, 0.0)), mk(0.0, 0.0));
+    for (int c = 0; c < 6; ++c) {
+      cd x0 = mk(a.c.XiStart, 0.0);
+      if (XI0) x0 = ld(XI0 + c * nw + (okb ? b : nw - 1));   // uniform branch; in-range address
+      xl[c * LT + b] = csel(okb, x0, mk(0.0, 0.0));
+    }
   }
   rh_c128* Xo = a.o.Xi + c6;
   rh_c128* XP = a.o.Xi_prev ? a.o.Xi_prev + c6 : nullptr;
@@ -251,7 +260,7 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
   const int nloop = a.c.nIter + 1;
   const double tol = a.c.tol;
   int status = RH_CASE_NOT_CONVERGED, iters = nloop;
-  double margin = INFINITY;
+  if (tid == 0) mred[LW] = INFINITY;   // closest call of the convergence test so far (LDS)
   __syncthreads();
   // phase-A node range of this lane's group: PB = 2 splits the node list at the member
   // boundary closest to its middle (a member's terms are computed once per group)
@@ -262,20 +271,25 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
       const int dd = abs(2 * mstart[m] - nn);
       if (dd < bestd) { bestd = dd; split = mstart[m]; }
     }
-    const int g = tid / TB;
+    split = __builtin_amdgcn_readfirstlane(split);   // uniform
+    const int g = wv_s / LWA;
     na0 = g ? split : 0;
     na1 = g ? nn : split;
   }
   cd X[6];   // this lane's unrelaxed solution of the current iteration
+  PROF_T(tp1);
+  PROF_ADD(0, tp1 - tp0);
 #ifdef ABL
   const bool n0_never = a.c.nIter == 12345;
 #endif
 
   for (int it = a.c.first_iter; it < nloop; ++it) {
+    PROF_T(ta0);
+    PROF_ADD(7, 1);
     // ---------------- A: per-node sums of squared relative-velocity components ----------
     // (raft/raft_fowt.py:1205-1211; member-factored as in k_solve_lds)
     {
-      const int tb = tid % TB, wg = tb >> 6;
+      const int tb = tnow() & (TB - 1), wg = wv_s & (LWA - 1);
       unsigned vb[PB];
       double bz[PB];
 #pragma unroll
@@ -365,8 +379,10 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
       }
     }
     __syncthreads();
+    PROF_T(ta1);
+    PROF_ADD(1, ta1 - ta0);
     // ---------------- B: node drag matrices and B_drag ----------------------------------
-    for (int n = tid; n < nn; n += LT) {
+    for (int n = tnow(); n < nn; n += LT) {
       double r3[3];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
@@ -393,15 +409,24 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
       for (int e = 0; e < 36; ++e) bdn[e * nn + n] = t3to6(bm + 9 * n, rx, ry, rz, e / 6, e % 6);
     }
     __syncthreads();
-    if (tid < 36) {
-      const double* P = bdn + tid * nn;
-      double s = 0;
-      for (int n = 0; n < nn; ++n) s += P[n];
-      bd[tid] = s;
-      bsum[tid] = mbc[36 + tid] + s;
+    if (wv_s == 0) {
+      const int e = lane_here();
+      if (e < 36) {
+        const double* P = bdn + e * nn;
+        double s = 0;
+        for (int n = 0; n < nn; ++n) s += P[n];
+        bd[e] = s;
+        bsum[e] = mbc[36 + e] + s;
+      }
     }
     __syncthreads();
+    PROF_T(ta2);
+    PROF_ADD(2, ta2 - ta1);
     // ---------------- C: excitation of this lane's bin ----------------------------------
+    const int b = tnow();
+    const bool okb = b < nw;
+    const int par = b & 1;
+    const unsigned vb_own = voff(b);
     cd F[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
@@ -467,6 +492,8 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
         }
       }
     }
+    PROF_T(ta3);
+    PROF_ADD(3, ta3 - ta2);
     // ---------------- C: Z(w) and the pair solves of the pair's two bins ---------------
     // Right-hand sides of both passes first, so that F is dead before the first solve: pass q
     // solves bin (tid & ~1) | q, whose rows 2s + par this lane needs.
@@ -480,7 +507,7 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
     double my_tmax = 0.0;
 #pragma unroll 1
     for (int q = 0; q < 2; ++q) {   // not unrolled: one pass's matrix live at a time
-      const int bq = (tid & ~1) | q;   // the bin solved in this pass (uniform in the pair)
+      const int bq = (b & ~1) | q;   // the bin solved in this pass (uniform in the pair)
       cd A[3][6], x[6], y[3];
 #pragma unroll
       for (int s = 0; s < 3; ++s) y[s] = csel(q != 0, y1[s], y0[s]);
@@ -535,19 +562,23 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
         }
       }
     }
+    PROF_T(ta4);
+    PROF_ADD(4, ta4 - ta3);
     // ---------------- D: the convergence vote ------------------------------------------
     if (a.o.margin) {
       const double mw = wave_max(my_tmax);
-      if (lane == 0) mred[wv] = mw;
+      if (lane_here() == 0) mred[wv_s] = mw;
     }
     const int all_ok = __syncthreads_and(my_ok ? 1 : 0);
-    if (a.o.margin && tid == 0) {
+    if (a.o.margin && b == 0) {   // mred is rewritten only after the next iteration's solves
       double mx = mred[0];
       for (int w = 1; w < LW; ++w) mx = fmax(mx, mred[w]);
-      margin = closer_call(margin, mx - tol);
+      mred[LW] = closer_call(mred[LW], mx - tol);
     }
     const int any_nan = __syncthreads_or(my_nan ? 1 : 0);
     const int any_sing = __syncthreads_or(my_sing ? 1 : 0);
+    PROF_T(ta5);
+    PROF_ADD(5, ta5 - ta4);
     const bool last = any_nan || any_sing || all_ok || it + 1 == nloop;
     if (last) {
       status = any_nan ? RH_CASE_NAN : any_sing ? RH_CASE_SINGULAR : all_ok ? RH_CASE_CONVERGED : RH_CASE_NOT_CONVERGED;
@@ -569,16 +600,20 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
       }
     }
   }
+  const int b = tid;
+  const bool okb = b < nw;
+  const int lane = tid & 63, wv = tid >> 6;
   if (!HOLD) {   // the final unrelaxed solution, for the statistics below
 #pragma unroll
     for (int c = 0; c < 6; ++c) X[c] = csel(okb, ld(Xo + c * (okb ? nw : 0) + (okb ? b : 0)), mk(0.0, 0.0));
   }
 
   // ---------------- outputs ------------------------------------------------------------
+  PROF_T(te0);
   if (tid == 0) {
     a.o.iters[ic] = iters;
     a.o.status[ic] = status;
-    if (a.o.margin) a.o.margin[ic] = margin;
+    if (a.o.margin) a.o.margin[ic] = mred[LW];
   }
   if (a.o.B_drag && tid < 36) a.o.B_drag[(size_t)ic * 36 + tid] = bd[tid];
   if (a.o.Bmat)
@@ -619,6 +654,8 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
       a.o.std[(size_t)ic * 6 + tid] = sqrt(0.5 * s);
     }
   }
+  PROF_T(te1);
+  PROF_ADD(6, te1 - te0);
 }
 
 }  // namespace rh

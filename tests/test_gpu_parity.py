@@ -228,17 +228,18 @@ def test_system_solve_12dof_matches_numpy():
         np.testing.assert_allclose(X[:, b], np.linalg.solve(Zs, F[:, b]), rtol=1e-10, atol=1e-12)
 
 
-@pytest.mark.parametrize("other", [1, 2, 3], ids=["general", "grouped", "lds512"])
+@pytest.mark.parametrize("other", [1, 2, 3], ids=["general", "grouped", "pair"])
 @pytest.mark.parametrize("tag,design,settings,ncase", [("c2_nw1000", "VolturnUS-S_example", {"min_freq": 0.0002}, 128),
                                                        ("c2_nw200", "VolturnUS-S_example", None, 64),
                                                        ("c1_OC3spar", "OC3spar", None, 17)])
 def test_fast_and_general_kernels_agree(tag, design, settings, ncase, other, monkeypatch):
-    """The default path (k_solve_pair: one bin per lane, lane-pair LU, XiLast in LDS) against
-    the general kernel (k_solve_cases, other=1), the lock-step grouped kernel (k_solve_grp, two
-    cases of one design and heading per workgroup, other=2) and the previous 512-thread fast
-    kernel (k_solve_lds, other=3) on the same batch: identical iteration counts and statuses,
-    outputs within 1e-12 (they differ only in the summation order of the per-node bin
-    reductions).  An odd case count leaves a half-empty group."""
+    """The default path (k_solve_lds: one case per workgroup, XiLast in LDS) against the
+    general kernel (k_solve_cases, other=1), the lock-step grouped kernel (k_solve_grp, two
+    cases of one design and heading per workgroup, other=2) and the lane-pair kernel
+    (k_solve_pair: one bin per lane, the LU split over a lane pair, other=3) on the same batch:
+    identical iteration counts and statuses, outputs within 1e-12 (they differ only in the
+    summation order of the per-node bin reductions).  An odd case count leaves a half-empty
+    group."""
     from raft import _native as N
     T = load_golden(tag)
     m, f = make_model(design, T, settings)
@@ -347,10 +348,11 @@ def test_margin_output_and_knobs():
 
 @pytest.mark.parametrize("nw", [77, 255, 256, 333, 513, 1000])
 def test_pair_kernel_odd_grids(nw):
-    """k_solve_pair on grids that leave pad lanes: nw not a multiple of 64 (every block size),
-    odd nw (a lane pair with one real and one pad bin), nw just past a block size (whole pad
-    waves).  Against the general kernel k_solve_cases and the previous fast kernel k_solve_lds
-    on the same batch: identical iteration counts and statuses, Xi within 1e-12."""
+    """Grids that leave pad lanes: nw not a multiple of 64 (every block size), odd nw (a lane
+    pair of k_solve_pair with one real and one pad bin), nw just past a block size (whole pad
+    waves).  The default kernel (k_solve_lds, including its <1, 256> form) against the general
+    kernel k_solve_cases and the lane-pair kernel k_solve_pair on the same batch: identical
+    iteration counts and statuses, Xi within 1e-12."""
     from raft import _native as N
     T = load_golden("c2_nw200")
     m, f = make_model("VolturnUS-S_example", T, {"min_freq": 0.2 / nw})
@@ -370,5 +372,7 @@ def test_pair_kernel_odd_grids(nw):
             assert rel(a["Xi"][ic], b["Xi"][ic]) < 1e-12, (other, ic)
             assert rel(a["psd"][ic], b["psd"][ic]) < 1e-12, (other, ic)
             assert rel(a["B_drag"][ic], b["B_drag"][ic]) < 1e-12, (other, ic)
-        np.testing.assert_allclose(a["std"], b["std"], rtol=1e-12)
+        # per case, relative to its largest DOF (a heading-0 case has noise-level sway/roll/yaw)
+        smax = np.abs(b["std"]).max(axis=1, keepdims=True)
+        assert np.all(np.abs(a["std"] - b["std"]) <= 1e-12 * smax)
         np.testing.assert_allclose(a["margin"], b["margin"], rtol=1e-9, atol=1e-15)

@@ -1,0 +1,24 @@
+"""CPU: the ISA gate of tools/isa_check.py on the gfx950 device code of librafthip.
+
+Compiles rh_abi.hip to assembly (hipcc cross-compiles without a GPU) and fails on
+  * dynamic register indexing (s_set_gpr_idx / v_movrel) in any kernel -- the lowering that
+    faulted k_qtf_hankel on the box in round 2;
+  * scratch (spill) instructions inside a streaming loop of a default-path hot kernel (a
+    reload there drains the wave-table prefetch ring every node); off-path kernels are held to
+    a ratchet of their current counts."""
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
+def test_isa_gate():
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_check.py")], capture_output=True, text=True,
+                       timeout=600)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
+    assert "k_solve_lds<2, 512>" in p.stdout and "FAIL" not in p.stdout
