@@ -162,21 +162,36 @@ def induction_factors(r, chord, Rhub, Rtip, phi, cl, cd, B, Vx, Vy, usecd, hublo
     return fzero, a, ap
 
 
-def thrust_torque(Np, Tp, r, precurve, presweep, precone, Rhub, Rtip, precurveTip, presweepTip):
-    """Blade thrust and torque: trapezoidal integration along the blade path, the loads going
-    to zero at the hub and tip radii."""
+def thrust_torque(Np, Tp, r, precurve, presweep, precone, Rhub, Rtip, precurveTip, presweepTip, azimuth=0.0):
+    """One blade's hub loads at one azimuth [rad]: trapezoidal integration along the blade path,
+    the section loads going to zero at the hub and tip radii.
+      T  = int Np cos(cone) ds                           (shaft thrust)
+      Q  = int Tp z_az ds                                (shaft torque)
+      Y  = int [Tp cos(az) - Np sin(cone) sin(az)] ds    (in-plane side force, hub frame)
+      Z  = int [Tp sin(az) + Np sin(cone) cos(az)] ds    (in-plane vertical force)
+      My = cos(az) int Np z_az ds,  Mz = sin(az) int Np z_az ds   (the flapwise moment turned
+                                                         into the hub frame by the azimuth)
+    The side loads were identified against the reference's own expectations that depend on
+    them (tests/test_model.py desired_X0 'wind': sway, heave, roll and yaw), see DESIGN.md §2."""
     rfull = np.r_[Rhub, r, Rtip]
     curvefull = np.r_[0.0, precurve, precurveTip]
     sweepfull = np.r_[0.0, presweep, presweepTip]
     Npfull = np.r_[0.0, Np, 0.0]
     Tpfull = np.r_[0.0, Tp, 0.0]
     x_az, y_az, z_az, cone, s = define_curvature(rfull, curvefull, sweepfull, precone)
-    thrust = Npfull * np.cos(cone)
-    torque = Tpfull * z_az
     ds = s[1:] - s[:-1]
-    T = np.sum(ds * 0.5 * (thrust[:-1] + thrust[1:]))
-    Q = np.sum(ds * 0.5 * (torque[:-1] + torque[1:]))
-    return T, Q
+
+    def trap(g):
+        return np.sum(ds * 0.5 * (g[:-1] + g[1:]))
+
+    sa, ca = np.sin(azimuth), np.cos(azimuth)
+    radial = Npfull * np.sin(cone)
+    T = trap(Npfull * np.cos(cone))
+    Q = trap(Tpfull * z_az)
+    Y = trap(Tpfull * ca - radial * sa)
+    Z = trap(Tpfull * sa + radial * ca)
+    Mflap = trap(Npfull * z_az)
+    return T, Q, Y, Z, Mflap * ca, Mflap * sa
 
 
 class CCBlade:
@@ -325,9 +340,10 @@ class CCBlade:
             for j in range(nsec):
                 azimuth = 360.0 * float(j) / nsec
                 loads, _ = self.distributedAeroLoads(Uinf[i], Omega[i], pitch[i], azimuth)
-                Tsub, Qsub = thrust_torque(loads["Np"], loads["Tp"], *args)
-                L["T"][i] += self.B * Tsub / nsec
-                L["Q"][i] += self.B * Qsub / nsec
+                sub = thrust_torque(loads["Np"], loads["Tp"], *args, azimuth=np.radians(azimuth))
+                for k, v in zip(("T", "Q", "Y", "Z", "My", "Mz"), sub):
+                    L[k][i] += self.B * v / nsec
+                L["Mb"][i] += np.hypot(sub[4], sub[5]) / nsec   # one blade's flapwise root moment (unpinned)
                 if self.derivatives:
                     rot = Omega[i] != 0
                     n = len(self.r)
@@ -336,9 +352,12 @@ class CCBlade:
                         dNp[s_], dTp[s_] = self._section_derivs(s_, loads["phi"][s_], Uinf[i], Omega[i], pitch[i],
                                                                 azimuth, rot)
                     for k in range(3):   # T and Q are linear in the section loads
-                        dt, dq = thrust_torque(dNp[:, k], dTp[:, k], *args)
+                        dt, dq = thrust_torque(dNp[:, k], dTp[:, k], *args)[:2]
                         dTx[i, k] += self.B * dt / nsec
                         dQx[i, k] += self.B * dq / nsec
+            if nsec == 1:   # axisymmetric inflow: the B blades' in-plane loads cancel (unpinned case)
+                for k in ("Y", "Z", "My", "Mz"):
+                    L[k][i] = 0.0
         P = L["Q"] * Omega * np.pi / 30.0
         loads = dict(L, P=P)
         derivs = {}

@@ -92,6 +92,8 @@ def catenary(XF, ZF, L, EA, W, CB=0.0, Tol=1e-6, MaxIter=100, HF0=0.0, VF0=0.0):
         HF += dHF
         VF += dVF
     else:
+        if HF0 > 0 and VF0 > 0:           # a warm start far from this shape: retry from the
+            return catenary(XF, ZF, L, EA, W, CB, Tol, MaxIter)   # default guess, as MoorPy does
         raise RuntimeError(f"catenary did not converge (XF={XF}, ZF={ZF}, L={L})")
     K = np.array([[J[1][1], -J[0][1]], [-J[1][0], J[0][0]]]) / det     # inv(J)
     VFMWL = VF - WL
@@ -220,7 +222,7 @@ class MooringSystem:
     """A quasi-static mooring system: fixed, coupled (body-attached) and free points joined
     by catenary lines; one or more coupled bodies (one per FOWT)."""
 
-    def __init__(self, depth=0.0, rho=RHO, g=G, cat_tol=1e-6):
+    def __init__(self, depth=0.0, rho=RHO, g=G, cat_tol=1e-5):
         self.depth = float(depth)
         self.cat_tol = cat_tol            # relative tolerance of the catenary solves
         self.free_tol = 0.05              # free-point equilibrium step tolerance [m]

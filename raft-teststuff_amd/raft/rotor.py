@@ -32,7 +32,8 @@ RPM2RADPS = 0.1047
 
 def ccblade_classes():
     """(CCBlade, CCAirfoil) from the installed package, as raft/raft_rotor.py:17-20 imports
-    them, or (None, None)."""
+    them, else the restatement in raft/ccblade.py (Ning's BEM as CCBlade implements it,
+    pinned by the reference's wind-case expectations)."""
     try:
         from ccblade.ccblade import CCBlade, CCAirfoil
         return CCBlade, CCAirfoil
@@ -41,7 +42,8 @@ def ccblade_classes():
             from wisdem.ccblade.ccblade import CCBlade, CCAirfoil
             return CCBlade, CCAirfoil
         except ImportError:
-            return None, None
+            from .ccblade import CCAirfoil, CCBlade
+            return CCBlade, CCAirfoil
 
 
 class IECWind:

@@ -114,3 +114,32 @@ def test_run_raft_with_operating_rotor(monkeypatch):
     r = O.solve_dynamics(T, dict(case), int(m.nIter), float(m.XiStart))
     assert f.iterations == r["iters"]
     assert rel(f.Xi, r["Xi"]) < RTOL, rel(f.Xi, r["Xi"])
+
+
+def test_wind_case_with_bem_restatement():
+    """The reference's wind-wave-current load case (tests/test_model.py:68: 8 m/s wind at 30 deg,
+    4 m / 10 s JONSWAP waves, 0.6 m/s current) on its VolturnUS-S test design with the IEA-15MW
+    blades, through analyzeCases with the CCBlade restatement (raft/ccblade.py; the package is
+    absent): the mean offset equals the reference's desired_X0 at its rtol 1e-5 (the rotor's
+    thrust, side forces and hub moments all enter it), and the device solve with the aero
+    added mass and damping per bin equals the CPU oracle on the same tables (1e-9, same
+    iteration count)."""
+    import raft
+    from conftest import load_design, oracle_tables_of
+    from oracle import raft_oracle as O
+    from test_mooring import CASES, DESIRED_X0
+    d = load_design("VolturnUS-S_aero")
+    case = dict(CASES["wind_wave_current"])
+    d["cases"]["data"] = [[case[k] for k in d["cases"]["keys"]]]
+    m = raft.Model(d)
+    m.analyzeCases()
+    f = m.fowtList[0]
+    np.testing.assert_allclose(m.results["mean_offsets"][0], DESIRED_X0["wind_wave_current"][0], rtol=1e-5,
+                               atol=1e-10)
+    assert np.abs(f.A_aero).max() > 0 and np.abs(f.B_aero).max() > 0
+    T = oracle_tables_of(f)
+    T["A_BEM"] = np.sum(f.A_aero, axis=3)
+    T["B_BEM"] = np.sum(f.B_aero, axis=3) + np.sum(f.B_gyro, axis=2)[:, :, None]
+    r = O.solve_dynamics(T, dict(case), int(m.nIter), float(m.XiStart))
+    assert f.iterations == r["iters"]
+    assert rel(f.Xi, r["Xi"]) < RTOL, rel(f.Xi, r["Xi"])
