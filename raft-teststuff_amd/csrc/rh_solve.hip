@@ -31,6 +31,12 @@ constexpr int kLT = 512;          // threads per case workgroup
 constexpr int kLW = kLT / 64;     // waves per case workgroup
 constexpr int kRingA = 3;         // wave-table prefetch depth (nodes) of phase A
 constexpr int kRingC = 6;         // ... of phase C (one bin per pass: less work per node)
+#ifndef RH_ONE_VOTE
+#define RH_ONE_VOTE 1                 // one barrier (LDS flag word) for the three end-of-iteration votes
+#endif
+#ifndef RH_A_BATCH
+#define RH_A_BATCH 0                  // > 0: phase-A nodes in batches of RH_A_BATCH, one tbfly16 per batch
+#endif
 #ifndef RH_LDS_LANE_BRANCH
 #define RH_LDS_LANE_BRANCH 0          // 1: the round-2 per-lane `continue` before the solve (A/B only)
 #endif
@@ -171,7 +177,7 @@ __host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB, int LT 
                            + (size_t)2 * LT * NB     // w and zeta per (padded) bin
                            + 36 + 108 + LW * 6 + 36  // B_drag, M|B|C image, std partials, B_lin+B_drag
                            + LW)                     // convergence-margin partials
-         + sizeof(int) * ((size_t)nm + 2);            // member node ranges
+         + sizeof(int) * ((size_t)nm + 4);            // member node ranges, vote words
 }
 
 // LT threads per case: 512 (8 waves), or 256 for nw <= 256 (two cases per CU; C4 has 240 bins)
@@ -211,10 +217,12 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
   double* lz = lw + NWP;                           // [NWP] zeta per bin (pad bins: 0)
   double* mred = lz + NWP;                         // [LW] per-wave max of tolCheck
   int* mstart = reinterpret_cast<int*>(mred + LW);  // [nm+1]
+  int* sflag = mstart + nm + 1;                      // [2] vote words of even / odd iterations
   load_mbc(d, mbc, tid);
   for (int n = tid; n < nn; n += LT) nt[n] = node[RH_NF_T * nn + n];
   for (int e = tid; e < 18 * nm; e += LT) mbf[e] = d.memb[e];   // RH_MF_CQ0..C20 are fields 0..17
   for (int e = tid; e <= nm; e += LT) mstart[e] = d.mstart[e];
+  if (tid < 2) sflag[tid] = 0;
 
   // Per-bin scalars live in LDS, not in registers: nothing per-thread stays live across the
   // phases, so the register-heavy solve of phase C does not push other values to scratch.
@@ -300,6 +308,9 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
       };
       auto load_node = [&](cd (&K)[3][NB], int n) {
         const unsigned so = (unsigned)(n < nn ? n : nn - 1) * 3u * nw16;
+#if RH_ABL_A_NOLOAD   // timing ablation: the ring keeps its first nodes (wrong results)
+        if (n >= kRingA) return;
+#endif
 #pragma unroll
         for (int j = 0; j < NB; ++j)
 #pragma unroll
@@ -309,6 +320,11 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
       auto node_sums = [&](const cd (&K)[3][NB], int n, double& s0, double& s1, double& s2) {
         const double t = nt[n];
         s0 = s1 = s2 = 0;
+#if RH_ABL_A_NOCOMP   // timing ablation: consume the loads with one add each (wrong results)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) { s0 += K[0][j].r + K[0][j].i; s1 += K[1][j].r + K[1][j].i; s2 += K[2][j].r + K[2][j].i; }
+        return;
+#endif
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
           const double z = bz[j];
@@ -320,6 +336,42 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
           s2 += abs2(sp2);
         }
       };
+#if RH_A_BATCH
+      // Nodes in batches of kB (= the ring depth): the three sums of each node of a batch are
+      // independent chains, and the 3 kB values are reduced over the wave by ONE transposing
+      // butterfly (tbfly16: 17 exchange steps for up to 16 values, against 8 per node for
+      // tbfly3); lanes 0..15 then hold the totals.  The ring slot of node n is refilled with
+      // node n + kB as soon as n is summed.
+      constexpr int kB = RH_A_BATCH;
+      static_assert(3 * kB <= 16, "tbfly16 reduces at most 16 values");
+      cd K[kB][3][NB];
+#pragma unroll
+      for (int r = 0; r < kB; ++r) load_node(K[r], r);
+      int m = -1, mnext = 0;
+      for (int n = 0; n < nn; n += kB) {
+        double u[16];
+#pragma unroll
+        for (int r = 0; r < kB; ++r) {
+          const int nr = n + r;
+          if (nr < nn) {
+            if (nr == mnext) {   // uniform: entering member m+1 (members are node-contiguous)
+              do { ++m; mnext = mstart[m + 1]; } while (mnext == nr);
+              member_terms(m);
+            }
+            node_sums(K[r], nr, u[3 * r], u[3 * r + 1], u[3 * r + 2]);
+            load_node(K[r], nr + kB);
+          } else {
+            u[3 * r] = u[3 * r + 1] = u[3 * r + 2] = 0.0;
+          }
+        }
+#pragma unroll
+        for (int v = 3 * kB; v < 16; ++v) u[v] = 0.0;
+        const int ln = lane_here();
+        const double tot = tbfly16(u, ln);
+        const int vi = tbfly16_index(ln);
+        if (ln < 16 && vi < 3 * kB && n + vi / 3 < nn) red[((n + vi / 3) * 3 + vi % 3) * LW + wv_s] = tot;
+      }
+#else
       // the three sums of a node are reduced over the wave together (tbfly3); lane k < 3
       // writes sum k.  The ring slot of node n is refilled with node n + kRingA.
       cd K[kRingA][3][NB];
@@ -339,11 +391,16 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
             node_sums(K[r], nr, s0, s1, s2);
             load_node(K[r], nr + kRingA);
             const int ln = lane_here();
+#if RH_ABL_A_NOBFLY
+            const double tot = s0 + s1 + s2;
+#else
             const double tot = tbfly3(s0, s1, s2, ln);
+#endif
             if (ln < 3) red[(nr * 3 + tbfly3_index(ln)) * LW + wv_s] = tot;
           }
         }
       }
+#endif
     }
     __syncthreads();
     PROF_T(ta1);
@@ -415,6 +472,9 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
         cd SQ = mk(0, 0), S1 = mk(0, 0), S2 = mk(0, 0), T1 = mk(0, 0), T2 = mk(0, 0);
         auto load1 = [&](cd (&K)[3], int n) {
           const unsigned so = (unsigned)(n < nn ? n : nn - 1) * 3u * nw16;
+#if RH_ABL_C_NOLOAD
+          if (n >= kRingC) return;
+#endif
 #pragma unroll
           for (int p = 0; p < 3; ++p) K[p] = bld(bK, vj, so + (unsigned)p * nw16);
         };
@@ -441,6 +501,11 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
           }
           const double* A = al + 5 * n;
           const double A0 = A[0], A1 = A[1], A2 = A[2], A3 = A[3], A4 = A[4];
+#if RH_ABL_C_NOCOMP
+          SQ = add(SQ, K[0]); S1 = add(S1, K[1]); S2 = add(S2, K[2]);
+          load1(K, n + kRingC);
+          return;
+#endif
           SQ = add(SQ, scl(K[0], A0));
           S1 = add(S1, scl(K[1], A1));
           S2 = add(S2, scl(K[2], A2));
@@ -542,6 +607,27 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
       const double mw = wave_max(my_tmax);
       if (lane == 0) mred[wv] = mw;
     }
+#if RH_ONE_VOTE
+    // One barrier for the three votes: each wave ORs its flag bits (1 = a bin not converged,
+    // 2 = NaN, 4 = singular) into this iteration's LDS word; tid 0 clears the other word for
+    // the next iteration (everyone has read it: it was last read before this iteration's
+    // phase-A barrier).
+    {
+      const unsigned long long bn = __builtin_amdgcn_ballot_w64(!my_ok), bx = __builtin_amdgcn_ballot_w64(my_nan),
+                               bs = __builtin_amdgcn_ballot_w64(my_sing);
+      const int bits = (bn ? 1 : 0) | (bx ? 2 : 0) | (bs ? 4 : 0);
+      if (lane == 0 && bits) atomicOr(&sflag[it & 1], bits);
+    }
+    __syncthreads();
+    const int fl = sflag[it & 1];
+    if (tid == 0) sflag[(it + 1) & 1] = 0;
+    const int all_ok = !(fl & 1), any_nan = fl & 2, any_sing = fl & 4;
+    if (a.o.margin && tid == 0) {   // mred is rewritten only after the next phase-A barrier
+      double mx = mred[0];
+      for (int w = 1; w < LW; ++w) mx = fmax(mx, mred[w]);
+      margin = closer_call(margin, mx - tol);
+    }
+#else
     const int all_ok = __syncthreads_and(my_ok ? 1 : 0);
     if (a.o.margin && tid == 0) {   // mred is rewritten only after the next phase-A barrier
       double mx = mred[0];
@@ -550,6 +636,7 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
     }
     const int any_nan = __syncthreads_or(my_nan ? 1 : 0);
     const int any_sing = __syncthreads_or(my_sing ? 1 : 0);
+#endif
     PROF_T(ta4);
     PROF_ADD(5, ta4 - ta3);
     if (any_nan) {
