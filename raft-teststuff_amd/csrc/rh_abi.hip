@@ -5,6 +5,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -48,6 +49,9 @@ struct rh_ctx {
   // a second stream for k_qtf_kay, which runs beside k_qtf_lcoef + k_qtf_gemm (rh_ctx_create)
   hipStream_t qtf_aux = nullptr;
   hipEvent_t qtf_tables_done = nullptr, qtf_kay_done = nullptr;
+  // serialises the record -> wait -> launch -> record sequence on qtf_aux and its two events:
+  // calls from several host threads on one context must not interleave it
+  std::mutex qtf_mu;
 };
 
 namespace {
@@ -585,6 +589,7 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
       // k_qtf_lcoef + k_qtf_gemm (each alone fills ~1.3 waves of workgroups), and k_qtf_kay_sum
       // joins the two on the caller's stream.  Every later use of the workspace on `s` is
       // ordered after k_qtf_kay_sum, which waits for k_qtf_kay.
+      std::lock_guard<std::mutex> lock(ctx->qtf_mu);
       RH_HIP(hipEventRecord(ctx->qtf_tables_done, s));
       RH_HIP(hipStreamWaitEvent(ctx->qtf_aux, ctx->qtf_tables_done, 0));
       hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, ctx->qtf_aux, *q, wk, qtf, rank, nrank,
@@ -696,8 +701,17 @@ int rh_prep_designs(int ndesign, const double* spec, const long long* spec_off, 
   nt = std::max(1, std::min({nt, 64, std::max(ndesign, 1)}));
   std::atomic<int> next{0};
   auto work = [&]() {
-    for (int i = next++; i < ndesign; i = next++)
-      rhp::prep_one(spec + spec_off[i], spec_off[i + 1] - spec_off[i], nw, w, k, p->res[i]);
+    for (int i = next++; i < ndesign; i = next++) {
+      try {   // an exception must not leave a worker thread (std::terminate): it becomes RH_EINVAL
+        rhp::prep_one(spec + spec_off[i], spec_off[i + 1] - spec_off[i], nw, w, k, p->res[i]);
+      } catch (const std::exception& e) {
+        p->res[i].ok = 0;
+        p->res[i].err = std::string("rh_prep_designs: ") + e.what();
+      } catch (...) {
+        p->res[i].ok = 0;
+        p->res[i].err = "rh_prep_designs: unknown exception";
+      }
+    }
   };
   if (nt == 1) {
     work();

@@ -616,6 +616,16 @@ struct Reader {
     }
     return *p++;
   }
+  // an element count: an integer in [0, what is left of the record] (a malformed record would
+  // otherwise size vectors from arbitrary doubles)
+  int count() {
+    const double v = get();
+    if (!(v >= 0.0) || v > (double)(end - p) || v != (double)(long long)v) {
+      bad = true;
+      return 0;
+    }
+    return (int)v;
+  }
   void vec(std::vector<double>& v, int n) {
     v.resize(n > 0 ? n : 0);
     for (int i = 0; i < n; ++i) v[i] = get();
@@ -630,7 +640,11 @@ inline void prep_one(const double* spec, long long len, int nw, const double* w,
     out.err = "rh_prep_designs: bad spec record (magic)";
     return;
   }
-  const int nmemb = (int)rd.get(), nrot = (int)rd.get();
+  const int nmemb = rd.count(), nrot = rd.count();
+  if (rd.bad) {
+    out.err = "rh_prep_designs: bad spec record (member / rotor counts)";
+    return;
+  }
   const double rho = rd.get(), g = rd.get();
   double r6[6];
   for (double& x : r6) x = rd.get();
@@ -650,7 +664,11 @@ inline void prep_one(const double* spec, long long len, int nw, const double* w,
     b.potMod = (int)rd.get();
     b.mcf = (int)rd.get();
     b.nacelle = (int)rd.get();
-    const int nst = (int)rd.get(), ncap = (int)rd.get(), nhead = (int)rd.get();
+    const int nst = rd.count(), ncap = rd.count(), nhead = rd.count();
+    if (rd.bad) {
+      out.err = "rh_prep_designs: bad spec record (station / cap / heading counts)";
+      return;
+    }
     b.has_t = (int)rd.get();
     const double gamma0 = rd.get();
     b.dlsMax = rd.get();

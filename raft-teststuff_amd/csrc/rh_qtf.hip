@@ -65,11 +65,14 @@ struct QtfWork {
                    //                  k_qtf_kay_sum, so k_qtf_kay can run beside k_qtf_gemm)
 };
 
+// The MFMA-path operands (R, L, Rp, Lp, KA, KB, KR and the Kim & Yue tile sums KS) are
+// reserved only for a sorted grid (order == 1), the only one the MFMA path runs on.
 __host__ __device__ inline size_t qtf_work_elems(const rh_qtf_design& q) {   // complex elements
   const size_t n2p = (size_t)qtf_n2p(q), kp = (size_t)qtf_kp(q), kq = (size_t)qtf_kq(q);
-  return (size_t)q.nq * QT_COUNT * q.n2 + (size_t)q.nmq * WT_COUNT * q.n2 + (size_t)FT_COUNT * q.n2 +
-         (size_t)q.nkr * q.n2 * 12 + ((size_t)q.nkr * q.n2 * kKayT + 1) / 2 +
-         7 * kp * n2p + 14 * kq * n2p + ((size_t)3 * q.nkr * kKayK * n2p + 1) / 2 +
+  const size_t base = (size_t)q.nq * QT_COUNT * q.n2 + (size_t)q.nmq * WT_COUNT * q.n2 + (size_t)FT_COUNT * q.n2 +
+                      (size_t)q.nkr * q.n2 * 12 + ((size_t)q.nkr * q.n2 * kKayT + 1) / 2;
+  if (q.order != 1) return base;
+  return base + 7 * kp * n2p + 14 * kq * n2p + ((size_t)3 * q.nkr * kKayK * n2p + 1) / 2 +
          (size_t)(n2p / 16) * (n2p / 16 + 1) / 2 * 12 * 256 / 2;
 }
 
@@ -91,6 +94,7 @@ __host__ inline QtfWork qtf_carve(const rh_qtf_design& q, void* work) {
   wk.KB = wk.KA + (size_t)q.nkr * kKayK * n2p;
   wk.KR = wk.KB + (size_t)q.nkr * kKayK * n2p;
   wk.KS = wk.KR + (size_t)q.nkr * kKayK * n2p;
+  if (q.order != 1) wk.R = wk.L = wk.Rp = wk.Lp = nullptr, wk.KA = wk.KB = wk.KR = wk.KS = nullptr;
   return wk;
 }
 

@@ -222,6 +222,14 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
         parts.append(res)
         keep.append((B, cs, prep, res))
     out = {k: torch.cat([r[k] for r in parts], 0) for k in parts[0]}
+    # The blocks' tables were allocated on the upload stream and are read by kernels on the
+    # solve stream.  The caching allocator hands a freed block back to work on the stream that
+    # allocated it, so order every later upload-stream operation after this sweep's kernels:
+    # dropping `keep` before synchronising can then never let an upload overwrite tables that
+    # a kernel is still reading.
+    done = torch.cuda.Event()
+    done.record(compute)
+    copy.wait_event(done)
     return out, keep
 
 

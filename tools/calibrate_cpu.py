@@ -1,0 +1,36 @@
+"""§8(d) calibration of the CPU baseline: the port (oracle/raft_oracle.py, loop=True, the
+reference's per-node/per-bin loop structure) against the reference itself on the same four C2
+golden cases (tests/golden/c2_nw1000.npz: VolturnUS-S, nw = 1000), one core each.  The
+reference's per-case seconds were recorded while it generated the fixture (out_seconds,
+tests/golden/make_golden.py run_solve).  Prints one line per case and the mean ratio."""
+import json
+import os
+import sys
+import time
+
+os.environ["OPENBLAS_NUM_THREADS"] = os.environ["OMP_NUM_THREADS"] = "1"
+import numpy as np  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from conftest import golden_cases  # noqa: E402
+from oracle import raft_oracle as O  # noqa: E402
+
+
+def main():
+    T = dict(np.load(os.path.join(ROOT, "tests", "golden", "c2_nw1000.npz")))
+    out = []
+    for ic, case in enumerate(golden_cases(T)):
+        t0 = time.perf_counter()
+        r = O.solve_dynamics(T, dict(case), int(T["nIter"]), float(T["XiStart"]), loop=True)
+        dt = time.perf_counter() - t0
+        ref = float(T["out_seconds"][ic])
+        assert r["iters"] == T["out_iters"][ic]
+        out.append(dict(case=ic, port_s=dt, reference_s=ref, ratio=dt / ref))
+        print(f"case {ic}: port {dt:6.1f} s  reference {ref:6.1f} s  ratio {dt / ref:5.2f}", flush=True)
+    print(json.dumps({"cases": out, "mean_ratio": float(np.mean([o["ratio"] for o in out]))}))
+
+
+if __name__ == "__main__":
+    main()
