@@ -32,7 +32,7 @@ constexpr int kLW = kLT / 64;     // waves per case workgroup
 constexpr int kRingA = 3;         // wave-table prefetch depth (nodes) of phase A
 constexpr int kRingC = 6;         // ... of phase C (one bin per pass: less work per node)
 #ifndef RH_ONE_VOTE
-#define RH_ONE_VOTE 1                 // one barrier (LDS flag word) for the three end-of-iteration votes
+#define RH_ONE_VOTE 0                 // 1: one barrier (LDS flag word) for the three end-of-iteration votes
 #endif
 #ifndef RH_A_BATCH
 #define RH_A_BATCH 0                  // > 0: phase-A nodes in batches of RH_A_BATCH, one tbfly16 per batch
