@@ -78,9 +78,9 @@ def pmc_l2(kernel, kernel_ms):
 def solve_kernel_name(nw):
     """The kernel rh_solve_cases launches for this grid (dispatch in rh_abi.hip)."""
     if nw <= 256:
-        return "rh::k_solve_lds<1, 256>"
+        return "rh::k_solve_lds<1, 256, false>"
     if nw <= 1024:
-        return f"rh::k_solve_lds<{1 if nw <= 512 else 2}>"
+        return f"rh::k_solve_lds<{1 if nw <= 512 else 2}, 512, false>"
     return "rh::k_solve_cases<4>"
 
 
@@ -399,9 +399,11 @@ def bench_c4(device, steps, world, rank, dist, ncase=512):
                        "cases_per_step_per_gpu": ncase, "nw": dd.nw, "fowts": len(m.fowtList),
                        "parallelism": f"case-sharded x{world}"},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP64, "traffic": None, "kernel": solve_kernel_name(dd.nw),
+                         "frac": achieved / PEAK_FP64, "traffic": pmc_traffic(solve_kernel_name(dd.nw)),
+                         "kernel": solve_kernel_name(dd.nw),
                          "kernel_ms": kern_ms, "flops_per_launch": flops,
-                         "note": "the (case, FOWT) drag fixed-point launch; SURVEY.md §8(d) formula per (case, FOWT)"}}
+                         "note": "the (case, FOWT) drag fixed-point launch; SURVEY.md §8(d) formula per (case, FOWT); "
+                                 "traffic = HBM bytes per launch from " + os.path.relpath(PMC_SUMMARY, ROOT)}}
 
 
 C5_DESIGNS = 250
@@ -719,8 +721,8 @@ def main():
                    "nodes_circ_rect": [nc, nr], "nIter": int(m.nIter), "headings": len(dd.headings),
                    "parallelism": f"case-sharded x{world}"},
         "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_FP64, "traffic": pmc_traffic(solve_kernel_name(dd.nw).split("<")[0]),
-                     "l2": pmc_l2(solve_kernel_name(dd.nw).split("<")[0], kern_ms),
+                     "frac": achieved / PEAK_FP64, "traffic": pmc_traffic(solve_kernel_name(dd.nw)),
+                     "l2": pmc_l2(solve_kernel_name(dd.nw), kern_ms),
                      "kernel": solve_kernel_name(dd.nw), "kernel_ms": kern_ms,
                      "wave_tables_ms": tab_ms,
                      "flops_per_launch": flops,

@@ -348,6 +348,24 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   }
   // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case (256 for nw <= 256), nw <= 1024.
   if (nw <= 2 * rh::kLT && !ctx->force_general) {
+#ifndef RH_SMALL_GRID_128
+#define RH_SMALL_GRID_128 0
+#endif
+    // Opt-in (-DRH_SMALL_GRID_128=1), measured and not kept: nw <= 256 on 128
+    // threads x 2 bins (x 1 bin for nw <= 128), node-chunked B_drag (rh_solve.hip), four cases per
+    // CU while a workgroup's LDS stays within 40 KB.  Parity-green; C4 0.73 ms against 0.59 ms
+    // for 256 threads x 1 bin.  The kernel depends on nw only, never on the batch's node counts,
+    // so the bits of a case do not depend on which designs share its launch.
+    if (RH_SMALL_GRID_128 && nw <= rh::kLT / 2) {
+      const int nb128 = nw <= rh::kLT / 4 ? 1 : 2;
+      const size_t lsm128 = rh::solve_lds_smem(nnmax, nmmax, nb128, rh::kLT / 4, true);
+      if (lsm128 <= kMaxLds) {
+        dim3 grid(cases->ncase), block(rh::kLT / 4);
+        if (nb128 == 1) hipLaunchKernelGGL((rh::k_solve_lds<1, rh::kLT / 4, true>), grid, block, lsm128, s, a);
+        else hipLaunchKernelGGL((rh::k_solve_lds<2, rh::kLT / 4, true>), grid, block, lsm128, s, a);
+        return designs_used(ctx, s);
+      }
+    }
     const int nb = nw <= rh::kLT ? 1 : 2;
     const int lt = nw <= rh::kLT / 2 ? rh::kLT / 2 : rh::kLT;   // nw <= 256: 256 threads, two cases per CU
     const size_t lsm = rh::solve_lds_smem(nnmax, nmmax, nb, lt);

@@ -163,13 +163,46 @@ __device__ __forceinline__ double wave_sum63(double v) {
   return v;
 }
 
+// A pointer made wave-uniform (SGPRs), so that loads through the constant address space become
+// scalar loads.
+__device__ __forceinline__ const double* uniform_ptr(const double* p) {
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (const double*)(((unsigned long long)hi << 32) | lo);
+}
+
+// One entry of translateMatrix3to6DOF by block: 0 = Bm[r][c], 1 = (Bm H)[r][c] (the upper-right
+// block; the lower-left one is its transpose), 2 = (H Bm H^T)[r][c]; the expressions of t3to6
+// (rh_kernels.hip), evaluated for all three and selected, so no lane branches.
+__device__ __forceinline__ double t3to6_block(const double* Bm, double rx, double ry, double rz, int blk, int r, int c) {
+  const double H[3][3] = {{0, rz, -ry}, {-rz, 0, rx}, {ry, -rx, 0}};
+  double hc[3], hr[3];   // column c of H, row r of H (selected without dynamic register indexing)
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    hc[k] = c == 0 ? H[k][0] : c == 1 ? H[k][1] : H[k][2];
+    hr[k] = r == 0 ? H[0][k] : r == 1 ? H[1][k] : H[2][k];
+  }
+  double hcc[3];   // row c of H
+#pragma unroll
+  for (int k = 0; k < 3; ++k) hcc[k] = c == 0 ? H[0][k] : c == 1 ? H[1][k] : H[2][k];
+  const double b0 = Bm[3 * r + c];
+  const double b1 = Bm[3 * r + 0] * hc[0] + Bm[3 * r + 1] * hc[1] + Bm[3 * r + 2] * hc[2];
+  double b2 = 0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double HB = hr[0] * Bm[0 * 3 + k] + hr[1] * Bm[1 * 3 + k] + hr[2] * Bm[2 * 3 + k];
+    b2 += HB * hcc[k];
+  }
+  return blk == 0 ? b0 : blk == 1 ? b1 : b2;
+}
+
 // Every table the loops read is staged here: a global load inside the node loops would share
 // the vector-memory counter with the prefetched wave-table loads and force them to drain.
-__host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB, int LT = kLT) {
+__host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB, int LT = kLT, bool ser = false) {
   const int LW = LT / 64;
   return sizeof(double) * ((size_t)12 * LT * NB      // XiLast [6][512 NB] complex
                            + (size_t)nn * 3 * LW     // per-wave node sums
-                           + (size_t)nn * 36          // per-node B_drag contributions
+                           + (ser ? (size_t)0 : (size_t)nn * 36)   // per-node B_drag contributions
                            + (size_t)nn * 9           // Bmat
                            + (size_t)nn * 5           // member-factored drag coefficients
                            + (size_t)nn               // node axial coordinate t
@@ -180,9 +213,11 @@ __host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB, int LT 
          + sizeof(int) * ((size_t)nm + 4);            // member node ranges, vote words
 }
 
-// LT threads per case: 512 (8 waves), or 256 for nw <= 256 (two cases per CU; C4 has 240 bins)
-template <int NB, int LT = kLT>
-__global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
+// LT threads per case: 512 (8 waves), or 256 for nw <= 256 (two cases per CU; C4 has 240 bins),
+// or 128 (SER: four cases per CU, B_drag summed node-serially per entry instead of through a
+// per-node LDS image, so a workgroup needs about 40 KB of LDS).
+template <int NB, int LT = kLT, bool SER = false>
+__global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(CaseArgs a) {
   constexpr int LW = LT / 64;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -210,8 +245,8 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
   double* mbc = bd + 36;                           // [108] M, B_lin, C
   double* sred = mbc + 108;                        // [LW][6]
   double* bsum = sred + LW * 6;                   // [36] B_lin + B_drag of this iteration
-  double* bdn = bsum + 36;                         // [36][nn]
-  double* nt = bdn + 36 * nn;                      // [nn]
+  double* bdn = bsum + 36;                         // [36][nn] (not with SER)
+  double* nt = bdn + (SER ? 0 : 36 * nn);          // [nn]
   double* mbf = nt + nn;                           // [18][nm]
   double* lw = mbf + 18 * nm;                      // [NWP] w per bin (pad bins: w[nw-1])
   double* lz = lw + NWP;                           // [NWP] zeta per bin (pad bins: 0)
@@ -429,15 +464,40 @@ __global__ __launch_bounds__(LT, 512 / LT) void k_solve_lds(CaseArgs a) {
       A[2] = B4[2];
       A[3] = t * B4[1];
       A[4] = t * B4[2];
-      // this node's translateMatrix3to6DOF (raft/helpers.py:455-478), summed below in node order
-      const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
+      if (!SER) {
+        // this node's translateMatrix3to6DOF (raft/helpers.py:455-478), summed below in node order
+        const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
 #pragma unroll
-      for (int e = 0; e < 36; ++e) bdn[e * nn + n] = t3to6(bm + 9 * n, rx, ry, rz, e / 6, e % 6);
+        for (int e = 0; e < 36; ++e) bdn[e * nn + n] = t3to6(bm + 9 * n, rx, ry, rz, e / 6, e % 6);
+      }
     }
     __syncthreads();
-    if (tid < 36) {
-      const double* P = bdn + tid * nn;
+    if (SER) {
+      // B_drag without the per-node image: lane e < 27 sums one of the 27 distinct entries of
+      // translateMatrix3to6DOF (9 of Bm, 9 of Bm H, 9 of H Bm H^T; the lower-left block is the
+      // transpose of the upper-right one) over the nodes in node order, each entry computed
+      // with t3to6's expressions (the same bits as the image path).  Node coordinates are
+      // wave-uniform: scalar loads.
+      if (tid < 27) {
+        const int blk = tid / 9, r = (tid % 9) / 3, c = tid % 3;
+        const f64_kp nodeU = (f64_kp)uniform_ptr(node);
+        double s = 0;
+        for (int n = 0; n < nn; ++n) {
+          const double* Bm = bm + 9 * n;
+          const double rx = nodeU[RH_NF_XX * nn + n], ry = nodeU[RH_NF_XY * nn + n], rz = nodeU[RH_NF_XZ * nn + n];
+          double v = t3to6_block(Bm, rx, ry, rz, blk, r, c);
+          asm volatile("" : "+v"(v));   // an entry is rounded before it is added (as through LDS)
+          s += v;
+        }
+        if (blk == 0) bd[6 * r + c] = s;
+        else if (blk == 1) bd[6 * r + 3 + c] = bd[6 * (3 + c) + r] = s;
+        else bd[6 * (3 + r) + 3 + c] = s;
+      }
+      __syncthreads();
+      if (tid < 36) bsum[tid] = mbc[36 + tid] + bd[tid];
+    } else if (tid < 36) {
       double s = 0;
+      const double* P = bdn + tid * nn;
       for (int n = 0; n < nn; ++n) s += P[n];
       bd[tid] = s;
       bsum[tid] = mbc[36 + tid] + s;   // the B_lin + B_drag of every bin's Z (same sum as before)

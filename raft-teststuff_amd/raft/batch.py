@@ -159,9 +159,58 @@ class DesignBatch:
 
     def solve(self, design_idx, cases, tol=0.01, want=("psd", "std", "zeta", "B_drag"), prepared=None):
         """Drag fixed point + response of every case in one device call.  Returns the
-        BatchResult (device tensors, stream-ordered): Xi [n,6,nw], iters, status, ..."""
-        cs = cases if isinstance(cases, CaseSet) else self.case_set(design_idx, cases)
-        return solve_batch(self.dds, cs, self.nIter, self.XiStart, tol, want=want, prepared=prepared)
+        BatchResult (device tensors, stream-ordered): Xi [n,6,nw], iters, status, ...
+        Case dicts with wind on an operating rotor (wind_speed > 0, turbine_status
+        'operating', aeroServoMod > 0) get their design's aero-servo added mass and damping per
+        bin, as runRAFT gives each case of a parametersweep design (raft/parametersweep.py:91,
+        raft/raft_model.py:887-889): one CaseMB view per (design, distinct wind state) on the
+        design's shared node and wave tables.  Such cases need the full design models
+        (native=False, light=False): the rotors are built there."""
+        if isinstance(cases, CaseSet):
+            return solve_batch(self.dds, cases, self.nIter, self.XiStart, tol, want=want, prepared=prepared)
+        cs = self.case_set(design_idx, cases)
+        aero = self._aero_views(np.asarray(design_idx, dtype=np.int64), cases)
+        if aero is None:
+            return solve_batch(self.dds, cs, self.nIter, self.XiStart, tol, want=want, prepared=prepared)
+        views, idx = aero
+        cs = CaseSet(idx, cs.heading, cs.spectrum, cs.Hs, cs.Tp, cs.gamma)
+        return solve_batch(views, cs, self.nIter, self.XiStart, tol, want=want)
+
+    _WAVE_KEYS = ("wave_spectrum", "wave_period", "wave_height", "wave_heading", "wave_gamma", "iCase")
+
+    def _aero_views(self, design_idx, cases):
+        """(views, per-case view index) when some case has an operating rotor, else None."""
+        import torch
+        from .model import CaseMB
+        from .prep import linear_matrices
+        hot = [i for i, c in enumerate(cases) if not isinstance(self.fowts[int(design_idx[i])], HostDesign)
+               and Model._operating_rotor(self.fowts[int(design_idx[i])], c)]
+        if not hot:
+            for i, c in enumerate(cases):
+                if get_from_dict(c, "wind_speed", shape=0, default=0.0) > 0 and \
+                        isinstance(self.fowts[int(design_idx[i])], HostDesign):
+                    raise NotImplementedError("DesignBatch: cases with wind need the full design models "
+                                              "(native=False, light=False) to build the rotors")
+            return None
+        views = list(self.dds)
+        idx = design_idx.astype(np.int32).copy()
+        made = {}
+        heads = np.unique([float(np.atleast_1d(c.get("wave_heading", 0))[0]) for c in cases]) * np.pi / 180.0
+        for i in hot:
+            d = int(design_idx[i])
+            c = cases[i]
+            key = (d, tuple(sorted((k, str(v)) for k, v in c.items() if k not in self._WAVE_KEYS)))
+            if key not in made:
+                fowt = self.fowts[d]
+                fowt.calcTurbineConstants(dict(c), ptfm_pitch=0)
+                M, B, _, _ = linear_matrices(fowt)
+                fowt.calcTurbineConstants(dict(c, wind_speed=0.0), ptfm_pitch=0)     # back to the aero-free design
+                f64 = dict(dtype=torch.float64, device=self.dds[d].device)
+                self.dds[d].ensure_headings(heads)
+                views.append(CaseMB(self.dds[d], torch.tensor(M, **f64).contiguous(), torch.tensor(B, **f64).contiguous()))
+                made[key] = len(views) - 1
+            idx[i] = made[key]
+        return views, idx
 
 
 def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, pool=None, chunks=4, tol=0.01,

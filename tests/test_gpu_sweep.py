@@ -240,3 +240,27 @@ def test_pipelined_sweep_equals_one_batch():
     for k in ("Xi", "iters", "status", "std", "psd"):
         assert torch.equal(out[k], ref[k]), k
         assert torch.equal(out2[k], ref[k]), k
+
+
+def test_design_batch_with_operating_rotor():
+    """Operating rotors in a design batch: two designs (the reference's VolturnUS-S test design
+    with its IEA-15MW rotor, and a parametersweep variant of it), each with a wind-wave-current
+    case (8 m/s, tests/test_model.py:68) and a calm sea state, in ONE DesignBatch launch, against
+    each design's own Model.analyzeCasesBatch (its per-case aero added mass and damping):
+    the same bits and iteration counts."""
+    from raft.batch import DesignBatch
+    from raft.sweep import sweep_variant
+    from test_mooring import CASES
+    base = load_design("VolturnUS-S_aero")
+    designs = [base, sweep_variant(base, [1.1, 0.9, 1.05, 1.0, 0.95])]
+    st = {"C_moor": np.diag([7e4, 7e4, 2e4, 1e7, 1e7, 1e8])}
+    wind = dict(CASES["wind_wave_current"])
+    calm = dict(wave_spectrum="JONSWAP", wave_period=9.0, wave_height=3.0, wave_heading=0.0, wave_gamma=0.0,
+                wind_speed=0)
+    B = DesignBatch(designs, statics=st)
+    res = B.solve([0, 0, 1, 1], [wind, calm, wind, calm], want=("std",)).host()
+    for d in range(2):
+        ref = B.models[d].analyzeCasesBatch([wind, calm], want=("std",))     # the same prepared design
+        np.testing.assert_array_equal(res["iters"][2 * d:2 * d + 2], ref["iters"])
+        np.testing.assert_array_equal(res["Xi"][2 * d:2 * d + 2], ref["Xi"])
+    assert not np.array_equal(res["Xi"][0], res["Xi"][2])          # the variant is another design

@@ -21,4 +21,4 @@ def test_isa_gate():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_check.py")], capture_output=True, text=True,
                        timeout=600)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
-    assert "k_solve_lds<2, 512>" in p.stdout and "FAIL" not in p.stdout
+    assert "k_solve_lds<2, 512, false>" in p.stdout and "k_solve_lds<2, 128, true>" in p.stdout and "FAIL" not in p.stdout
