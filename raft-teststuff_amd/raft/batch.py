@@ -241,6 +241,9 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
     from .solver import prepare_batch
     design_idx = np.asarray(design_idx, dtype=np.int64)
     state_idx = np.asarray(state_idx, dtype=np.int64)
+    if any(get_from_dict(c, "wind_speed", shape=0, default=0.0) > 0 for c in sea_states):
+        raise NotImplementedError("solve_sweep: sea states with wind need the rotors of the full design models; "
+                                  "use DesignBatch(designs, native=False).solve(design_idx, cases)")
     if np.any(np.diff(design_idx) < 0):
         raise ValueError("solve_sweep: cases must be design-major (non-decreasing design index)")
     nd = len(designs)
