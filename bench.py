@@ -29,7 +29,7 @@ C5_CHUNKS = 5         # C5 design blocks: block k+1 is prepared on the host whil
 PEAK_FP64 = 78.6e12   # MI355X FP64 dense peak (vector = matrix rate), FLOP/s
 # HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950
 # correction of MI355X_MICROARCH.md + WRITE_SIZE), written by tools/pmc_summary.py
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_v2", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_v3", "pmc_summary.json")
 
 
 def pmc_traffic(*kernels):
@@ -326,13 +326,13 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
                       "parallelism": f"tile-sharded x{world} + all-gather of packed pairs"},
            "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                         "frac": achieved / PEAK_FP64,
-                        "traffic": pmc_traffic("k_qtf_freq", "k_qtf_tables", "k_qtf_lcoef", "k_qtf_gemm", "k_qtf_kay"),
+                        "traffic": pmc_traffic("k_qtf_freq", "k_qtf_tables", "k_qtf_lcoef", "k_qtf_gemm", "k_qtf_kay", "k_qtf_kay_sum"),
                         "kernel": "rh_qtf_slender%s: k_qtf_freq, k_qtf_tables, k_qtf_lcoef, k_qtf_gemm, k_qtf_kay (second "
                                   "stream), k_qtf_kay_sum (every launch of a QTF on this rank)" % ("_rows" if world > 1 else ""),
                         "kernel_ms": ms, "flops_per_pair": fpp, "pairs_this_rank": mine,
                         "note": "FP64: the pair sum as MFMA GEMMs (k_qtf_gemm) + VALU Kim & Yue epilogue (DESIGN.md "
                                 "§4); peak = MI355X FP64 dense (matrix = vector rate); algorithmic FLOPs from SURVEY.md "
-                                "§8(d) over this rank's pairs; traffic = HBM bytes of all five launches of a QTF (PMC)"}}
+                                "§8(d) over this rank's pairs; traffic = HBM bytes of all six launches of a QTF (PMC)"}}
     return out
 
 
