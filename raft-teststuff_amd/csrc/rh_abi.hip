@@ -352,9 +352,9 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
 #define RH_SMALL_GRID_128 0
 #endif
     // Opt-in (-DRH_SMALL_GRID_128=1), measured and not kept: nw <= 256 on 128
-    // threads x 2 bins (x 1 bin for nw <= 128), node-serial B_drag (rh_solve.hip), four cases per
-    // CU while a workgroup's LDS stays within 40 KB.  Parity-green; C4 0.73 ms against 0.59 ms
-    // for 256 threads x 1 bin.  The kernel depends on nw only, never on the batch's node counts,
+    // threads x 2 bins (x 1 bin for nw <= 128), B_drag summed without the per-node image
+    // (rh_solve.hip), four cases per CU while a workgroup's LDS stays within 40 KB.  Parity-green;
+    // C4 0.598 ms against 0.585 ms for 256 threads x 1 bin.  The kernel depends on nw only, never on the batch's node counts,
     // so the bits of a case do not depend on which designs share its launch.
     if (RH_SMALL_GRID_128 && nw <= rh::kLT / 2) {
       const int nb128 = nw <= rh::kLT / 4 ? 1 : 2;

@@ -163,14 +163,6 @@ __device__ __forceinline__ double wave_sum63(double v) {
   return v;
 }
 
-// A pointer made wave-uniform (SGPRs), so that loads through the constant address space become
-// scalar loads.
-__device__ __forceinline__ const double* uniform_ptr(const double* p) {
-  const unsigned long long v = (unsigned long long)p;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-  return (const double*)(((unsigned long long)hi << 32) | lo);
-}
-
 // One entry of translateMatrix3to6DOF by block: 0 = Bm[r][c], 1 = (Bm H)[r][c] (the upper-right
 // block; the lower-left one is its transpose), 2 = (H Bm H^T)[r][c]; the expressions of t3to6
 // (rh_kernels.hip), evaluated for all three and selected, so no lane branches.
@@ -201,7 +193,7 @@ __device__ __forceinline__ double t3to6_block(const double* Bm, double rx, doubl
 __host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB, int LT = kLT, bool ser = false) {
   const int LW = LT / 64;
   return sizeof(double) * ((size_t)12 * LT * NB      // XiLast [6][512 NB] complex
-                           + (size_t)nn * 3 * LW     // per-wave node sums
+                           + (size_t)(ser && nn * 3 * LW < 27 ? 27 : nn * 3 * LW)   // per-wave node sums (SER: >= 27 entries)
                            + (ser ? (size_t)0 : (size_t)nn * 36)   // per-node B_drag contributions
                            + (size_t)nn * 9           // Bmat
                            + (size_t)nn * 5           // member-factored drag coefficients
@@ -239,7 +231,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   constexpr int NWP = LT * NB;                    // padded bins held in LDS
   cd* xl = reinterpret_cast<cd*>(smem);            // [6][NWP]
   double* red = smem + 12 * NWP;                   // [nn*3][LW]
-  double* bm = red + nn * 3 * LW;                 // [nn][9]
+  double* bm = red + (SER && nn * 3 * LW < 27 ? 27 : nn * 3 * LW);   // [nn][9]
   double* al = bm + nn * 9;                        // [nn][5]
   double* bd = al + nn * 5;                        // [36]
   double* mbc = bd + 36;                           // [108] M, B_lin, C
@@ -473,25 +465,43 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     }
     __syncthreads();
     if (SER) {
-      // B_drag without the per-node image: lane e < 27 sums one of the 27 distinct entries of
-      // translateMatrix3to6DOF (9 of Bm, 9 of Bm H, 9 of H Bm H^T; the lower-left block is the
-      // transpose of the upper-right one) over the nodes in node order, each entry computed
-      // with t3to6's expressions (the same bits as the image path).  Node coordinates are
-      // wave-uniform: scalar loads.
+      // B_drag without the per-node image: the 27 distinct entries of translateMatrix3to6DOF (9 of
+      // Bm, 9 of Bm H, 9 of H Bm H^T; the lower-left block is the transpose of the upper-right
+      // one) of cn nodes at a time go to the node-sum buffer (free after the Bmat loop above), all
+      // threads computing them with t3to6's expressions; lane e < 27 then adds entry e of those
+      // nodes to its running sum in node order (the same bits as the image path).
+      const int cn = (nn * 3 * LW) / 27 > 0 ? (nn * 3 * LW) / 27 : 1;
+      double se = 0.0;
+      for (int n0 = 0; n0 < nn; n0 += cn) {
+        const int cnt = nn - n0 < cn ? nn - n0 : cn;
+        for (int kb = tid; kb < 27 * cnt; kb += 3 * LT) {   // three entries per thread in flight
+          double rx[3], ry[3], rz[3];
+          int kk[3];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            kk[i] = kb + i * LT < 27 * cnt ? kb + i * LT : 27 * cnt - 1;
+            const int n = n0 + kk[i] / 27;
+            rx[i] = nf(node, nn, RH_NF_XX, n);
+            ry[i] = nf(node, nn, RH_NF_XY, n);
+            rz[i] = nf(node, nn, RH_NF_XZ, n);
+          }
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const int k = kk[i], e = k % 27;
+            const double v = t3to6_block(bm + 9 * (n0 + k / 27), rx[i], ry[i], rz[i], e / 9, (e % 9) / 3, e % 3);
+            if (kb + i * LT < 27 * cnt) red[k] = v;
+          }
+        }
+        __syncthreads();
+        if (tid < 27)
+          for (int k = 0; k < cnt; ++k) se += red[27 * k + tid];
+        __syncthreads();
+      }
       if (tid < 27) {
         const int blk = tid / 9, r = (tid % 9) / 3, c = tid % 3;
-        const f64_kp nodeU = (f64_kp)uniform_ptr(node);
-        double s = 0;
-        for (int n = 0; n < nn; ++n) {
-          const double* Bm = bm + 9 * n;
-          const double rx = nodeU[RH_NF_XX * nn + n], ry = nodeU[RH_NF_XY * nn + n], rz = nodeU[RH_NF_XZ * nn + n];
-          double v = t3to6_block(Bm, rx, ry, rz, blk, r, c);
-          asm volatile("" : "+v"(v));   // an entry is rounded before it is added (as through LDS)
-          s += v;
-        }
-        if (blk == 0) bd[6 * r + c] = s;
-        else if (blk == 1) bd[6 * r + 3 + c] = bd[6 * (3 + c) + r] = s;
-        else bd[6 * (3 + r) + 3 + c] = s;
+        if (blk == 0) bd[6 * r + c] = se;
+        else if (blk == 1) bd[6 * r + 3 + c] = bd[6 * (3 + c) + r] = se;
+        else bd[6 * (3 + r) + 3 + c] = se;
       }
       __syncthreads();
       if (tid < 36) bsum[tid] = mbc[36 + tid] + bd[tid];
