@@ -282,8 +282,17 @@ class Model:
                 F_env[6 * i:6 * i + 6] = np.sum(fowt.f_aero0, axis=1) + fowt.calcCurrentLoads(ci)
                 if getattr(fowt, "Fhydro_2nd_mean", None) is not None:
                     F_env[6 * i:6 * i + 6] += np.sum(fowt.Fhydro_2nd_mean, axis=0)
-        if case and self.mooring_currentMod > 0 and get_from_dict(case, "current_speed", shape=0, default=0.0) > 0:
-            raise NotImplementedError("current loads on mooring lines (mooring currentMod > 0)")
+        # uniform current on the mooring lines (raft/raft_model.py:561-577): set for this case,
+        # cleared otherwise, on the array system and every FOWT's own system
+        cur = np.zeros(3)
+        if case and self.mooring_currentMod > 0:
+            speed = get_from_dict(case, "current_speed", shape=0, default=0.0)
+            head = get_from_dict(case, "current_heading", shape=0, default=0)
+            if speed > 0:
+                cur = np.array([speed * np.cos(np.radians(head)), speed * np.sin(np.radians(head)), 0.0])
+        for sysm in [self.ms] + [fowt.ms for fowt in self.fowtList]:
+            if sysm is not None:
+                sysm.current = cur.copy()
         tols = np.array([0.05, 0.05, 0.05, 0.005, 0.005, 0.005] * len(self.fowtList))
 
         def eval_func(X, args):

@@ -171,30 +171,67 @@ class Line:
         self.KA = self.KB = self.KAB = np.zeros([3, 3])
         self.TA = self.TB = 0.0
 
-    def static_solve(self, depth, tol=1e-6):
+    def current_load(self, U, rho=RHO):
+        """Mean drag of a uniform current U on the line, per unit (unstretched) length, on the
+        straight chord between its ends: transverse 0.5 rho d Cd |Un| Un plus tangential
+        0.5 rho pi d CdAx |Ut| Ut (the MoorDyn drag convention of the line-type table).
+        MoorPy's currentMod = 1 (raft/raft_model.py:561-577) applies a current this way; its
+        exact form is not visible from the reference, so this is parity unpinned."""
+        U = np.asarray(U, dtype=float)
+        if not np.any(U):
+            return np.zeros(3)
+        d = self.pB.r - self.pA.r
+        n = np.linalg.norm(d)
+        q = d / n if n > 0 else np.array([0.0, 0.0, 1.0])
+        Ut = np.dot(U, q) * q
+        Un = U - Ut
+        dia = self.type["d"]
+        return (0.5 * rho * dia * self.type.get("Cd", 0.0) * np.linalg.norm(Un) * Un
+                + 0.5 * rho * math.pi * dia * self.type.get("CdAx", 0.0) * np.linalg.norm(Ut) * Ut)
+
+    def static_solve(self, depth, tol=1e-6, current=None, rho=RHO):
         """End forces and 3-D end stiffness for the current end positions.  The catenary is
         solved from the lower end (anchor side) to the upper end; the forces on the ends are
         the line's pull: the upper end toward the lower one and down, the lower end toward
-        the upper one (zero vertical force where the line rests on the seabed)."""
+        the upper one (zero vertical force where the line rests on the seabed).
+        With a uniform `current`, the distributed load is the wet weight plus the line's
+        current drag (current_load); the catenary is solved in the frame whose -z axis is that
+        load's direction, with the same seabed-contact rule (the seabed plane then taken
+        normal to the load through the lower end), and forces and stiffness are rotated back.
+        Zero current gives the plain solve bit for bit."""
         swap = self.pB.r[2] < self.pA.r[2]
         lower, upper = (self.pB, self.pA) if swap else (self.pA, self.pB)
         d = upper.r - lower.r
+        W = self.type["w"]
+        R = None
+        if current is not None and np.any(current):
+            f = np.array([0.0, 0.0, -W]) + self.current_load(current, rho)
+            W = float(np.linalg.norm(f))
+            a = f / W                                  # load direction -> (0, 0, -1)
+            v = np.array([a[1] * -1.0 - a[2] * 0.0, a[2] * 0.0 - a[0] * -1.0, 0.0])   # a x (0, 0, -1)
+            cth = -a[2]
+            V = np.array([[0.0, -v[2], v[1]], [v[2], 0.0, -v[0]], [-v[1], v[0], 0.0]])
+            R = np.eye(3) + V + V @ V / (1.0 + cth)   # Rodrigues: R a = (0, 0, -1)
+            d = R @ d
         LH = math.hypot(d[0], d[1])
         c, s = (d[0] / LH, d[1] / LH) if LH > 0 else (0.0, 0.0)
         CB = -depth - lower.r[2] if lower.r[2] > -depth else 0.0    # off the seabed: no contact
-        HA, VA, HF, VF, K2 = catenary(LH, d[2], self.L, self.type["EA"], self.type["w"], CB=CB,
+        HA, VA, HF, VF, K2 = catenary(LH, d[2], self.L, self.type["EA"], W, CB=CB,
                                        HF0=self.HF, VF0=self.VF, Tol=tol)
         self.HF, self.VF = HF, VF
         f_up = np.array([-HF * c, -HF * s, -VF])
         f_lo = np.array([HA * c, HA * s, VA])
-        self.fA, self.fB = (f_up, f_lo) if swap else (f_lo, f_up)
-        self.TA = float(np.linalg.norm(self.fA))
-        self.TB = float(np.linalg.norm(self.fB))
         Kt = HF / LH if LH > 0 else 0.0                          # transverse (geometric) stiffness
         Kxx, Kxz, Kzx, Kzz = K2[0, 0], K2[0, 1], K2[1, 0], K2[1, 1]
         Ku = np.array([[c * c * Kxx + s * s * Kt, c * s * (Kxx - Kt), c * Kxz],
                        [c * s * (Kxx - Kt), s * s * Kxx + c * c * Kt, s * Kxz],
                        [c * Kzx, s * Kzx, Kzz]])
+        if R is not None:                                        # back to the global frame
+            f_up, f_lo = R.T @ f_up, R.T @ f_lo
+            Ku = R.T @ Ku @ R
+        self.fA, self.fB = (f_up, f_lo) if swap else (f_lo, f_up)
+        self.TA = float(np.linalg.norm(self.fA))
+        self.TB = float(np.linalg.norm(self.fB))
         # the end forces depend on the end separation only (line weight and, for a fixed
         # anchor, the seabed reaction aside): both ends see Ku, the cross term is -Ku
         self.KA = Ku
@@ -227,13 +264,15 @@ class MooringSystem:
         self.cat_tol = cat_tol            # relative tolerance of the catenary solves
         self.free_tol = 0.05              # free-point equilibrium step tolerance [m]
         self.rho, self.g = rho, g
+        self.current = np.zeros(3)        # uniform current [m/s] on the lines (MoorPy currentMod 1)
         self.points, self.lines, self.bodies = [], [], []
         self.line_types = {}
 
     # ----------------------------------------------------------------- construction
-    def add_line_type(self, name, d, m, EA):
+    def add_line_type(self, name, d, m, EA, Cd=0.0, CdAx=0.0):
         w = (m - self.rho * math.pi / 4.0 * d * d) * self.g       # wet weight per length
-        self.line_types[name] = dict(name=name, d=float(d), m=float(m), EA=float(EA), w=w)
+        self.line_types[name] = dict(name=name, d=float(d), m=float(m), EA=float(EA), w=w, Cd=float(Cd),
+                                     CdAx=float(CdAx))
 
     def add_point(self, ptype, r, m=0.0, v=0.0):
         p = Point(len(self.points) + 1, ptype, r, m, v)
@@ -258,7 +297,8 @@ class MooringSystem:
         coupled body at the origin carrying the 'vessel' points (raft/raft_fowt.py:166-186)."""
         ms = cls(depth=float(d["water_depth"]))
         for lt in d.get("line_types", []):
-            ms.add_line_type(lt["name"], float(lt["diameter"]), float(lt["mass_density"]), float(lt["stiffness"]))
+            ms.add_line_type(lt["name"], float(lt["diameter"]), float(lt["mass_density"]), float(lt["stiffness"]),
+                             float(lt.get("transverse_drag", 0.0)), float(lt.get("tangential_drag", 0.0)))
         body = ms.add_body(np.zeros(6))
         names = {}
         for pd in d.get("points", []):
@@ -293,8 +333,9 @@ class MooringSystem:
                            "lines" if "LINES" in up else "options" if "OPTIONS" in up else "other")
                 continue
             tok = s.split()
-            if section == "types" and len(tok) >= 4 and _isnum(tok[1]):
-                self.add_line_type(tok[0], float(tok[1]), float(tok[2]), float(tok[3]))
+            if section == "types" and len(tok) >= 4 and _isnum(tok[1]):   # Name Diam Mass/m EA BA EI Cd Ca CdAx CaAx
+                self.add_line_type(tok[0], float(tok[1]), float(tok[2]), float(tok[3]),
+                                   float(tok[6]) if len(tok) > 6 else 0.0, float(tok[8]) if len(tok) > 8 else 0.0)
             elif section == "points" and len(tok) >= 5 and _isnum(tok[0]):
                 att = tok[1].lower()
                 r = np.array([float(tok[2]), float(tok[3]), float(tok[4])])
@@ -333,8 +374,9 @@ class MooringSystem:
 
     # ----------------------------------------------------------------- statics
     def _solve_lines(self):
+        cur = self.current if np.any(self.current) else None
         for ln in self.lines:
-            ln.static_solve(self.depth, self.cat_tol)
+            ln.static_solve(self.depth, self.cat_tol, cur, self.rho)
 
     def point_force(self, p, lines_only=False):
         f = np.zeros(3)

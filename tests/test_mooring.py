@@ -155,3 +155,113 @@ def test_analytic_stiffness_is_the_derivative_at_zero_rotation(index):
     Ka = ms.coupled_stiffness_analytic()
     Kf = ms.coupled_stiffness_fd(dx=1e-3, dth=1e-5)
     assert np.abs(Ka - Kf).max() <= 1e-5 * np.abs(Ka).max(), np.abs(Ka - Kf).max() / np.abs(Ka).max()
+
+
+# ------------------------------------------------------------------ current loads on the lines
+# mooring currentMod = 1 (raft/raft_model.py:561-577).  No design or expectation of the reference
+# uses it, so these tests pin the restatement's own physics, not MoorPy ("parity unpinned").
+def _suspended_line(Cd=1.6, CdAx=0.1):
+    from raft.mooring import MooringSystem, Point
+    ms = MooringSystem(depth=200.0)
+    ms.add_line_type("chain", 0.185, 685.0, 3270e6, Cd, CdAx)
+    a = ms.add_point(Point.FIXED, [0.0, 0.0, -150.0])
+    b = ms.add_point(Point.FIXED, [300.0, 40.0, -14.0])
+    ln = ms.add_line(360.0, "chain", a, b)
+    return ms, ln
+
+
+def _shooting_end_forces(ln, f, T0):
+    """The continuous elastic line under a constant distributed load f [N/m] of unstretched
+    length, solved by shooting: tension T(s) = T0 - f s, dr/ds = (1 + |T|/EA) T/|T|, r(L) = rB,
+    integrated by 400-point Gauss-Legendre; returns the line's forces on ends A and B."""
+    from scipy.optimize import fsolve
+    rA, rB = ln.pA.r, ln.pB.r
+    EA, L = ln.type["EA"], ln.L
+    x, wq = np.polynomial.legendre.leggauss(400)
+    s = 0.5 * L * (x + 1.0)
+
+    def end(T0_):
+        T = T0_[None, :] - f[None, :] * s[:, None]
+        n = np.linalg.norm(T, axis=1)
+        return rA + 0.5 * L * np.sum(wq[:, None] * (1.0 + n / EA)[:, None] * T / n[:, None], axis=0)
+
+    sc = np.linalg.norm(T0)
+    sol = fsolve(lambda t: (end(t * sc) - rB) / L, T0 / sc, xtol=1e-13, full_output=True)
+    T0 = sol[0] * sc
+    assert np.abs(end(T0) - rB).max() < 1e-8 * L
+    return T0, -(T0 - f * L)
+
+
+def test_line_current_zero_is_the_plain_solve():
+    ms, ln = _suspended_line()
+    ln.static_solve(ms.depth, 1e-8)
+    f0, K0 = (ln.fA.copy(), ln.fB.copy()), ln.KA.copy()
+    ln.HF = ln.VF = 0.0
+    ln.static_solve(ms.depth, 1e-8, np.zeros(3))
+    assert np.array_equal(ln.fA, f0[0]) and np.array_equal(ln.fB, f0[1]) and np.array_equal(ln.KA, K0)
+
+
+@pytest.mark.parametrize("U", [[1.0, 0.0, 0.0], [0.3, -0.9, 0.0], [0.0, 1.5, 0.0]])
+def test_line_current_force_balance_and_lumped_mass(U):
+    """A suspended line under weight + current drag: the end forces balance the whole distributed
+    load, and match an independent shooting solve of the continuous elastic line under the same
+    constant load (the rotated-frame catenary is exact for it)."""
+    ms, ln = _suspended_line()
+    U = np.array(U)
+    f = np.array([0.0, 0.0, -ln.type["w"]]) + ln.current_load(U, ms.rho)
+    ln.static_solve(ms.depth, 1e-10, U, ms.rho)
+    assert np.allclose(ln.fA + ln.fB, f * ln.L, rtol=1e-8, atol=1e-6 * np.linalg.norm(f) * ln.L)
+    fA, fB = _shooting_end_forces(ln, f, ln.fA * 1.05)
+    T = np.linalg.norm(ln.fB)
+    assert np.abs(ln.fA - fA).max() < 1e-7 * T and np.abs(ln.fB - fB).max() < 1e-7 * T
+    # the drag is transverse-dominated and points downstream
+    fc = ln.current_load(U, ms.rho)
+    assert np.dot(fc, U) > 0
+
+
+def test_line_current_stiffness_matches_differences():
+    """End stiffness of the rotated solve against central differences of its end forces (the
+    current load held at the base geometry's value, as the analytic stiffness assumes)."""
+    ms, ln = _suspended_line()
+    U = np.array([0.8, 0.4, 0.0])
+    ln.static_solve(ms.depth, 1e-12, U, ms.rho)
+    K = ln.KB.copy()
+    fc = ln.current_load(U, ms.rho)
+    r0 = ln.pB.r.copy()
+    h = 1e-3
+    for j in range(3):
+        fs = []
+        for sgn in (1.0, -1.0):
+            ln.pB.r = r0.copy()
+            ln.pB.r[j] += sgn * h
+            ln.HF = ln.VF = 0.0
+            ln.current_load = lambda U_, rho=ms.rho: fc       # freeze the drag at the base chord
+            ln.static_solve(ms.depth, 1e-12, U, ms.rho)
+            fs.append(ln.fB.copy())
+        col = -(fs[0] - fs[1]) / (2 * h)
+        assert np.allclose(K[:, j], col, rtol=2e-4, atol=2e-4 * np.abs(K).max()), (j, K[:, j], col)
+    del ln.current_load
+    ln.pB.r = r0
+
+
+def test_mooring_current_moves_the_platform_downstream():
+    """VolturnUS-S with mooring currentMod = 1 in the reference's current case: the line drag
+    adds to the hull's current load, so the mean offset moves further downstream (heading 15°),
+    and the system stays solvable (natural frequencies finite and positive)."""
+    import raft
+    d = load_design(DESIGNS[0])
+    base = raft.Model(d)
+    base.solveStatics(dict(CASES["current"]))
+    X0 = np.array(base.fowtList[0].r6)
+    d["mooring"]["currentMod"] = 1
+    m = raft.Model(d)
+    m.solveStatics(dict(CASES["current"]))
+    X1 = np.array(m.fowtList[0].r6)
+    u = np.array([np.cos(np.radians(15)), np.sin(np.radians(15))])
+    assert np.dot(X1[:2] - X0[:2], u) > 0.05          # metres further downstream
+    assert np.linalg.norm(X1[:2] - X0[:2]) < 0.5 * np.linalg.norm(X0[:2])
+    fns, _ = m.solveEigen()
+    assert np.all(np.isfinite(fns)) and np.all(fns > 0)
+    # a calm case afterwards clears the current (the reference resets currentMod per case)
+    m.solveStatics(dict(CASES["wave"]))
+    assert not np.any(m.fowtList[0].ms.current)
