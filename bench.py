@@ -78,7 +78,7 @@ def pmc_l2(kernel, kernel_ms):
 def solve_kernel_name(nw):
     """The kernel rh_solve_cases launches for this grid (dispatch in rh_abi.hip)."""
     if nw <= 256:
-        return "rh::k_solve_lds<1, 256, false>"
+        return f"rh::k_solve_lds<{1 if nw <= 128 else 2}, 128, true>"
     if nw <= 1024:
         return f"rh::k_solve_lds<{1 if nw <= 512 else 2}, 512, false>"
     return "rh::k_solve_cases<4>"

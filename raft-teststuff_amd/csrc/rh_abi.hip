@@ -349,12 +349,12 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case (256 for nw <= 256), nw <= 1024.
   if (nw <= 2 * rh::kLT && !ctx->force_general) {
 #ifndef RH_SMALL_GRID_128
-#define RH_SMALL_GRID_128 0
+#define RH_SMALL_GRID_128 1
 #endif
-    // Opt-in (-DRH_SMALL_GRID_128=1), measured and not kept: nw <= 256 on 128
-    // threads x 2 bins (x 1 bin for nw <= 128), B_drag summed without the per-node image
-    // (rh_solve.hip), four cases per CU while a workgroup's LDS stays within 40 KB.  Parity-green;
-    // C4 0.598 ms against 0.585 ms for 256 threads x 1 bin.  The kernel depends on nw only, never on the batch's node counts,
+    // nw <= 256 on 128 threads x 2 bins (x 1 bin for nw <= 128), B_drag summed without the
+    // per-node image (rh_solve.hip), four cases per CU while a workgroup's LDS stays within
+    // 40 KB: C4 0.544-0.554 ms against 0.586-0.590 ms for 256 threads x 1 bin
+    // (-DRH_SMALL_GRID_128=0).  The kernel depends on nw only, never on the batch's node counts,
     // so the bits of a case do not depend on which designs share its launch.
     if (RH_SMALL_GRID_128 && nw <= rh::kLT / 2) {
       const int nb128 = nw <= rh::kLT / 4 ? 1 : 2;

@@ -467,30 +467,21 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     if (SER) {
       // B_drag without the per-node image: the 27 distinct entries of translateMatrix3to6DOF (9 of
       // Bm, 9 of Bm H, 9 of H Bm H^T; the lower-left block is the transpose of the upper-right
-      // one) of cn nodes at a time go to the node-sum buffer (free after the Bmat loop above), all
-      // threads computing them with t3to6's expressions; lane e < 27 then adds entry e of those
-      // nodes to its running sum in node order (the same bits as the image path).
+      // one) of cn nodes at a time go to the node-sum buffer (free after the Bmat loop above), one
+      // thread per node computing them with t3to6's expressions; lane e < 27 then adds entry e of
+      // those nodes to its running sum in node order (the same bits as the image path).
       const int cn = (nn * 3 * LW) / 27 > 0 ? (nn * 3 * LW) / 27 : 1;
       double se = 0.0;
       for (int n0 = 0; n0 < nn; n0 += cn) {
         const int cnt = nn - n0 < cn ? nn - n0 : cn;
-        for (int kb = tid; kb < 27 * cnt; kb += 3 * LT) {   // three entries per thread in flight
-          double rx[3], ry[3], rz[3];
-          int kk[3];
+        for (int nl = tid; nl < cnt; nl += LT) {   // one node per thread: its 27 entries share the loads
+          const int n = n0 + nl;
+          const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
+          double Bn[9];
 #pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            kk[i] = kb + i * LT < 27 * cnt ? kb + i * LT : 27 * cnt - 1;
-            const int n = n0 + kk[i] / 27;
-            rx[i] = nf(node, nn, RH_NF_XX, n);
-            ry[i] = nf(node, nn, RH_NF_XY, n);
-            rz[i] = nf(node, nn, RH_NF_XZ, n);
-          }
+          for (int k = 0; k < 9; ++k) Bn[k] = bm[9 * n + k];
 #pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            const int k = kk[i], e = k % 27;
-            const double v = t3to6_block(bm + 9 * (n0 + k / 27), rx[i], ry[i], rz[i], e / 9, (e % 9) / 3, e % 3);
-            if (kb + i * LT < 27 * cnt) red[k] = v;
-          }
+          for (int e = 0; e < 27; ++e) red[27 * nl + e] = t3to6_block(Bn, rx, ry, rz, e / 9, (e % 9) / 3, e % 3);
         }
         __syncthreads();
         if (tid < 27)

@@ -350,7 +350,7 @@ def test_margin_output_and_knobs():
 def test_pair_kernel_odd_grids(nw):
     """Grids that leave pad lanes: nw not a multiple of 64 (every block size), odd nw (a lane
     pair of k_solve_pair with one real and one pad bin), nw just past a block size (whole pad
-    waves).  The default kernel (k_solve_lds, including its <1, 256> form) against the general
+    waves).  The default kernel (k_solve_lds, including its 128-thread form) against the general
     kernel k_solve_cases and the lane-pair kernel k_solve_pair on the same batch: identical
     iteration counts and statuses, Xi within 1e-12."""
     from raft import _native as N

@@ -5,7 +5,7 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
-for wl in solve c4 qtf; do
+for wl in ${WLS:-solve c4 qtf}; do
   case $wl in
     solve) cmd="$R/tools/ubench/time_solve.py pmc" ;;
     c4) cmd="$R/tools/ubench/time_c4.py 3" ;;
@@ -29,7 +29,11 @@ cd $R
 python - <<'PY'
 import json, subprocess, sys
 out = {}
-for wl in ("solve", "c4", "qtf"):
+import os
+prev = os.environ.get("PMC_BASE")
+if prev:
+    out.update(json.load(open(prev)))
+for wl in os.environ.get("WLS", "solve c4 qtf").split():
     r = subprocess.run([sys.executable, "tools/pmc_summary.py", f"gpurun_out/pmc_{wl}"], capture_output=True, text=True, check=True)
     out.update(json.loads(r.stdout))
 json.dump(out, open("gpurun_out/pmc_summary.json", "w"), indent=1)
