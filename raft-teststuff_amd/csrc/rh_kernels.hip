@@ -82,7 +82,88 @@ __global__ __launch_bounds__(256) void k_sea_state(int nw, const double* __restr
 // order, so F is bitwise the node-serial sum.  kWtN times the waves of a thread-per-bin
 // loop: one design's tables (1000 bins) are 128 waves instead of 16.
 // ----------------------------------------------------------------------------------------
-constexpr int kWtN = 8;
+#ifndef RH_WTN
+#define RH_WTN 8
+#endif
+constexpr int kWtN = RH_WTN;
+
+// One (heading, node, bin): the unit-amplitude Airy velocity uhat and its member-axis
+// projections kproj (stored when okb), and the node's inertial-excitation contribution
+// f6 = [f; r x f] (raft/raft_fowt.py:1113-1124).
+__device__ __forceinline__ void wave_node(const rh_design& d, int h, int n, int b, bool okb, double w, double k,
+                                          double cb, double sb, rh_c128* __restrict__ uhat,
+                                          rh_c128* __restrict__ kproj, cd (&f6)[6]) {
+  const int nw = d.nw, nn = d.nn;
+  const double hd = d.depth;
+  const double* node = d.node;
+  const double x = nf(node, nn, RH_NF_RX, n), y = nf(node, nn, RH_NF_RY, n), z = nf(node, nn, RH_NF_RZ, n);
+  const double th = k * (cb * x + sb * y);
+  const cd e = mk(cos(th), -sin(th));      // exp(-1j*th)
+  double s_sh, c_sh, c_ch;
+  if (k * hd > 89.4) {                     // deep-water switch (raft/helpers.py:133-136)
+    const double ez = exp(k * z);
+    s_sh = ez;
+    c_sh = ez;
+    c_ch = ez + exp(-k * (z + 2.0 * hd));
+  } else {
+    const double skh = sinh(k * hd);
+    s_sh = sinh(k * (z + hd)) / skh;
+    c_sh = cosh(k * (z + hd)) / skh;
+    c_ch = cosh(k * (z + hd)) / cosh(k * hd);
+  }
+  const cd we = scl(e, w);
+  const cd u0 = scl(scl(we, c_sh), cb);
+  const cd u1 = scl(scl(we, c_sh), sb);
+  const cd u2 = scl(iw(w, e), s_sh);
+  rh_c128* U = uhat + ((size_t)(h * nn + n) * 3) * nw + b;
+  if (okb) {
+    st(U, u0);
+    st(U + nw, u1);
+    st(U + 2 * nw, u2);
+  }
+  {  // projections on the member axes: the drag loop's only view of the wave field
+    rh_c128* K = kproj + ((size_t)(h * nn + n) * 3) * nw + b;
+    const int fo[3] = {RH_NF_QX, RH_NF_P1X, RH_NF_P2X};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const double e0 = nf(node, nn, fo[a], n), e1 = nf(node, nn, fo[a] + 1, n), e2 = nf(node, nn, fo[a] + 2, n);
+      if (okb) st(K + a * nw, add(add(scl(u0, e0), scl(u1, e1)), scl(u2, e2)));
+    }
+  }
+  // inertial excitation: Imat ud + pDyn a_i q, ud = i w u  (raft/raft_fowt.py:1113-1124)
+  const cd ud[3] = {iw(w, u0), iw(w, u1), iw(w, u2)};
+  const cd pd = scl(scl(e, d.pdyn_rho_g), c_ch);
+  const double ai = nf(node, nn, RH_NF_AI, n);
+  const double q[3] = {nf(node, nn, RH_NF_QX, n), nf(node, nn, RH_NF_QY, n), nf(node, nn, RH_NF_QZ, n)};
+  const cd pa = scl(pd, ai);
+  cd f[3];
+  if (nf(node, nn, RH_NF_MCF, n) != 0.0) {
+    const rh_c128* I = d.imat_mcf + (size_t)n * 9 * nw + b;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      cd s = mul(ld(I + (3 * r + 0) * nw), ud[0]);
+      s = add(s, mul(ld(I + (3 * r + 1) * nw), ud[1]));
+      s = add(s, mul(ld(I + (3 * r + 2) * nw), ud[2]));
+      f[r] = add(s, scl(pa, q[r]));
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      cd s = scl(ud[0], nf(node, nn, RH_NF_I00 + 3 * r + 0, n));
+      s = add(s, scl(ud[1], nf(node, nn, RH_NF_I00 + 3 * r + 1, n)));
+      s = add(s, scl(ud[2], nf(node, nn, RH_NF_I00 + 3 * r + 2, n)));
+      f[r] = add(s, scl(pa, q[r]));
+    }
+  }
+  const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
+  f6[0] = f[0];
+  f6[1] = f[1];
+  f6[2] = f[2];
+  f6[3] = sub(scl(f[2], ry), scl(f[1], rz));
+  f6[4] = sub(scl(f[0], rz), scl(f[2], rx));
+  f6[5] = sub(scl(f[1], rx), scl(f[0], ry));
+}
+
 __device__ __forceinline__ void wave_tables_body(const rh_design& d, const double* __restrict__ beta, int h, int bx,
                                                  rh_c128* __restrict__ uhat, rh_c128* __restrict__ finer,
                                                  rh_c128* __restrict__ kproj, cd (&fs)[kWtN][6][64]) {
@@ -91,82 +172,19 @@ __device__ __forceinline__ void wave_tables_body(const rh_design& d, const doubl
   const int b0 = bx * 64 + lb;
   const bool okb = b0 < nw;
   const int b = okb ? b0 : nw - 1;           // pad lanes compute a valid bin and store nothing
-  const double w = d.w[b], k = d.k[b], hd = d.depth;
+  const double w = d.w[b], k = d.k[b];
   const double be = beta[h];
   const double cb = cos(be), sb = sin(be);
   cd F[6];
 #pragma unroll
   for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
-  const double* node = d.node;
   for (int nb = 0; nb < nn; nb += kWtN) {
     const int n = nb + slot;
     if (n < nn) {
-      const double x = nf(node, nn, RH_NF_RX, n), y = nf(node, nn, RH_NF_RY, n), z = nf(node, nn, RH_NF_RZ, n);
-      const double th = k * (cb * x + sb * y);
-      const cd e = mk(cos(th), -sin(th));      // exp(-1j*th)
-      double s_sh, c_sh, c_ch;
-      if (k * hd > 89.4) {                     // deep-water switch (raft/helpers.py:133-136)
-        const double ez = exp(k * z);
-        s_sh = ez;
-        c_sh = ez;
-        c_ch = ez + exp(-k * (z + 2.0 * hd));
-      } else {
-        const double skh = sinh(k * hd);
-        s_sh = sinh(k * (z + hd)) / skh;
-        c_sh = cosh(k * (z + hd)) / skh;
-        c_ch = cosh(k * (z + hd)) / cosh(k * hd);
-      }
-      const cd we = scl(e, w);
-      const cd u0 = scl(scl(we, c_sh), cb);
-      const cd u1 = scl(scl(we, c_sh), sb);
-      const cd u2 = scl(iw(w, e), s_sh);
-      rh_c128* U = uhat + ((size_t)(h * nn + n) * 3) * nw + b;
-      if (okb) {
-        st(U, u0);
-        st(U + nw, u1);
-        st(U + 2 * nw, u2);
-      }
-      {  // projections on the member axes: the drag loop's only view of the wave field
-        rh_c128* K = kproj + ((size_t)(h * nn + n) * 3) * nw + b;
-        const int fo[3] = {RH_NF_QX, RH_NF_P1X, RH_NF_P2X};
+      cd f6[6];
+      wave_node(d, h, n, b, okb, w, k, cb, sb, uhat, kproj, f6);
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          const double e0 = nf(node, nn, fo[a], n), e1 = nf(node, nn, fo[a] + 1, n), e2 = nf(node, nn, fo[a] + 2, n);
-          if (okb) st(K + a * nw, add(add(scl(u0, e0), scl(u1, e1)), scl(u2, e2)));
-        }
-      }
-      // inertial excitation: Imat ud + pDyn a_i q, ud = i w u  (raft/raft_fowt.py:1113-1124)
-      const cd ud[3] = {iw(w, u0), iw(w, u1), iw(w, u2)};
-      const cd pd = scl(scl(e, d.pdyn_rho_g), c_ch);
-      const double ai = nf(node, nn, RH_NF_AI, n);
-      const double q[3] = {nf(node, nn, RH_NF_QX, n), nf(node, nn, RH_NF_QY, n), nf(node, nn, RH_NF_QZ, n)};
-      const cd pa = scl(pd, ai);
-      cd f[3];
-      if (nf(node, nn, RH_NF_MCF, n) != 0.0) {
-        const rh_c128* I = d.imat_mcf + (size_t)n * 9 * nw + b;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          cd s = mul(ld(I + (3 * r + 0) * nw), ud[0]);
-          s = add(s, mul(ld(I + (3 * r + 1) * nw), ud[1]));
-          s = add(s, mul(ld(I + (3 * r + 2) * nw), ud[2]));
-          f[r] = add(s, scl(pa, q[r]));
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          cd s = scl(ud[0], nf(node, nn, RH_NF_I00 + 3 * r + 0, n));
-          s = add(s, scl(ud[1], nf(node, nn, RH_NF_I00 + 3 * r + 1, n)));
-          s = add(s, scl(ud[2], nf(node, nn, RH_NF_I00 + 3 * r + 2, n)));
-          f[r] = add(s, scl(pa, q[r]));
-        }
-      }
-      const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
-      fs[slot][0][lb] = f[0];
-      fs[slot][1][lb] = f[1];
-      fs[slot][2][lb] = f[2];
-      fs[slot][3][lb] = sub(scl(f[2], ry), scl(f[1], rz));
-      fs[slot][4][lb] = sub(scl(f[0], rz), scl(f[2], rx));
-      fs[slot][5][lb] = sub(scl(f[1], rx), scl(f[0], ry));
+      for (int c = 0; c < 6; ++c) fs[slot][c][lb] = f6[c];
     }
     __syncthreads();
     if (slot == 0) {
@@ -181,6 +199,43 @@ __device__ __forceinline__ void wave_tables_body(const rh_design& d, const doubl
   rh_c128* Fo = finer + (size_t)h * 6 * nw + b;
 #pragma unroll
   for (int c = 0; c < 6; ++c) st(Fo + c * nw, F[c]);
+}
+
+// One design's tables with the nodes spread over the grid (rh_wave_tables): a workgroup is 64
+// bins x kWtN nodes of one heading (blockIdx.z = node group), one node per wave, and every node's
+// six force contributions go to fw[h][n][6][nw]; k_wave_force_sum then adds them in node order
+// (the same bits as wave_tables_body).  A 1000-bin, 4-heading design is 448 workgroups instead
+// of 64, which left three CUs in four idle.
+__global__ __launch_bounds__(64 * kWtN) void k_wave_tables_nodes(rh_design d, const double* __restrict__ beta,
+                                                                  rh_c128* __restrict__ uhat, rh_c128* __restrict__ kproj,
+                                                                  rh_c128* __restrict__ fw) {
+  const int lb = (int)threadIdx.x & 63, slot = (int)threadIdx.x >> 6;
+  const int nw = d.nw, nn = d.nn, h = (int)blockIdx.y;
+  const int n = (int)blockIdx.z * kWtN + slot;
+  if (n >= nn) return;                       // uniform per wave
+  const int b0 = (int)blockIdx.x * 64 + lb;
+  const bool okb = b0 < nw;
+  const int b = okb ? b0 : nw - 1;
+  const double be = beta[h];
+  cd f6[6];
+  wave_node(d, h, n, b, okb, d.w[b], d.k[b], cos(be), sin(be), uhat, kproj, f6);
+  if (!okb) return;
+  rh_c128* o = fw + ((size_t)(h * nn + n) * 6) * nw + b;
+#pragma unroll
+  for (int c = 0; c < 6; ++c) st(o + c * nw, f6[c]);
+}
+
+// finer[h][c][b] = sum over nodes, in node order, of fw[h][n][c][b]
+__global__ __launch_bounds__(256) void k_wave_force_sum(int nw, int nn, int nhead, const rh_c128* __restrict__ fw,
+                                                        rh_c128* __restrict__ finer) {
+  const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (t >= nhead * 6 * nw) return;
+  const int b = t % nw, c = (t / nw) % 6, h = t / (6 * nw);
+  const rh_c128* p = fw + ((size_t)h * nn * 6 + c) * nw + b;
+  cd F = mk(0, 0);
+#pragma unroll 4
+  for (int n = 0; n < nn; ++n) F = add(F, ld(p + (size_t)n * 6 * nw));
+  st(finer + ((size_t)h * 6 + c) * nw + b, F);
 }
 
 __global__ __launch_bounds__(64 * kWtN) void k_wave_tables(rh_design d, const double* __restrict__ beta,
