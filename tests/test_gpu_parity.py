@@ -202,6 +202,42 @@ def test_full_size_c2_batch_properties():
         assert rel(a["Xi"][ic], r["Xi"][0]) < RTOL
 
 
+def _oracle_c2_case(args):
+    """Worker of test_full_size_c2_every_case_vs_oracle (spawned process: NumPy only)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from conftest import load_golden as lg
+    from oracle import raft_oracle as Ow
+    case, = args
+    T = lg("c2_nw1000")
+    r = Ow.solve_dynamics(T, dict(case), int(T["nIter"]), float(T["XiStart"]))
+    return int(r["iters"]), np.asarray(r["Xi"][0])
+
+
+def test_full_size_c2_every_case_vs_oracle():
+    """Every one of the 512 full-size C2 cases (nw=1000) against the oracle:
+    identical iteration counts and Xi within RTOL (the oracle in a pool of spawned CPU
+    processes, about 0.1 s per case)."""
+    import multiprocessing as mp
+    import os
+    from concurrent.futures import ProcessPoolExecutor
+    T = load_golden("c2_nw1000")
+    m, f = make_model("VolturnUS-S_example", T, {"min_freq": 0.0002})
+    cases = random_cases(512, 20241016)
+    a = m.analyzeCasesBatch(cases)
+    nproc = max(1, min(16, len(os.sched_getaffinity(0)), os.cpu_count() or 1))
+    # spawned workers (never forked from this GPU process); a worker that cannot start breaks
+    # the executor with an error instead of being respawned
+    with ProcessPoolExecutor(nproc, mp_context=mp.get_context("spawn")) as ex:
+        refs = list(ex.map(_oracle_c2_case, [(c,) for c in cases], chunksize=8))
+    bad = [ic for ic, (it, _) in enumerate(refs) if it != a["iters"][ic]]
+    assert not bad, f"iteration counts differ for cases {bad[:10]}"
+    worst = max(rel(a["Xi"][ic], X) for ic, (_, X) in enumerate(refs))
+    print(f"512 cases: worst rel Xi error vs oracle {worst:.2e}")
+    assert worst < RTOL
+
+
 def test_system_solve_12dof_matches_numpy():
     """rh_system_solve on random well-conditioned 2-FOWT systems (farm path)."""
     import torch
