@@ -579,8 +579,8 @@ def harness_check(args, world, rank):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=200)   # ~0.2 s: the GPU comes out of the CPU-baseline idle at full clock
     ap.add_argument("--ncase", type=int, default=NCASE)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-qtf", action="store_true")

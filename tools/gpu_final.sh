@@ -12,7 +12,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 rc=$?; echo "smoke rc=$rc"; tail -2 $OUT/smoke.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-c5 > $OUT/bench_prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-c5 > $OUT/bench_prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"
 if [ $rc -ne 0 ]; then tail -5 $OUT/bench_prof.log; exit $rc; fi
 cd $R

@@ -43,6 +43,22 @@ def main():
     t2 = time.perf_counter()
     print(f"enqueue {1e3 * (t1 - t0) / K:.3f} ms/step  finish {1e3 * (t2 - t0) / K:.3f} ms/step  "
           f"gpu {e0.elapsed_time(e1) / K:.3f} ms/step", flush=True)
+    # the bench's per-step timing events: wall time per step with 0, 2 and 3 events per step
+    for nev in (0, 2, 3):
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for i in range(K):
+            if nev == 3:
+                evs[i][0].record()
+            dd.retabulate()
+            if nev >= 2:
+                evs[i][1].record()
+            solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=want, prepared=prep)
+            if nev >= 2:
+                evs[i][2].record()
+        torch.cuda.synchronize()
+        print(f"  {nev} timing events per step: {1e3 * (time.perf_counter() - a) / K:.3f} ms/step wall", flush=True)
     # host cost alone: the same calls with the GPU idle are not possible (they launch), so time
     # a few pieces with a synchronisation in front of each
     for name, fn in (("retabulate", lambda: dd.retabulate()),
