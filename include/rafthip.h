@@ -163,7 +163,10 @@ int rh_version(void);
  * 0 = automatic (the grouped kernel when group_start is given and no margin is requested;
  * else the LDS-resident fast path when nw <= 1024 and the node tables fit in LDS; else the
  * general kernel), 1 = always the general kernel, 2 = never the grouped kernel (one case per
- * workgroup).  Used by the parity tests to cross-check the device paths on the same inputs. */
+ * workgroup), 3 = the lane-pair kernel, 4 / 5 = as 2 with the LDS-resident kernel in one launch
+ * / in two passes when the batch needs more than one round of workgroups (the cases that need
+ * the last iteration finish in a second launch; same results).
+ * Used by the parity tests to cross-check the device paths on the same inputs. */
 int rh_set_solver(rh_ctx* ctx, int which);
 
 /* Maximum cases per group of rh_cases.group_start (the compiled lock-step width). */

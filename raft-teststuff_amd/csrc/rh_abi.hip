@@ -46,6 +46,12 @@ struct rh_ctx {
 #define RH_PAIR_ON 0
 #endif
   bool use_pair = RH_PAIR_ON;   // rh_set_solver(ctx, 3): k_solve_pair instead of k_solve_lds (cross-checks)
+#ifndef RH_TWO_PASS
+#define RH_TWO_PASS 0
+#endif
+  bool two_pass = RH_TWO_PASS;  // k_solve_lds in two passes when a batch needs more than one round
+                                // (rh_set_solver(ctx, 5) on, 4 off; the default is RH_TWO_PASS)
+  int ncu = 0;                  // compute units of the device (rh_ctx_create)
   int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
   bool qtf_direct = false;      // rh_set_qtf_path(ctx, 1): the per-pair kernel even on a sorted grid
   // a second stream for k_qtf_kay, which runs beside k_qtf_lcoef + k_qtf_gemm (rh_ctx_create)
@@ -189,14 +195,23 @@ extern "C" int rh_prof_read(unsigned long long* out, int reset) {
 }
 #endif
 
+#ifdef RH_WGTIME
+extern "C" int rh_wgt_read(unsigned long long* out, int n) {
+  RH_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(rh::rh_wgt), sizeof(unsigned long long) * 2 * (n < 8192 ? n : 8192)));
+  return RH_OK;
+}
+#endif
+
 int rh_set_solver(rh_ctx* ctx, int which) {
   if (!ctx) return fail(RH_EINVAL, "rh_set_solver: null context");
-  if (which < 0 || which > 3)
-    return fail(RH_EINVAL, "rh_set_solver: which=%d (0 = auto, 1 = general kernel, 2 = ungrouped, 3 = k_solve_pair)",
-                which);
+  if (which < 0 || which > 5)
+    return fail(RH_EINVAL,
+                "rh_set_solver: which=%d (0 = auto, 1 = general kernel, 2 = ungrouped, 3 = k_solve_pair, "
+                "4 / 5 = ungrouped, k_solve_lds in one / two passes)", which);
   ctx->force_general = which == 1;
-  ctx->no_group = which == 2 || which == 3;
+  ctx->no_group = which >= 2;
   ctx->use_pair = which == 3 || (which == 0 && RH_PAIR_ON);
+  ctx->two_pass = which == 5 || (which != 4 && RH_TWO_PASS);
   return RH_OK;
 }
 
@@ -225,7 +240,7 @@ int rh_ctx_create(int device, rh_ctx** out) {
   RH_HIP(hipSetDevice(device));
   rh_ctx* c = new rh_ctx;
   c->device = device;
-  hipError_t e = hipSuccess;
+  hipError_t e = hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device);
   for (auto& sl : c->slot) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.staged, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.used, hipEventDisableTiming);
@@ -431,9 +446,22 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
     const size_t lsm = rh::solve_lds_smem(nnmax, nmmax, nb, lt);
     if (lsm <= 160 * 1024) {
       dim3 grid(cases->ncase), block(lt);
-      if (lt < rh::kLT) hipLaunchKernelGGL((rh::k_solve_lds<1, rh::kLT / 2>), grid, block, lsm, s, a);
-      else if (nb == 1) hipLaunchKernelGGL(rh::k_solve_lds<1>, grid, block, lsm, s, a);
-      else hipLaunchKernelGGL(rh::k_solve_lds<2>, grid, block, lsm, s, a);
+      auto kern = lt < rh::kLT ? rh::k_solve_lds<1, rh::kLT / 2> : nb == 1 ? rh::k_solve_lds<1> : rh::k_solve_lds<2>;
+      // Two passes when the batch needs more than one round of workgroups: a case's iteration
+      // count is not known at launch, and in one launch a CU that draws two long cases sets the
+      // makespan (C2: 0.87 of the CU time busy, tools/ubench/wg_times.py).  Pass 1 runs every
+      // case up to its last possible iteration, pass 2 finishes the cases that need it, one
+      // round, from the parked iterate (the same bits as one pass: test_two_pass_equals_one_pass).
+      int per_cu = 0;
+      RH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, lt, lsm));
+      const int nloop = cases->nIter + 1;
+      if (ctx->two_pass && nloop - 1 > cases->first_iter && cases->ncase > per_cu * ctx->ncu) {
+        a.stop_iter = nloop - 1;
+        hipLaunchKernelGGL(kern, grid, block, lsm, s, a);
+        RH_HIP(hipGetLastError());
+        a.resume = 1;
+      }
+      hipLaunchKernelGGL(kern, grid, block, lsm, s, a);
       return designs_used(ctx, s);
     }
   }

@@ -403,7 +403,13 @@ struct CaseArgs {
   const DevDesign* designs;
   rh_cases c;
   rh_solve_out o;
+  // two-pass launch of k_solve_lds (rh_solve_cases): pass 1 stops a case before iteration
+  // stop_iter, parks its relaxed iterate in o.Xi_last and marks it kCaseStopped; pass 2
+  // (resume = 1) continues only those cases from there.  The default runs one pass.
+  int stop_iter = 1 << 30;
+  int resume = 0;
 };
+constexpr int kCaseStopped = 9;   // internal status between the two passes (never returned)
 
 template <int NB>
 __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {

@@ -27,6 +27,12 @@ __device__ unsigned long long rh_prof[8];
 #define PROF_ADD(i, x)
 #endif
 
+#ifdef RH_WGTIME
+// Per-workgroup wall-clock (s_memrealtime, 100 MHz) of the fixed point: [2 slot] = start,
+// [2 slot + 1] = end of the loop, by dispatch slot (launch-tail analysis, tools/ubench/wg_times.py)
+__device__ unsigned long long rh_wgt[2 * 8192];
+#endif
+
 constexpr int kLT = 512;          // threads per case workgroup
 constexpr int kLW = kLT / 64;     // waves per case workgroup
 constexpr int kRingA = 3;         // wave-table prefetch depth (nodes) of phase A
@@ -215,8 +221,12 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wv_s = __builtin_amdgcn_readfirstlane(wv);   // wave index in an SGPR
   PROF_T(tp0);
+#ifdef RH_WGTIME
+  const unsigned long long wgt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int slot = xcd_remap(blockIdx.x, a.c.ncase);
   const int ic = a.c.order ? a.c.order[slot] : slot;
+  if (a.resume && a.o.status[ic] != kCaseStopped) return;   // pass 2: only the parked cases (uniform)
   const rh_design& d = a.designs[a.c.design[ic]].d;
   const int nw = d.nw, nn = d.nn, nm = d.nm;
   const unsigned nw16 = (unsigned)nw * 16u;
@@ -259,7 +269,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   {
     const int spec = a.c.spectrum[ic];
     const double Hs = a.c.Hs[ic], Tp = a.c.Tp[ic], gam = a.c.gamma[ic];
-    const rh_c128* XI0 = a.c.Xi_init ? a.c.Xi_init + c6 : nullptr;
+    const rh_c128* XI0 = a.resume ? a.o.Xi_last + c6 : a.c.Xi_init ? a.c.Xi_init + c6 : nullptr;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int b = tid + LT * j;
@@ -280,12 +290,15 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   const int nloop = a.c.nIter + 1;
   const double tol = a.c.tol;
   int status = RH_CASE_NOT_CONVERGED, iters = nloop;
-  double margin = INFINITY;   // closest call of the convergence test (rh_solve_out.margin)
+  // closest call of the convergence test (rh_solve_out.margin); pass 2 continues pass 1's
+  double margin = a.resume && a.o.margin ? a.o.margin[ic] : INFINITY;
+  const int it0 = a.resume ? a.stop_iter : a.c.first_iter;
+  const int itend = a.resume || a.stop_iter >= nloop ? nloop : a.stop_iter;
   __syncthreads();
   PROF_T(tp1);
   PROF_ADD(0, tp1 - tp0);
 
-  for (int it = a.c.first_iter; it < nloop; ++it) {
+  for (int it = it0; it < itend; ++it) {
     PROF_T(ta0);
     PROF_ADD(7, 1);
     // ---------------- A: per-node sums of squared relative-velocity components ----------
@@ -717,7 +730,30 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     }
   }
 
+  if (status == RH_CASE_NOT_CONVERGED && itend < nloop) {
+    // pass 1 stops here: park the relaxed iterate (the next iteration's XiLast) and the margin
+    // so far; pass 2 continues the case from iteration itend with the same bits
+#pragma unroll 1
+    for (int j = 0; j < NB; ++j) {
+      const int b = tid + LT * j;
+      if (b >= nw) continue;
+#pragma unroll 1
+      for (int c = 0; c < 6; ++c) st(a.o.Xi_last + c6 + c * nw + b, xl[c * NWP + b]);
+    }
+    if (tid == 0) {
+      a.o.status[ic] = kCaseStopped;
+      if (a.o.margin) a.o.margin[ic] = margin;
+    }
+    return;
+  }
+
   // ---------------- outputs ------------------------------------------------------------
+#ifdef RH_WGTIME
+  if (tid == 0 && blockIdx.x < 8192) {
+    rh_wgt[2 * blockIdx.x] = wgt0;
+    rh_wgt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   PROF_T(te0);
   if (tid == 0) {
     a.o.iters[ic] = iters;

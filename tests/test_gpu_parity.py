@@ -202,6 +202,27 @@ def test_full_size_c2_batch_properties():
         assert rel(a["Xi"][ic], r["Xi"][0]) < RTOL
 
 
+def test_two_pass_equals_one_pass():
+    """k_solve_lds in two launches (pass 1 parks the cases that need the last iteration, pass 2
+    finishes them; rh_solve_cases does this when a batch needs more than one round of
+    workgroups) gives the bits of one launch: Xi, iteration counts, statuses, margins, PSD."""
+    from raft import _native as N
+    T = load_golden("c2_nw1000")
+    m, f = make_model("VolturnUS-S_example", T, {"min_freq": 0.0002})
+    cases = random_cases(600, 4242)        # > 256 CUs x 1 workgroup: two passes
+    want = ("psd", "std", "zeta", "B_drag", "margin")
+    try:
+        N.check(N.lib().rh_set_solver(N.context(0), 5), "rh_set_solver")
+        a = m.analyzeCasesBatch(cases, want=want)
+        N.check(N.lib().rh_set_solver(N.context(0), 4), "rh_set_solver")
+        b = m.analyzeCasesBatch(cases, want=want)
+    finally:
+        N.check(N.lib().rh_set_solver(N.context(0), 0), "rh_set_solver")
+    assert np.any(a["iters"] == int(T["nIter"]) + 1)          # some cases went through pass 2
+    for k in ("Xi", "iters", "status", "margin", "psd", "std", "B_drag"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
 def _oracle_c2_case(args):
     """Worker of test_full_size_c2_every_case_vs_oracle (spawned process: NumPy only)."""
     import os

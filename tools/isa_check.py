@@ -47,7 +47,7 @@ def compile_asm():
 
 
 def kernels(lines):
-    """{mangled name: [instruction lines]} for every kernel body (up to its s_endpgm)."""
+    """{mangled name: [instruction lines]} for every kernel body (up to its .Lfunc_end label)."""
     out, name, body = {}, None, []
     for ln in lines:
         m = re.match(r"^(_Z\w+):", ln)
@@ -55,10 +55,11 @@ def kernels(lines):
             name, body = m.group(1), []
             continue
         if name is not None:
-            body.append(ln)
-            if re.match(r"^\s*s_endpgm", ln):
+            if re.match(r"^\.Lfunc_end\d+:", ln):   # the whole body: a kernel may end early in several places
                 out[name] = body
                 name = None
+                continue
+            body.append(ln)
     return out
 
 
