@@ -43,11 +43,24 @@ def pmc_traffic(*kernels):
     total = 0.0
     for kernel in kernels:
         hit = [v for name, v in d.items()
-               if kernel in name and "hbm_read_bytes_corrected" in v and "hbm_write_bytes" in v]
-        if not hit:
+               if kernel_name_is(name, kernel) and "hbm_read_bytes_corrected" in v and "hbm_write_bytes" in v]
+        if len(hit) != 1:      # exactly one launch of exactly this kernel
             return None
         total += hit[0]["hbm_read_bytes_corrected"] + hit[0]["hbm_write_bytes"]
     return total
+
+
+def kernel_name_is(name, kernel):
+    """Whether the demangled rocprof kernel `name` ("rh::k_qtf_kay(rh_qtf_design, ...)" or
+    "void rh::k_solve_lds<2, 512, false>(rh::CaseArgs)") is `kernel` exactly (a namespace-
+    qualified or bare name, template arguments included when `kernel` has them): k_qtf_kay
+    does not match k_qtf_kay_sum, k_solve_lds<2, 512 does not match k_solve_lds<2, 512, false>."""
+    base = name.split("(")[0].strip()
+    if base.startswith("void "):
+        base = base[5:]
+    if "<" not in kernel:
+        base = base.split("<")[0]
+    return base == kernel or base.endswith("::" + kernel)
 
 
 # The L2 -> CU rate of the solve kernel's own kproj access pattern with no arithmetic beside it
@@ -66,7 +79,7 @@ def pmc_l2(kernel, kernel_ms):
         return None
     for name, v in d.items():
         c = v.get("counters", {})
-        if kernel in name and "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        if kernel_name_is(name, kernel) and "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
             b = 128.0 * (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
             rate = b / (kernel_ms * 1e-3)
             return {"bytes": b, "TB_per_s": rate / 1e12, "peak_TB_per_s": L2_PEAK / 1e12, "frac": rate / L2_PEAK,
@@ -192,30 +205,47 @@ def cpu_baselines(qtf_seconds=10.0):
 CPU_BASELINE_CACHE = os.path.join("/tmp", "raft_bench_cpu_baseline.json")
 
 
-def cpu_baselines_cached(harness=False):
+def cpu_baseline_key():
+    """What a cached baseline must match: the code that produced it (this file and the oracle
+    sources, by content: the GPU box has no git history) and the host-core count it ran on."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in ["bench.py", os.path.join("oracle", "raft_oracle.py"), os.path.join("oracle", "qtf_oracle.py")]:
+        with open(os.path.join(ROOT, rel), "rb") as fh:
+            h.update(fh.read())
+    return f"{h.hexdigest()[:16]}-P{host_cores()[0]}"
+
+
+def cpu_baselines_cached(harness=False, reuse=False):
     """The CPU baseline legs for this run, measured before the process touches the GPU.
-    A `--gpus N` run started as one process measures them in the relaunch() parent (which never
-    touches the GPU) and hands them to rank 0 through CPU_BASELINE_CACHE; a torchrun-launched
-    N > 1 series (N = 1, 2, 4, 8 back to back on one node) reuses the measurement of an earlier
-    run on the same host from the last 24 h, and rank 0 measures it itself when there is none.
+    A plain single-process run (N = 1) always times them itself and leaves them in
+    CPU_BASELINE_CACHE.  reuse=True (the ranks of a torchrun-launched N > 1 run) takes that
+    file instead when it was written on this host in the last 24 h by the same code and core
+    count (cpu_baseline_key) -- the relaunch() parent of `--gpus N` writes it just before it
+    starts the ranks, and the driver's N = 1, 2, 4, 8 series runs N = 1 first -- and times them
+    itself otherwise.  Every leg says whether it was reused ("cached") and where it came from.
     harness=True (--harness-check) writes a stub instead of timing the oracle."""
     import socket
-    host = socket.gethostname()
-    try:
-        with open(CPU_BASELINE_CACHE) as fh:
-            d = json.load(fh)
-        if d.get("host") == host and time.time() - d.get("time", 0) < 86400 and d.get("stub", False) == harness:
-            return d["case"], d["qtf"]
-    except (OSError, ValueError, KeyError):
-        pass
+    host, key = socket.gethostname(), cpu_baseline_key()
+    if reuse:
+        try:
+            with open(CPU_BASELINE_CACHE) as fh:
+                d = json.load(fh)
+            if (d.get("host") == host and d.get("key") == key and time.time() - d.get("time", 0) < 86400
+                    and d.get("stub", False) == harness):
+                note = (f"reused: measured {time.time() - d['time']:.0f} s earlier on this host by the same code "
+                        f"(key {key}), {CPU_BASELINE_CACHE}")
+                return dict(d["case"], cached=True, provenance=note), dict(d["qtf"], cached=True, provenance=note)
+        except (OSError, ValueError, KeyError):
+            pass
     if harness:
         case = {"value": 0.0, "unit": "cases/s", "cores": 0, "kind": "stub", "sample": "harness check: no timing"}
         qtf = dict(case, unit="pairs/s")
     else:
         case, qtf = cpu_baselines()
     with open(CPU_BASELINE_CACHE, "w") as fh:
-        json.dump({"host": host, "time": time.time(), "stub": harness, "case": case, "qtf": qtf}, fh)
-    return case, qtf
+        json.dump({"host": host, "key": key, "time": time.time(), "stub": harness, "case": case, "qtf": qtf}, fh)
+    return dict(case, cached=False), dict(qtf, cached=False)
 
 
 def pack_outputs(res):
@@ -523,7 +553,7 @@ def relaunch(nproc, argv):
     import socket
     import subprocess
     if "--no-cpu-baseline" not in argv:
-        cpu_baselines_cached(harness="--harness-check" in argv)   # this process never touches the GPU
+        cpu_baselines_cached(harness="--harness-check" in argv)   # this process never touches the GPU: fresh
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
@@ -540,7 +570,7 @@ def harness_check(args, world, rank):
     import torch.distributed as dist
     base = None
     if rank == 0 and not args.no_cpu_baseline:
-        base = cpu_baselines_cached(harness=True)
+        base = cpu_baselines_cached(harness=True, reuse=world > 1)
     if world > 1:
         dist.init_process_group("gloo")
     for _ in range(args.warmup):
@@ -600,7 +630,7 @@ def main():
         return harness_check(args, world, rank)
     baselines = None
     if rank == 0 and not args.no_cpu_baseline:
-        baselines = cpu_baselines_cached()   # before this process initialises the GPU
+        baselines = cpu_baselines_cached(reuse=world > 1)   # before this process initialises the GPU
     pool, nproc = None, 1     # C5 prepares designs on native host threads (no worker pool)
     import torch
     import torch.distributed as dist
@@ -750,9 +780,6 @@ def main():
         pool.join()
     if baselines is not None:
         line["cpu_baseline"] = dict(baselines[0])
-        if world > 1:
-            line["cpu_baseline"]["note"] = ("measured on this host before the GPU work (relaunch() parent, or an "
-                                            "earlier run of this series within 24 h: " + CPU_BASELINE_CACHE + ")")
         if "qtf" in line:
             line["qtf"]["cpu_baseline"] = baselines[1]
     if rank == 0:

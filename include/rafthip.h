@@ -127,8 +127,8 @@ typedef struct {
   const int* group_start; /* optional [ngroup+1] device array of offsets into `order`: group g
                              is order[group_start[g] .. group_start[g+1]), 1..rh_group_cases()
                              cases that share design AND heading index, solved in lock-step by
-                             one workgroup (one wave-table load serves the group).  NULL ->
-                             one case per workgroup.  The caller guarantees the sharing.     */
+                             one workgroup.  Ignored when rh_group_cases() == 1 (the shipped
+                             library: one case per workgroup).  NULL -> one case per workgroup. */
   int ngroup;
 } rh_cases;
 
@@ -160,16 +160,15 @@ int rh_ctx_destroy(rh_ctx* ctx);
 int rh_version(void);
 
 /* Kernel selection for rh_solve_cases on this context (not part of the reference API):
- * 0 = automatic (the grouped kernel when group_start is given and no margin is requested;
- * else the LDS-resident fast path when nw <= 1024 and the node tables fit in LDS; else the
- * general kernel), 1 = always the general kernel, 2 = never the grouped kernel (one case per
- * workgroup), 3 = the lane-pair kernel, 4 / 5 = as 2 with the LDS-resident kernel in one launch
- * / in two passes when the batch needs more than one round of workgroups (the cases that need
- * the last iteration finish in a second launch; same results).
- * Used by the parity tests to cross-check the device paths on the same inputs. */
+ * 0 = automatic (the LDS-resident fast path when nw <= 1024 and the node tables fit in LDS;
+ * else the general kernel), 1 = always the general kernel.  Used by the parity tests to
+ * cross-check the device paths on the same inputs.  (Builds with -DRH_VARIANTS, made by
+ * tools/build_variants.sh for on-box A/B timing only, also accept 2..5: the lock-step grouped
+ * kernel, the lane-pair kernel and the two-pass launch, all measured slower) */
 int rh_set_solver(rh_ctx* ctx, int which);
 
-/* Maximum cases per group of rh_cases.group_start (the compiled lock-step width). */
+/* Maximum cases per group of rh_cases.group_start: 1 in the shipped library (no grouped
+ * kernel; group_start is then ignored). */
 int rh_group_cases(void);
 
 /* Waves per 64 (w1, w2) pairs in the QTF pair kernel on this context (not part of the

@@ -15,8 +15,13 @@
 #include "rh_qtf.hip"
 #include "rh_qtf_mfma.hip"
 #include "rh_solve.hip"
-#include "rh_solve_grp.hip"
-#include "rh_solve_pair.hip"
+#ifdef RH_VARIANTS
+// Opt-in solve kernels that were measured slower than k_solve_lds on C2: the
+// lock-step grouped kernel, the lane-pair kernel and the two-pass launch.  They are not part
+// of the shipped library; tools/build_variants.sh builds them for on-box A/B timing.
+#include "../../tools/ubench/variants_src/rh_solve_grp.hip"
+#include "../../tools/ubench/variants_src/rh_solve_pair.hip"
+#endif
 #include "rh_prep.h"       // host-only: native per-design preparation (rh_prep_designs)
 
 // One staging slot of the design descriptor array.  A context cycles through kDescSlots of
@@ -41,6 +46,7 @@ struct rh_ctx {
   int cur = 0;                          // slot of the last staging
   // tuning / cross-check knobs (per context: the ABI has no mutable process globals)
   bool force_general = false;   // rh_set_solver(ctx, 1): always use k_solve_cases (parity cross-checks)
+#ifdef RH_VARIANTS
   bool no_group = false;        // rh_set_solver(ctx, 2): ignore group_start (one case per workgroup)
 #ifndef RH_PAIR_ON
 #define RH_PAIR_ON 0
@@ -51,6 +57,7 @@ struct rh_ctx {
 #endif
   bool two_pass = RH_TWO_PASS;  // k_solve_lds in two passes when a batch needs more than one round
                                 // (rh_set_solver(ctx, 5) on, 4 off; the default is RH_TWO_PASS)
+#endif
   int ncu = 0;                  // compute units of the device (rh_ctx_create)
   int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
   bool qtf_direct = false;      // rh_set_qtf_path(ctx, 1): the per-pair kernel even on a sorted grid
@@ -73,7 +80,11 @@ struct rh_ctx {
 
 namespace {
 thread_local std::string g_err;
+#ifdef RH_VARIANTS
 constexpr int kGroupCases = 2;   // lock-step width of k_solve_grp
+#else
+constexpr int kGroupCases = 1;   // no grouped kernel in the shipped library: group_start is ignored
+#endif
 #ifndef RH_PAIR_RA
 #define RH_PAIR_RA 2
 #endif
@@ -152,6 +163,10 @@ int stage_designs(rh_ctx* ctx, const rh_design* designs, int n, hipStream_t s) {
   // the slot's device array may still be read by a kernel of an earlier call on another
   // stream: order the overwrite after it (a no-op on the same stream)
   RH_HIP(hipStreamWaitEvent(s, sl.used, 0));
+  // the slot describes no valid device copy until the copy and its event are enqueued: a failure
+  // below must not leave new descriptors in h beside a stale (n, stream) that the dedupe trusts
+  sl.n = 0;
+  sl.stream = nullptr;
   for (int i = 0; i < n; ++i) sl.h[i].d = designs[i];
   RH_HIP(hipMemcpyAsync(sl.d, sl.h, sizeof(rh::DevDesign) * n, hipMemcpyHostToDevice, s));
   RH_HIP(hipEventRecord(sl.staged, s));
@@ -204,14 +219,20 @@ extern "C" int rh_wgt_read(unsigned long long* out, int n) {
 
 int rh_set_solver(rh_ctx* ctx, int which) {
   if (!ctx) return fail(RH_EINVAL, "rh_set_solver: null context");
+#ifdef RH_VARIANTS
   if (which < 0 || which > 5)
     return fail(RH_EINVAL,
                 "rh_set_solver: which=%d (0 = auto, 1 = general kernel, 2 = ungrouped, 3 = k_solve_pair, "
                 "4 / 5 = ungrouped, k_solve_lds in one / two passes)", which);
-  ctx->force_general = which == 1;
   ctx->no_group = which >= 2;
   ctx->use_pair = which == 3 || (which == 0 && RH_PAIR_ON);
   ctx->two_pass = which == 5 || (which != 4 && RH_TWO_PASS);
+#else
+  if (which < 0 || which > 1)
+    return fail(RH_EINVAL, "rh_set_solver: which=%d (0 = auto, 1 = general kernel; the grouped, lane-pair and "
+                "two-pass kernels are tools/ubench variant builds)", which);
+#endif
+  ctx->force_general = which == 1;
   return RH_OK;
 }
 
@@ -391,12 +412,13 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   a.designs = staged_designs(ctx);
   a.c = *cases;
   a.o = *out;
+  int nmmax = 0;
+  for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
+#ifdef RH_VARIANTS
   // Grouped path (rh_solve_grp.hip): kGroupCases cases of one (design, heading) per workgroup.
   // (It does not report the convergence margin: with out->margin the ungrouped kernels run.)
   if (cases->group_start && cases->ngroup > 0 && !ctx->force_general && !ctx->no_group && !out->margin) {
     if (cases->ngroup > cases->ncase) return fail(RH_EINVAL, "rh_solve_cases: ngroup=%d > ncase", cases->ngroup);
-    int nmmax = 0;
-    for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
     const int npass = (nw + rh::kGT - 1) / rh::kGT;
     const size_t lsm = rh::solve_grp_smem(nnmax, nmmax, npass, kGroupCases);
     if (lsm <= 160 * 1024) {
@@ -405,8 +427,6 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
       return designs_used(ctx, s);
     }
   }
-  int nmmax = 0;
-  for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
   // Opt-in path (rh_solve_pair.hip, rh_set_solver(ctx, 3)): one bin per lane, lane-pair LU,
   // 4 waves per SIMD.  Parity-green but slower than k_solve_lds on C2.
   if (nw <= 1024 && !ctx->force_general && ctx->use_pair) {
@@ -421,6 +441,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
       return designs_used(ctx, s);
     }
   }
+#endif
   // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case (256 for nw <= 256), nw <= 1024.
   if (nw <= 2 * rh::kLT && !ctx->force_general) {
 #ifndef RH_SMALL_GRID_128
@@ -447,20 +468,22 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
     if (lsm <= 160 * 1024) {
       dim3 grid(cases->ncase), block(lt);
       auto kern = lt < rh::kLT ? rh::k_solve_lds<1, rh::kLT / 2> : nb == 1 ? rh::k_solve_lds<1> : rh::k_solve_lds<2>;
-      // Two passes when the batch needs more than one round of workgroups: a case's iteration
-      // count is not known at launch, and in one launch a CU that draws two long cases sets the
-      // makespan (C2: 0.87 of the CU time busy, tools/ubench/wg_times.py).  Pass 1 runs every
-      // case up to its last possible iteration, pass 2 finishes the cases that need it, one
-      // round, from the parked iterate (the same bits as one pass: test_two_pass_equals_one_pass).
-      int per_cu = 0;
-      RH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, lt, lsm));
+#ifdef RH_VARIANTS
+      // Two passes when the batch needs more than one round of workgroups (measured slower on
+      // C2: 0.895 vs 0.828 ms).  Pass 1 runs every case up to its last possible
+      // iteration, pass 2 finishes the cases that need it from the parked iterate.
       const int nloop = cases->nIter + 1;
-      if (ctx->two_pass && nloop - 1 > cases->first_iter && cases->ncase > per_cu * ctx->ncu) {
-        a.stop_iter = nloop - 1;
-        hipLaunchKernelGGL(kern, grid, block, lsm, s, a);
-        RH_HIP(hipGetLastError());
-        a.resume = 1;
+      if (ctx->two_pass && nloop - 1 > cases->first_iter) {
+        int per_cu = 0;
+        RH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, lt, lsm));
+        if (cases->ncase > per_cu * ctx->ncu) {
+          a.stop_iter = nloop - 1;
+          hipLaunchKernelGGL(kern, grid, block, lsm, s, a);
+          RH_HIP(hipGetLastError());
+          a.resume = 1;
+        }
       }
+#endif
       hipLaunchKernelGGL(kern, grid, block, lsm, s, a);
       return designs_used(ctx, s);
     }

@@ -226,7 +226,15 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
 #endif
   const int slot = xcd_remap(blockIdx.x, a.c.ncase);
   const int ic = a.c.order ? a.c.order[slot] : slot;
-  if (a.resume && a.o.status[ic] != kCaseStopped) return;   // pass 2: only the parked cases (uniform)
+#ifdef RH_VARIANTS
+  // two-pass launch (a tools/ubench variant, rh_abi.hip): pass 2 runs only the parked cases
+  const bool resume = a.resume != 0;
+  const int stop_iter = a.stop_iter;
+  if (resume && a.o.status[ic] != kCaseStopped) return;   // uniform
+#else
+  constexpr bool resume = false;
+  constexpr int stop_iter = 1 << 30;
+#endif
   const rh_design& d = a.designs[a.c.design[ic]].d;
   const int nw = d.nw, nn = d.nn, nm = d.nm;
   const unsigned nw16 = (unsigned)nw * 16u;
@@ -269,7 +277,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   {
     const int spec = a.c.spectrum[ic];
     const double Hs = a.c.Hs[ic], Tp = a.c.Tp[ic], gam = a.c.gamma[ic];
-    const rh_c128* XI0 = a.resume ? a.o.Xi_last + c6 : a.c.Xi_init ? a.c.Xi_init + c6 : nullptr;
+    const rh_c128* XI0 = resume ? a.o.Xi_last + c6 : a.c.Xi_init ? a.c.Xi_init + c6 : nullptr;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int b = tid + LT * j;
@@ -291,9 +299,9 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   const double tol = a.c.tol;
   int status = RH_CASE_NOT_CONVERGED, iters = nloop;
   // closest call of the convergence test (rh_solve_out.margin); pass 2 continues pass 1's
-  double margin = a.resume && a.o.margin ? a.o.margin[ic] : INFINITY;
-  const int it0 = a.resume ? a.stop_iter : a.c.first_iter;
-  const int itend = a.resume || a.stop_iter >= nloop ? nloop : a.stop_iter;
+  double margin = resume && a.o.margin ? a.o.margin[ic] : INFINITY;
+  const int it0 = resume ? stop_iter : a.c.first_iter;
+  const int itend = resume || stop_iter >= nloop ? nloop : stop_iter;
   __syncthreads();
   PROF_T(tp1);
   PROF_ADD(0, tp1 - tp0);
@@ -525,6 +533,8 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     // ---------------- C: excitation, Z(w), LU solve, convergence flags ------------------
     bool my_ok = true, my_nan = false, my_sing = false;
     double my_tmax = 0.0;
+    // the last allowed iteration stores every entry of the unrelaxed iterate (uniform)
+    const bool last_it = __builtin_amdgcn_readfirstlane(it + 1 == nloop ? 1 : 0) != 0;
 #pragma unroll 1
     for (int j = 0; j < NB; ++j) {
       // per-bin scalars picked without dynamic register indexing (the loop is not unrolled,
@@ -663,10 +673,14 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
         const double tt = sqrt(abs2(sub(x, xlast))) / (sqrt(abs2(x)) + tol);
         my_ok = my_ok && (!okj || tt < tol);
         my_tmax = okj ? fmax(my_tmax, tt) : my_tmax;
-        if (okj) {   // stores only
+        // The unrelaxed iterate leaves the kernel only as the output of the case's final
+        // iteration: the one whose test every (bin, DOF) passed, or the last allowed one
+        // (raft/raft_model.py:996-1000).  So an entry is stored only when it passed its own test
+        // or the loop is at its last iteration; the others are never read.
+        if (okj && (tt < tol || last_it)) {   // stores only
           st_nt(Xo + c * nw + b, x);   // streamed: only the last iteration's value is kept
-          if (XP) st(XP + c * nw + b, xlast);
         }
+        if (okj && XP) st(XP + c * nw + b, xlast);
         // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged (pads: 0)
         xl[c * NWP + b] = add(scl(xlast, 0.2), scl(x, 0.8));
       }

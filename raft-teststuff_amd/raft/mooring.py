@@ -198,24 +198,40 @@ class Line:
         current drag (current_load); the catenary is solved in the frame whose -z axis is that
         load's direction, with the same seabed-contact rule (the seabed plane then taken
         normal to the load through the lower end), and forces and stiffness are rotated back.
-        Zero current gives the plain solve bit for bit."""
-        swap = self.pB.r[2] < self.pA.r[2]
-        lower, upper = (self.pB, self.pA) if swap else (self.pA, self.pB)
-        d = upper.r - lower.r
+        Zero current gives the plain solve bit for bit.
+        Approximation (parity unpinned): with current, seabed contact is decided
+        from the lower end's global depth as without it; a net load that points away from the
+        seabed (a buoyant line in current) has no seabed contact at all, and the ends are then
+        ordered by height along the load (the catenary hangs "below" the end that is upstream
+        of the load)."""
         W = self.type["w"]
         R = None
+        up = False                                     # the net load points away from the seabed
         if current is not None and np.any(current):
             f = np.array([0.0, 0.0, -W]) + self.current_load(current, rho)
             W = float(np.linalg.norm(f))
             a = f / W                                  # load direction -> (0, 0, -1)
+            up = a[2] > 0.0
+            # a load with an upward component is first turned 180 deg about x, so that the
+            # Rodrigues step is taken at 1 + cos >= 1 (it is singular for a load straight up)
+            R0 = np.diag([1.0, -1.0, -1.0]) if up else np.eye(3)
+            a = R0 @ a
             v = np.array([a[1] * -1.0 - a[2] * 0.0, a[2] * 0.0 - a[0] * -1.0, 0.0])   # a x (0, 0, -1)
             cth = -a[2]
             V = np.array([[0.0, -v[2], v[1]], [v[2], 0.0, -v[0]], [-v[1], v[0], 0.0]])
-            R = np.eye(3) + V + V @ V / (1.0 + cth)   # Rodrigues: R a = (0, 0, -1)
+            R = (np.eye(3) + V + V @ V / (1.0 + cth)) @ R0   # R f / |f| = (0, 0, -1)
+        zA, zB = (self.pA.r[2], self.pB.r[2]) if R is None else ((R @ self.pA.r)[2], (R @ self.pB.r)[2])
+        swap = zB < zA
+        lower, upper = (self.pB, self.pA) if swap else (self.pA, self.pB)
+        d = upper.r - lower.r
+        if R is not None:
             d = R @ d
         LH = math.hypot(d[0], d[1])
         c, s = (d[0] / LH, d[1] / LH) if LH > 0 else (0.0, 0.0)
-        CB = -depth - lower.r[2] if lower.r[2] > -depth else 0.0    # off the seabed: no contact
+        if up:
+            CB = -1.0                                  # pulled away from the seabed: never in contact
+        else:
+            CB = -depth - lower.r[2] if lower.r[2] > -depth else 0.0    # off the seabed: no contact
         HA, VA, HF, VF, K2 = catenary(LH, d[2], self.L, self.type["EA"], W, CB=CB,
                                        HF0=self.HF, VF0=self.VF, Tol=tol)
         self.HF, self.VF = HF, VF

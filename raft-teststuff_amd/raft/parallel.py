@@ -29,6 +29,14 @@ def world_of(group=None):
     return dist.get_rank(group), dist.get_world_size(group)
 
 
+def _collective():
+    """True when a process group is initialised: the exchanges below then run through it even
+    at world size 1 (an identity exchange, but through the backend -- RCCL on the GPU box:
+    tests/test_gpu_rccl.py), and never without one."""
+    dist = _dist()
+    return dist.is_available() and dist.is_initialized()
+
+
 def case_shard(n, rank, world):
     """[lo, hi) of rank's contiguous block; sizes differ by at most one."""
     base, extra = divmod(n, world)
@@ -70,7 +78,7 @@ def gather_cases(local, n_total, group=None):
     import torch
     dist = _dist()
     rank, world = world_of(group)
-    if world == 1:
+    if not _collective():
         return dict(local)
     m = -(-n_total // world)
     out = {}
@@ -118,7 +126,7 @@ def assemble_qtf(compute_rows, hermitian_fill, n2, device=None, group=None, on_c
     compute_rows(out, rank, world)
     if on_computed is not None:
         on_computed()
-    if world > 1:
+    if _collective():
         flat = out.view(n2 * n2, 6)
         idx = [qtf_pair_index(n2, r, world, device) for r in range(world)]
         m = max(int(i.numel()) for i in idx)
@@ -126,9 +134,8 @@ def assemble_qtf(compute_rows, hermitian_fill, n2, device=None, group=None, on_c
         buf[:idx[rank].numel()] = flat.index_select(0, idx[rank])
         parts = [torch.empty_like(torch.view_as_real(buf)) for _ in range(world)]
         dist.all_gather(parts, torch.view_as_real(buf), group=group)
-        for r in range(world):
-            if r != rank:
-                flat.index_copy_(0, idx[r], torch.view_as_complex(parts[r])[:idx[r].numel()])
+        for r in range(world):   # own shard too: the matrix is what the exchange delivered
+            flat.index_copy_(0, idx[r], torch.view_as_complex(parts[r])[:idx[r].numel()])
     hermitian_fill(out)
     return out
 
@@ -180,6 +187,7 @@ def bin_fixed_point(partial, step, nn, nIter, nw, device=None, group=None, shard
     from . import _native as N
     dist = _dist()
     rank, world = world_of(group)
+    coll = _collective()
     mine = shards if shards is not None else [bin_shard(nw, rank, world)]
     sums = torch.zeros(3 * nn, dtype=torch.float64, device=device)
     part = torch.empty_like(sums)
@@ -189,12 +197,12 @@ def bin_fixed_point(partial, step, nn, nIter, nw, device=None, group=None, shard
         for lo, hi in mine:
             partial(lo, hi, part)
             sums += part
-        if world > 1:
+        if coll:
             _all_reduce(sums, dist.ReduceOp.SUM, group)
         flags.zero_()
         for lo, hi in mine:
             step(sums, lo, hi, flags)
-        if world > 1:
+        if coll:
             _all_reduce(flags, dist.ReduceOp.MAX, group)
         f = flags.tolist()
         if f[1]:
@@ -244,8 +252,7 @@ def solve_bins_sharded(fowt, case, nIter, XiStart=0.0, tol=0.01, group=None, sha
                               N.ptr(Bmat), N.ptr(Bd), N.ptr(Xi), N.ptr(XL), N.ptr(flags), s), "rh_bin_step")
 
     iters, status = bin_fixed_point(partial, step, nn, nIter, nw, device=dev, group=group, shards=shards)
-    rank, world = world_of(group)
-    if world > 1:
+    if _collective():
         _all_reduce(torch.view_as_real(Xi), dist.ReduceOp.SUM, group)
     if status == N.RH_CASE_NAN:
         raise Exception("Nan detected in response vector Xi.")       # raft/raft_model.py:957

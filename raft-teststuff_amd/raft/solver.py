@@ -135,9 +135,9 @@ def prepare_batch(designs, cases, tables_stream=None):
             d = designs[int(di)]
             sel = np.nonzero(cases.design_idx == di)[0]
             head[sel] = d.ensure_headings(cases.heading[sel] * DEG2RAD)
-    # Lock-step groups (k_solve_grp) are opt-in: RAFT_GROUP_WIDTH=2.  Measured on the C2
-    # batch they halve the wave-table stream but not the time per case, and
-    # one case per workgroup (k_solve_lds) schedules better at 512 cases per GPU.
+    # Lock-step groups (k_solve_grp) exist only in tools/ubench variant builds of the library
+    # (rh_group_cases() > 1 there) and are opt-in even then: RAFT_GROUP_WIDTH=2.  Measured on
+    # the C2 batch they halve the wave-table stream but not the time per case.
     width = min(N.lib().rh_group_cases(), int(os.environ.get("RAFT_GROUP_WIDTH", "1") or 1))
     if width > 1:
         # design-major, then heading; within a (design, heading) run by sea state, so that

@@ -202,27 +202,6 @@ def test_full_size_c2_batch_properties():
         assert rel(a["Xi"][ic], r["Xi"][0]) < RTOL
 
 
-def test_two_pass_equals_one_pass():
-    """k_solve_lds in two launches (pass 1 parks the cases that need the last iteration, pass 2
-    finishes them; rh_solve_cases does this when a batch needs more than one round of
-    workgroups) gives the bits of one launch: Xi, iteration counts, statuses, margins, PSD."""
-    from raft import _native as N
-    T = load_golden("c2_nw1000")
-    m, f = make_model("VolturnUS-S_example", T, {"min_freq": 0.0002})
-    cases = random_cases(600, 4242)        # > 256 CUs x 1 workgroup: two passes
-    want = ("psd", "std", "zeta", "B_drag", "margin")
-    try:
-        N.check(N.lib().rh_set_solver(N.context(0), 5), "rh_set_solver")
-        a = m.analyzeCasesBatch(cases, want=want)
-        N.check(N.lib().rh_set_solver(N.context(0), 4), "rh_set_solver")
-        b = m.analyzeCasesBatch(cases, want=want)
-    finally:
-        N.check(N.lib().rh_set_solver(N.context(0), 0), "rh_set_solver")
-    assert np.any(a["iters"] == int(T["nIter"]) + 1)          # some cases went through pass 2
-    for k in ("Xi", "iters", "status", "margin", "psd", "std", "B_drag"):
-        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
-
-
 def _oracle_c2_case(args):
     """Worker of test_full_size_c2_every_case_vs_oracle (spawned process: NumPy only)."""
     import os
@@ -285,28 +264,21 @@ def test_system_solve_12dof_matches_numpy():
         np.testing.assert_allclose(X[:, b], np.linalg.solve(Zs, F[:, b]), rtol=1e-10, atol=1e-12)
 
 
-@pytest.mark.parametrize("other", [1, 2, 3], ids=["general", "grouped", "pair"])
 @pytest.mark.parametrize("tag,design,settings,ncase", [("c2_nw1000", "VolturnUS-S_example", {"min_freq": 0.0002}, 128),
                                                        ("c2_nw200", "VolturnUS-S_example", None, 64),
                                                        ("c1_OC3spar", "OC3spar", None, 17)])
-def test_fast_and_general_kernels_agree(tag, design, settings, ncase, other, monkeypatch):
+def test_fast_and_general_kernels_agree(tag, design, settings, ncase):
     """The default path (k_solve_lds: one case per workgroup, XiLast in LDS) against the
-    general kernel (k_solve_cases, other=1), the lock-step grouped kernel (k_solve_grp, two
-    cases of one design and heading per workgroup, other=2) and the lane-pair kernel
-    (k_solve_pair: one bin per lane, the LU split over a lane pair, other=3) on the same batch:
-    identical iteration counts and statuses, outputs within 1e-12 (they differ only in the
-    summation order of the per-node bin reductions).  An odd case count leaves a half-empty
-    group."""
+    general kernel (k_solve_cases, rh_set_solver(ctx, 1)) on the same batch: identical
+    iteration counts and statuses, outputs within 1e-12 (they differ only in the summation
+    order of the per-node bin reductions)."""
     from raft import _native as N
     T = load_golden(tag)
     m, f = make_model(design, T, settings)
     cases = random_cases(ncase, 99)
     want = ("psd", "std", "zeta", "B_drag", "rao")
     a = m.analyzeCasesBatch(cases, want=want)
-    if other == 2:
-        monkeypatch.setenv("RAFT_GROUP_WIDTH", "2")
-    else:
-        N.check(N.lib().rh_set_solver(N.context(0), other), "rh_set_solver")
+    N.check(N.lib().rh_set_solver(N.context(0), 1), "rh_set_solver")
     try:
         b = m.analyzeCasesBatch(cases, want=want)
     finally:
@@ -391,6 +363,7 @@ def test_margin_output_and_knobs():
     a = solve_batch([f.device_design()], cs, m.nIter, m.XiStart, 0.01, want=("margin",)).host()
     ctx = N.context(0)
     assert N.lib().rh_set_solver(ctx, 7) == N.RH_EINVAL
+    assert N.lib().rh_set_solver(ctx, 3) == N.RH_EINVAL      # the lane-pair kernel is a tools/ubench variant
     N.check(N.lib().rh_set_solver(ctx, 1), "rh_set_solver")
     try:
         b = solve_batch([f.device_design()], cs, m.nIter, m.XiStart, 0.01, want=("margin",)).host()
@@ -404,11 +377,10 @@ def test_margin_output_and_knobs():
 
 
 @pytest.mark.parametrize("nw", [77, 255, 256, 333, 513, 1000])
-def test_pair_kernel_odd_grids(nw):
-    """Grids that leave pad lanes: nw not a multiple of 64 (every block size), odd nw (a lane
-    pair of k_solve_pair with one real and one pad bin), nw just past a block size (whole pad
-    waves).  The default kernel (k_solve_lds, including its 128-thread form) against the general
-    kernel k_solve_cases and the lane-pair kernel k_solve_pair on the same batch: identical
+def test_odd_grids(nw):
+    """Grids that leave pad lanes: nw not a multiple of 64 (every block size), odd nw, nw just
+    past a block size (whole pad waves).  The default kernel (k_solve_lds, including its
+    128-thread form) against the general kernel k_solve_cases on the same batch: identical
     iteration counts and statuses, Xi within 1e-12."""
     from raft import _native as N
     T = load_golden("c2_nw200")
@@ -417,7 +389,7 @@ def test_pair_kernel_odd_grids(nw):
     cases = random_cases(24, nw)
     want = ("psd", "std", "zeta", "B_drag", "rao", "margin")
     a = m.analyzeCasesBatch(cases, want=want)
-    for other in (1, 3):
+    for other in (1,):
         N.check(N.lib().rh_set_solver(N.context(0), other), "rh_set_solver")
         try:
             b = m.analyzeCasesBatch(cases, want=want)

@@ -219,6 +219,30 @@ def test_line_current_force_balance_and_lumped_mass(U):
     assert np.dot(fc, U) > 0
 
 
+@pytest.mark.parametrize("U", [[1.0, 0.0, 0.0], [0.0, 0.8, 0.0], [1e-7, 0.0, 0.0]])
+def test_buoyant_line_in_current(U):
+    """A buoyant line (30 kg/m at 0.3 m diameter: net weight -416 N/m) held between two fixed
+    points, in current: the net
+    load points up, so the solve turns the frame 180 deg before the Rodrigues step (which is
+    singular for a load straight up: U = 1e-7 m/s leaves 1 + cos ~ 1e-16 there).  The end forces
+    balance the distributed load and match the shooting solve of the continuous elastic line."""
+    from raft.mooring import MooringSystem, Point
+    ms = MooringSystem(depth=200.0)
+    ms.add_line_type("float", 0.3, 30.0, 500e6, 1.2, 0.1)
+    a = ms.add_point(Point.FIXED, [0.0, 0.0, -180.0])
+    b = ms.add_point(Point.FIXED, [150.0, 20.0, -60.0])
+    ln = ms.add_line(200.0, "float", a, b)
+    assert ln.type["w"] < 0
+    U = np.array(U)
+    f = np.array([0.0, 0.0, -ln.type["w"]]) + ln.current_load(U, ms.rho)
+    ln.static_solve(ms.depth, 1e-10, U, ms.rho)
+    assert np.all(np.isfinite(ln.fA)) and np.all(np.isfinite(ln.KA))
+    assert np.allclose(ln.fA + ln.fB, f * ln.L, rtol=1e-8, atol=1e-6 * np.linalg.norm(f) * ln.L)
+    fA, fB = _shooting_end_forces(ln, f, ln.fA * 1.05)
+    T = np.linalg.norm(ln.fB)
+    assert np.abs(ln.fA - fA).max() < 1e-7 * T and np.abs(ln.fB - fB).max() < 1e-7 * T
+
+
 def test_line_current_stiffness_matches_differences():
     """End stiffness of the rotated solve against central differences of its end forces (the
     current load held at the base geometry's value, as the analytic stiffness assumes)."""

@@ -18,7 +18,7 @@
 // Per case the arithmetic is that of k_solve_lds except the order of the bin sums of
 // phase A (pass-wise), so the two kernels agree to rounding, with identical iteration
 // counts on the parity cases (tests/test_gpu_parity.py).
-#include "rh_device.h"
+#include "../../../raft-teststuff_amd/csrc/rh_device.h"
 
 namespace rh {
 

@@ -18,7 +18,7 @@
 //     streamed it out every iteration: ~0.2 GB per C2 launch that only the last one used).
 //   * No per-lane branch anywhere around the solve: pad lanes (b >= nw) solve the clamped last
 //     bin with a zero right-hand side (x = 0 exactly) and store nothing.
-#include "rh_device.h"
+#include "../../../raft-teststuff_amd/csrc/rh_device.h"
 
 namespace rh {
 
