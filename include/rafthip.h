@@ -284,6 +284,20 @@ int rh_system_solve(rh_ctx* ctx, int nf, int nw, const rh_c128* Z, const double*
 int rh_system_solve_batch(rh_ctx* ctx, int ncase, int nf, int nw, const rh_c128* Z, const double* K,
                           const rh_c128* F, rh_c128* Xi, rh_stream stream);
 
+/* The coupled-array response of a batch of single-sea-state cases in one launch
+ * (raft/raft_model.py:1021-1065 with the per-heading excitation of :1049-1061): for every
+ * case and bin, each FOWT's wave excitation F_f = zeta (F_iner + F_drag(Bmat)) and impedance
+ * Z_f = -w^2 M + i w (B_lin + B_drag) + C (the fowt.Z of :1013, rebuilt from the design's
+ * matrices and the case's B_drag), then Xi = (blockdiag(Z_f) + K)^-1 F.  Replaces the
+ * rh_wave_excitation + rh_system_solve_batch pair without the per-(case, bin) Z and F arrays.
+ * Entries e = ic * nf + f (case-major, FOWT-minor) index design_idx, head, zeta [.][nw],
+ * B_drag [.][36] and Bmat [.][nn][9] (as rh_solve_cases writes them; every design must share
+ * nw and the submerged node count nn).  K: [6nf][6nf] array stiffness or NULL.
+ * Xi out: [ncase][6 nf][nw]. */
+int rh_array_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf, int ncase, const int* design_idx,
+                      const int* head, const double* zeta, const double* B_drag, const double* Bmat, const double* K,
+                      rh_c128* Xi, rh_stream stream);
+
 /* ------------------------------------------------------------------------------------
  * Slender-body second-order QTF (FOWT.calcQTF_slenderBody, raft/raft_fowt.py:1385-1648)
  * ------------------------------------------------------------------------------------ */

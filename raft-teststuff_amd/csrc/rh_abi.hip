@@ -677,6 +677,30 @@ int rh_system_solve_batch(rh_ctx* ctx, int ncase, int nf, int nw, const rh_c128*
   return RH_OK;
 }
 
+int rh_array_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf, int ncase, const int* design_idx,
+                      const int* head, const double* zeta, const double* B_drag, const double* Bmat, const double* K,
+                      rh_c128* Xi, rh_stream stream) {
+  if (!ctx || !designs || !design_idx || !head || !zeta || !B_drag || !Bmat || !Xi)
+    return fail(RH_EINVAL, "rh_array_response: null argument");
+  if (nf < 1 || nf > 2) return fail(RH_EINVAL, "rh_array_response: nf=%d (supported: 1, 2)", nf);
+  if (ncase <= 0) return ncase == 0 ? RH_OK : fail(RH_EINVAL, "rh_array_response: ncase=%d", ncase);
+  if (ndesign < 1) return fail(RH_EINVAL, "rh_array_response: ndesign=%d", ndesign);
+  const int nw = designs[0].nw, nn = designs[0].nn;
+  for (int i = 0; i < ndesign; ++i) {
+    if (int r = check_design(designs[i], true)) return r;
+    if (designs[i].nw != nw || designs[i].nn != nn)
+      return fail(RH_EINVAL, "rh_array_response: all designs must share nw and the submerged node count");
+  }
+  RH_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
+  rh::ArrayArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, B_drag, Bmat, K, Xi};
+  const dim3 g((nw + 63) / 64, ncase);
+  if (nf == 1) hipLaunchKernelGGL(rh::k_array_resp<1>, g, dim3(64), 0, s, a);
+  else hipLaunchKernelGGL(rh::k_array_resp<2>, g, dim3(64), 0, s, a);
+  return designs_used(ctx, s);
+}
+
 long long rh_qtf_workspace_bytes(const rh_qtf_design* q) {
   if (!q) return -1;
   return (long long)(rh::qtf_work_elems(*q) * sizeof(rh_c128));

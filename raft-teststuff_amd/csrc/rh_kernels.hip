@@ -1182,4 +1182,169 @@ __global__ __launch_bounds__(64) void k_system_solve_reg(int nw, const rh_c128* 
   }
 }
 
+
+// ----------------------------------------------------------------------------------------
+// k_array_resp: the coupled-array response of every (case, bin), one lane per bin
+// (raft/raft_model.py:1021-1065 for a batch of single-sea-state cases): for each FOWT f of
+// the case, its wave excitation with the final drag linearisation (k_heading_resp's
+// arithmetic, raft/raft_model.py:1049-1061) and its impedance rebuilt from the design's
+// M / B_lin / C and the case's B_drag (the expression of fowt.Z, raft/raft_model.py:944,
+// 1013: the bits the fixed point's Z output had), then Z_sys = blockdiag(Z_f) + K_array and
+// Xi = Z_sys^-1 F solved by the 6x6 blocks as in k_system_solve_reg.  Nothing per (case,
+// bin) goes through HBM but Xi: no Z and no F array.  For two FOWTs the excitation of the
+// second is formed after the first block is factored (A is then dead), so F2 never lives
+// beside A's factors.
+// ----------------------------------------------------------------------------------------
+struct ArrayArgs {
+  const DevDesign* designs;
+  int ncase;                   // cases; entry e = ic * NF + f is FOWT f of case ic
+  const int* design_idx;       // [ncase * NF] design of each entry
+  const int* head;             // [ncase * NF] heading index of each entry
+  const double* zeta;          // [ncase * NF][nw]
+  const double* B_drag;        // [ncase * NF][36]
+  const double* Bmat;          // [ncase * NF][nn][9] (equal nn over the FOWTs)
+  const double* K;             // [6 NF][6 NF] array stiffness, or NULL
+  rh_c128* Xi;                 // [ncase][6 NF][nw]
+};
+
+template <int NF>
+__global__ __launch_bounds__(64) void k_array_resp(ArrayArgs a) {
+  constexpr int N = 6 * NF;
+  __shared__ double ks[N * N];        // K_array (uniform reads)
+  __shared__ double mz[NF][4][36];    // per FOWT: M, B_lin (frequency-independent designs), C, B_drag
+  const int tid = (int)threadIdx.x;
+  const int ic = blockIdx.y;
+  for (int e = tid; e < N * N; e += 64) ks[e] = a.K ? a.K[e] : 0.0;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const rh_design& d = a.designs[a.design_idx[ic * NF + f]].d;
+    if (tid < 36) {
+      mz[f][0][tid] = d.mb_per_bin ? 0.0 : d.M[tid];
+      mz[f][1][tid] = d.mb_per_bin ? 0.0 : d.B[tid];
+      mz[f][2][tid] = d.C[tid];
+      mz[f][3][tid] = a.B_drag[((size_t)ic * NF + f) * 36 + tid];
+    }
+  }
+  __syncthreads();
+  const rh_design& d0 = a.designs[a.design_idx[ic * NF]].d;
+  const int nw = d0.nw;
+  const int b0 = blockIdx.x * 64 + tid;
+  const bool live = b0 < nw;
+  const int b = live ? b0 : nw - 1;          // pad lanes solve the last bin and store nothing
+  rh_c128* Xo = a.Xi + (size_t)ic * N * nw;
+  int zo;                        // a zero the compiler cannot see through: the LDS reads stay where
+  asm volatile("s_mov_b32 %0, 0" : "=s"(zo));   // they are used instead of being hoisted into registers
+  const double* ksz = ks + zo;
+  auto kk = [&](int i, int j) { return ksz[i * N + j]; };
+  // (0 + Z_f) + K_ff, Z_f = (-w^2 M + C) + i w (B + B_drag): the additions in the reference's order
+  auto zload = [&](int f, cd (&A)[6][6]) {
+    const rh_design& d = a.designs[a.design_idx[ic * NF + f]].d;
+    const double w = d.w[b], w2 = -(w * w);
+    const double* m = &mz[f][0][0] + zo;
+    if (d.mb_per_bin) {    // uniform: per-bin M and B (aero / BEM) from the design's arrays
+      const double* M = d.M + (size_t)b * 36;
+      const double* B = d.B + (size_t)b * 36;
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          const int e = 6 * i + j;
+          A[i][j] = mk((w2 * M[e] + m[72 + e]) + kk(6 * f + i, 6 * f + j), w * (B[e] + m[108 + e]));
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          const int e = 6 * i + j;
+          A[i][j] = mk((w2 * m[e] + m[72 + e]) + kk(6 * f + i, 6 * f + j), w * (m[36 + e] + m[108 + e]));
+        }
+    }
+  };
+  // F_wave of FOWT f (raft/raft_model.py:1049-1061; k_heading_resp with a.F)
+  auto excite = [&](int f, cd (&F)[6]) {
+    const size_t e = (size_t)ic * NF + f;
+    const rh_design& d = a.designs[a.design_idx[e]].d;
+    const int nn = d.nn, head = a.head[e];
+    const rh_c128* Uh = d.uhat + (size_t)head * nn * 3 * nw;
+    const rh_c128* Fe = d.finer + (size_t)head * 6 * nw;
+    const double z = a.zeta[e * nw + b];
+    drag_exc_bin(d.node, nn, a.Bmat + e * nn * 9, Uh, nw, b, F);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) F[c] = add(scl(ld(Fe + c * nw + b), z), scl(F[c], z));
+  };
+  if constexpr (NF == 1) {
+    cd A[6][6], x[6];
+    excite(0, x);
+    zload(0, A);
+    lu_solve<6>(A, x);
+    if (live)
+#pragma unroll
+      for (int i = 0; i < 6; ++i) st(Xo + (size_t)i * nw + b, x[i]);
+  } else {
+    static_assert(NF == 2, "k_array_resp: one or two FOWTs");
+    // X = A^-1 K12 column by column to a lane-private LDS slab [36][re, im][64 lanes]
+    __shared__ double xs[36 * 2 * 64];
+    cd y[6];
+    {
+      cd A[6][6];
+      int pa[6];
+      excite(0, y);                           // f1
+      zload(0, A);
+      lu_factor<6>(A, pa);
+      lu_apply<6>(A, pa, y);                  // y = A^-1 f1
+#pragma unroll 1
+      for (int j = 0; j < 6; ++j) {
+        cd c[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c[i] = mk(kk(i, 6 + j), 0.0);
+        lu_apply<6>(A, pa, c);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          xs[((6 * i + j) * 2) * 64 + tid] = c[i].r;
+          xs[((6 * i + j) * 2 + 1) * 64 + tid] = c[i].i;
+        }
+      }
+    }
+    auto X = [&](int i, int j) { return mk(xs[((6 * i + j) * 2) * 64 + tid], xs[((6 * i + j) * 2 + 1) * 64 + tid]); };
+    cd g[6];
+    excite(1, g);                             // f2, formed once A is dead
+    cd S[6][6];
+    int ps[6];
+    zload(1, S);                              // S = D - K21 X
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        cd t = mk(0, 0);
+#pragma unroll
+        for (int m = 0; m < 6; ++m) t = add(t, scl(X(m, j), kk(6 + i, m)));
+        S[i][j] = sub(S[i][j], t);
+      }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {             // g = f2 - K21 A^-1 f1
+      cd t = mk(0, 0);
+#pragma unroll
+      for (int m = 0; m < 6; ++m) t = add(t, scl(y[m], kk(6 + i, m)));
+      g[i] = sub(g[i], t);
+    }
+    lu_factor<6>(S, ps);
+    lu_apply<6>(S, ps, g);                    // x2
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {             // x1 = A^-1 f1 - X x2
+      cd t = y[i];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) t = sub(t, mul(X(i, m), g[m]));
+      y[i] = t;
+    }
+    if (live) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        st(Xo + (size_t)i * nw + b, y[i]);
+        st(Xo + (size_t)(6 + i) * nw + b, g[i]);
+      }
+    }
+  }
+}
+
 }  // namespace rh

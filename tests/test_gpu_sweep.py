@@ -264,3 +264,43 @@ def test_design_batch_with_operating_rotor():
         np.testing.assert_array_equal(res["iters"][2 * d:2 * d + 2], ref["iters"])
         np.testing.assert_array_equal(res["Xi"][2 * d:2 * d + 2], ref["Xi"])
     assert not np.array_equal(res["Xi"][0], res["Xi"][2])          # the variant is another design
+
+
+def _two_step_array_response(m, P, res):
+    """The pre-round-4 path of analyzeArrayBatch's response step: rh_wave_excitation (F of
+    every (case, FOWT) to HBM) then rh_system_solve_batch on the fixed point's per-bin Z."""
+    import torch
+    from raft import _native as N
+    nf, n, nw, dev = m.nFOWT, P["n"], m.nw, P["dev"]
+    s, ctx = N.stream_handle(torch, dev), N.context(m.device)
+    F = torch.empty([n * nf, 6, nw], dtype=torch.complex128, device=dev)
+    N.check(N.lib().rh_wave_excitation(ctx, P["arr"], nf, n * nf, N.ptr(P["prep"]["design"]), N.ptr(P["prep"]["head"]),
+                                       N.ptr(res["zeta"]), N.ptr(res["Bmat"].contiguous()), N.ptr(F), s),
+            "rh_wave_excitation")
+    X = torch.empty([n, 6 * nf, nw], dtype=torch.complex128, device=dev)
+    N.check(N.lib().rh_system_solve_batch(ctx, n, nf, nw, N.ptr(res["Z"]), N.ptr(P["K"]), N.ptr(F), N.ptr(X), s),
+            "rh_system_solve_batch")
+    return X.cpu().numpy()
+
+
+@pytest.mark.parametrize("farm", [True, False], ids=["two_fowts", "one_fowt"])
+def test_array_response_equals_two_step_path(farm):
+    """rh_array_response (one launch: excitation, impedance rebuilt from M / B_lin / C and the
+    case's B_drag, block solve) gives the bits of the two-step path that wrote every (case, bin)
+    impedance Z and excitation F to HBM, for two coupled FOWTs (k_array_resp<2>) and for one
+    (k_array_resp<1>)."""
+    from raft.solver import solve_batch
+    from test_gpu_parity import make_model
+    if farm:
+        m, _ = _farm_model(load_golden("c4_farm"))
+    else:
+        T = load_golden("c2_nw200")
+        m, _ = make_model("VolturnUS-S_example", T)
+        assert m.nFOWT == 1
+    rng = np.random.default_rng(46)
+    cases = [dict(wave_spectrum="JONSWAP", wave_period=float(rng.uniform(6, 18)), wave_height=float(rng.uniform(1, 10)),
+                  wave_heading=float(rng.choice([0, 45, 135, 270])), wave_gamma=0.0) for _ in range(24)]
+    P = m.prepareArrayBatch(cases)
+    fused = m.analyzeArrayBatch(prepared=P)["Xi"]
+    res = solve_batch(P["dds"], P["cs"], m.nIter, m.XiStart, 0.01, want=("zeta", "Bmat", "Z"), prepared=P["prep"])
+    np.testing.assert_array_equal(fused, _two_step_array_response(m, P, res))
