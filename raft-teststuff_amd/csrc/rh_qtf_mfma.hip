@@ -563,6 +563,42 @@ __device__ __forceinline__ void node_probe_glob(const rh_qtf_design& q, int n, i
   }
 }
 
+// node_probe_glob for one kind of probe: K = 0 (g < 6: X_j), 1 (6 <= g < 9: w X_j translation),
+// 2 (9 <= g < 12: w X_j rotation): the same arithmetic, one node_force_z instantiation per kind
+template <int K>
+__device__ __forceinline__ void node_probe_glob_k(const rh_qtf_design& q, int n, int g, const NodeW1& a, cd* Q) {
+  NodeZ z;
+  const double x = qn(q, RH_QN_RX, n), y = qn(q, RH_QN_RY, n), zz = qn(q, RH_QN_RZ, n);
+  double D[3];
+  if constexpr (K == 0) {
+    dlin_unit(g, x, y, zz, D);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) z.dr[i] = mk(D[i], 0);
+    node_force_z<ZDR>(q, n, a, z, Q);
+  } else {
+    const int j = g - 6;
+    dlin_unit(j, x, y, zz, D);
+    const double qv[3] = {qn(q, RH_QN_QX, n), qn(q, RH_QN_QY, n), qn(q, RH_QN_QZ, n)};
+    cd v[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) v[i] = mk(0, -D[i]);
+    const cd vq = add(add(scl(v[0], qv[0]), scl(v[1], qv[1])), scl(v[2], qv[2]));
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      z.vp[i] = sub(v[i], scl(vq, qv[i]));
+      z.om[i] = mk(0, 0);
+    }
+    z.va = scl(vq, -1.0);
+    if constexpr (K == 2) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) z.om[i] = mk(0, i == j - 3 ? -1.0 : 0.0);
+      node_force_z<ZVP | ZVA | ZOM>(q, n, a, z, Q);
+    } else {
+      node_force_z<ZVP | ZVA>(q, n, a, z, Q);
+    }
+  }
+}
+
 // own probe j (0..7) of node n (basis order of qtf_node_basis)
 __device__ __forceinline__ void node_probe_own(const rh_qtf_design& q, int n, int j, const NodeW1& a, cd* Q) {
   NodeZ z;
@@ -702,14 +738,19 @@ __global__ __launch_bounds__(512) void k_qtf_lcoef(rh_qtf_design q, QtfWork wk, 
   };
   if (y < 18) {
     const int g = y;
-    if (g < 12) {
+    // one probe kind per node loop (the branch on g is uniform and hoisted): a loop body that
+    // held every kind of node_probe_glob would need the registers of the largest one throughout
+    auto node_loop = [&](auto kind) {
 #pragma unroll 1
       for (int n = wv; n < q.nq; n += 8) {
         NodeW1 a;
         load_w1(q, wk, n, fs, a);
-        node_probe_glob(q, n, g, a, Q);
+        node_probe_glob_k<decltype(kind)::value>(q, n, g, a, Q);
       }
-    }
+    };
+    if (g < 6) node_loop(std::integral_constant<int, 0>{});
+    else if (g < 9) node_loop(std::integral_constant<int, 1>{});
+    else if (g < 12) node_loop(std::integral_constant<int, 2>{});
 #pragma unroll 1
     for (int m = wv; m < q.nmq; m += 8) {
       WlSide a;

