@@ -61,12 +61,6 @@ struct rh_ctx {
   int ncu = 0;                  // compute units of the device (rh_ctx_create)
   int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
   bool qtf_direct = false;      // rh_set_qtf_path(ctx, 1): the per-pair kernel even on a sorted grid
-  // a second stream for k_qtf_kay, which runs beside k_qtf_lcoef + k_qtf_gemm (rh_ctx_create)
-  hipStream_t qtf_aux = nullptr;
-  hipEvent_t qtf_tables_done = nullptr, qtf_kay_done = nullptr;
-  // serialises the record -> wait -> launch -> record sequence on qtf_aux and its two events:
-  // calls from several host threads on one context must not interleave it
-  std::mutex qtf_mu;
   // per-stream scratch of rh_wave_tables (per-node forces, k_wave_tables_nodes ->
   // k_wave_force_sum): one buffer per stream, so stream order alone protects its reuse
   struct Scratch {
@@ -266,14 +260,7 @@ int rh_ctx_create(int device, rh_ctx** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.staged, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.used, hipEventDisableTiming);
   }
-  // the QTF's second stream, made here so that a first QTF does not pay for it
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->qtf_aux, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->qtf_tables_done, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->qtf_kay_done, hipEventDisableTiming);
   if (e != hipSuccess) {
-    if (c->qtf_aux) (void)hipStreamDestroy(c->qtf_aux);
-    if (c->qtf_tables_done) (void)hipEventDestroy(c->qtf_tables_done);
-    if (c->qtf_kay_done) (void)hipEventDestroy(c->qtf_kay_done);
     for (auto& sl : c->slot) {
       if (sl.staged) (void)hipEventDestroy(sl.staged);
       if (sl.used) (void)hipEventDestroy(sl.used);
@@ -299,12 +286,6 @@ int rh_ctx_destroy(rh_ctx* ctx) {
     if (sl.d) (void)hipFree(sl.d);
     if (sl.h) (void)hipHostFree(sl.h);
   }
-  if (ctx->qtf_aux) {
-    (void)hipStreamSynchronize(ctx->qtf_aux);
-    (void)hipStreamDestroy(ctx->qtf_aux);
-  }
-  if (ctx->qtf_tables_done) (void)hipEventDestroy(ctx->qtf_tables_done);
-  if (ctx->qtf_kay_done) (void)hipEventDestroy(ctx->qtf_kay_done);
   if (!ctx->wt_scratch.empty()) (void)hipDeviceSynchronize();
   for (auto& sc : ctx->wt_scratch) (void)hipFree(sc.p);
   delete ctx;
@@ -733,30 +714,17 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
     RH_HIP(hipGetLastError());
   }
   if (gemm) {
-    // w1-side coefficients, then the pair tiles: bilinear + potential GEMMs, then Kim & Yue
-    // and the Hermitian fill (rh_qtf_mfma.hip)
+    // the w1-side GEMM coefficients, the Kim & Yue tile sums (both need only the tables), then
+    // the pair tiles: bilinear + potential GEMMs plus the Kim & Yue sums, and the Hermitian fill
+    // (rh_qtf_mfma.hip)
     const int nt = n2p / 16, ntile = nt * (nt + 1) / 2;
     const int blocks = (ntile - rank + nrank - 1) / nrank;
-    if (blocks > 0) {
-      // k_qtf_kay needs only the tables: it runs on the context's second stream beside
-      // k_qtf_lcoef + k_qtf_gemm (each alone fills ~1.3 waves of workgroups), and k_qtf_kay_sum
-      // joins the two on the caller's stream.  Every later use of the workspace on `s` is
-      // ordered after k_qtf_kay_sum, which waits for k_qtf_kay.
-      std::lock_guard<std::mutex> lock(ctx->qtf_mu);
-      RH_HIP(hipEventRecord(ctx->qtf_tables_done, s));
-      RH_HIP(hipStreamWaitEvent(ctx->qtf_aux, ctx->qtf_tables_done, 0));
-      hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, ctx->qtf_aux, *q, wk, qtf, rank, nrank,
-                         mirror);
-      RH_HIP(hipGetLastError());
-      RH_HIP(hipEventRecord(ctx->qtf_kay_done, ctx->qtf_aux));
-    }
     hipLaunchKernelGGL(rh::k_qtf_lcoef, dim3(nb, 18 + q->nq + q->nmq), dim3(512), 0, s, *q, wk, M66);
     RH_HIP(hipGetLastError());
     if (blocks > 0) {
-      hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(2 * blocks), dim3(384), 0, s, *q, wk, qtf, rank, nrank);
+      hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, s, *q, wk, rank, nrank);
       RH_HIP(hipGetLastError());
-      RH_HIP(hipStreamWaitEvent(s, ctx->qtf_kay_done, 0));
-      hipLaunchKernelGGL(rh::k_qtf_kay_sum, dim3(blocks), dim3(256), 0, s, *q, wk, qtf, rank, nrank, mirror);
+      hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(2 * blocks), dim3(384), 0, s, *q, wk, qtf, rank, nrank, mirror);
       RH_HIP(hipGetLastError());
     }
     return RH_OK;

@@ -719,15 +719,14 @@ __device__ __forceinline__ void pinkster_probe(const rh_qtf_design& q, const Qtf
 //                 wave 0 adds Pinkster; the 8 partial sums meet in LDS in wave order
 //   y < 18 + nq : the 8 own columns of node y - 18 (wave j = probe j)
 //   else        : the 3 own columns of waterline member y - 18 - nq (waves 0..2)
-__global__ __launch_bounds__(512) void k_qtf_lcoef(rh_qtf_design q, QtfWork wk, const double* __restrict__ M66) {
-  __shared__ double red[8][12][64];
+__device__ __forceinline__ void lcoef_block(const rh_qtf_design& q, const QtfWork& wk, const double* __restrict__ M66,
+                                            int fb, int y, double (*red)[12][64]) {
   const int lane = (int)threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int f = (int)blockIdx.x * 64 + lane;
+  const int f = fb * 64 + lane;
   const int n2 = q.n2, n2p = qtf_n2p(q), kp = qtf_kp(q);
   const bool live = f < n2;
   const int fs = live ? f : 0;            // pad lanes evaluate a valid column and store zeros
-  const int y = (int)blockIdx.y;
   cd Q[6];
 #pragma unroll
   for (int d = 0; d < 6; ++d) Q[d] = mk(0, 0);
@@ -841,6 +840,9 @@ __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const
   p3 += q3;
 }
 
+// row-major index of upper-triangle tile (T1, T2), T2 >= T1, of an nt x nt tile grid
+__device__ __forceinline__ int qtf_tile_id(int T1, int T2, int nt) { return T1 * nt - T1 * (T1 - 1) / 2 + (T2 - T1); }
+
 // Q_d over the bilinear terms and the two potential channels for one tile and three DOFs.
 // Workgroup = 6 waves: wave w takes DOF 3 dg + (w % 3) (dg = the block's DOF half) and half
 // w / 3 of the work: the first half of K and channel +, or the second half and channel -
@@ -848,7 +850,7 @@ __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const
 // reach the first through LDS.  Blocks are (tile, DOF half) pairs, remapped so that an XCD
 // works on a contiguous run of tiles (their L rows stay in its L2).
 __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf, int rank,
-                                                  int nrank) {
+                                                  int nrank, int mirror) {
   __shared__ double part[3][16][64];
   __shared__ double pscal[4][256];   // per pair: aux2 (w1 - w2) alpha+, ... alpha- (complex)
   const int lane = (int)threadIdx.x & 63;
@@ -915,6 +917,10 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
   }
   __syncthreads();
   if (half == 1) return;
+  // + the tile's Kim & Yue sums (k_qtf_kay, the previous launch), then the upper-triangle entry and,
+  // for a whole QTF, its Hermitian mirror (raft/raft_fowt.py:1639-1640: qtf + conj(qtf).T -
+  // diag(conj(diag(qtf))))
+  const double* ks = wk.KS + (size_t)qtf_tile_id(T1, T2, nt) * 12 * 256;
   const int i2 = i2b + mr;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -924,7 +930,17 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
     const cd Pp = mk(cre[r], cim[r]), Pm = mk(part[dl][8 + r][lane], part[dl][12 + r][lane]);
     const cd Qd = add(mk(mre[r] + part[dl][r][lane], mim[r] + part[dl][4 + r][lane]),
                       add(mul(mk(pscal[0][e], pscal[1][e]), Pp), mul(mk(pscal[2][e], pscal[3][e]), Pm)));
-    st(qtf + ((size_t)i1 * n2 + i2) * 6 + d, Qd);
+    const int ek = kr * 16 + mr + 64 * r;   // kay_tile's element of this pair
+    const cd Qf = add(Qd, mk(ks[(2 * d) * 256 + ek], ks[(2 * d + 1) * 256 + ek]));
+    rh_c128* up = qtf + ((size_t)i1 * n2 + i2) * 6 + d;
+    if (!mirror) {
+      st(up, Qf);
+    } else if (i1 == i2) {
+      st(up, sub(add(Qf, cconj(Qf)), cconj(Qf)));
+    } else {
+      st(up, Qf);
+      st(qtf + ((size_t)i2 * n2 + i1) * 6 + d, cconj(Qf));
+    }
   }
 }
 
@@ -937,23 +953,18 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
 // keeps per element sum sre and sum sre p over the member's rows, and adds
 // phase x [s0 pf; s x pf] (the rows' translateForce3to6DOF) to the tile's LDS sum in member
 // order.  The next row's operands are loaded while the current row is reduced.
-// row-major index of upper-triangle tile (T1, T2), T2 >= T1, of an nt x nt tile grid
-__device__ __forceinline__ int qtf_tile_id(int T1, int T2, int nt) { return T1 * nt - T1 * (T1 - 1) / 2 + (T2 - T1); }
 
 constexpr int kKayW = 4;
 constexpr int kKayThreads = 64 * kKayW;
-__global__ __launch_bounds__(kKayThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_qtf_kay(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf,
-                                                         int rank, int nrank, int mirror) {
-  __shared__ double acc[12][256];   // [re/im x DOF][element]
-  const int tid = (int)threadIdx.x, lane = tid & 63;
+// One pair tile's Kim & Yue sums by a group of kKayW waves (tid 0 .. kKayThreads - 1 of the
+// group) into acc[12][256]; live = false: the group has no tile and only joins the block's
+// barriers (every group of a block runs the same member rounds).  Every __syncthreads here is
+// a whole-block barrier: the caller's block is made of such groups only.
+__device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& wk, int T1, int T2, bool live, int tid,
+                                         double (*acc)[256]) {
+  const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n2 = q.n2, n2p = qtf_n2p(q), nt = n2p / 16, nkr = q.nkr;
-  int T1 = 0, t = rank + nrank * xcd_remap((int)blockIdx.x, (int)gridDim.x);
-  while (t >= nt - T1) {   // block-uniform
-    t -= nt - T1;
-    ++T1;
-  }
-  const int T2 = T1 + t;
   const int mr = lane & 15, kr = lane >> 4;
   const int i1b = 16 * T1, i2b = 16 * T2;
   for (int e = tid; e < 12 * 256; e += kKayThreads) (&acc[0][0])[e] = 0.0;
@@ -978,6 +989,7 @@ __global__ __launch_bounds__(kKayThreads) __attribute__((amdgpu_waves_per_eu(2))
     }
     const bool any_left = j > round * kKayW;   // block-uniform: this round has at least one member
     if (!any_left) break;
+    if (!live) mine = -1;                      // no tile: the rounds' barriers only
     double sg[4][4];   // [s0, sx, sy, sz][element] of this wave's member
     if (mine >= 0) {
       const int r0 = ldsi(q.kstart + mine), r1 = min(ldsi(q.kstart + mine + 1), nkr);
@@ -995,58 +1007,76 @@ __global__ __launch_bounds__(kKayThreads) __attribute__((amdgpu_waves_per_eu(2))
           Rr[s] = wk.KR[o2 + (size_t)4 * s * n2p];
         }
       };
-      load_row(r0, va, vb, vr);
+      // Per (row, element) factors: every table value an element's epilogue needs is loaded at
+      // the start of its row, in one batch, before the row's MFMAs; the row's tail (the element
+      // formulas) then runs without a memory wait, and the wave-uniform waterline / interval
+      // choices are selects, not branches.  (The epilogue used to load each element's factors
+      // where it used them, behind a branch: every element drained the whole vector-memory queue,
+      // the next row's prefetched operands included.)
+      double k1v[4], w1v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i1 = min(i1b + kr + 4 * r, n2 - 1);
+        k1v[r] = q.k2[i1];
+        w1v[r] = q.w2[i1];
+      }
 #pragma unroll 1
       for (int ir = r0; ir < r1; ++ir) {
+        load_row(ir, va, vb, vr);
+        double t1[4][6], t2[6];
+        {
+          const double2* T2 = reinterpret_cast<const double2*>(wk.kayt + ((size_t)ir * n2 + i2s) * kKayT + 2);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const double2 v = T2[c];
+            t2[2 * c] = v.x;
+            t2[2 * c + 1] = v.y;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i1 = min(i1b + kr + 4 * r, n2 - 1);
+            const double2* T1 = reinterpret_cast<const double2*>(wk.kayt + ((size_t)ir * n2 + i1) * kKayT + 2);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const double2 v = T1[c];
+              t1[r][2 * c] = v.x;
+              t1[r][2 * c + 1] = v.y;
+            }
+          }
+        }
+        const double R = ldsd(q.kray + RH_KR_R * nkr + ir);
+        const bool wl = ir == r0;
+        const double px = wl ? qm(q, RH_QM_WLX, mine) : ldsd(q.kray + RH_KR_MX * nkr + ir);
+        const double py = wl ? qm(q, RH_QM_WLY, mine) : ldsd(q.kray + RH_KR_MY * nkr + ir);
+        const double pz = wl ? qm(q, RH_QM_WLZ, mine) : ldsd(q.kray + RH_KR_MZ * nkr + ir);
+        const double z1 = ldsd(q.kray + RH_KR_Z1 * nkr + ir), z2 = ldsd(q.kray + RH_KR_Z2 * nkr + ir);
         d4 ca = {0, 0, 0, 0}, cbk = {0, 0, 0, 0};
 #pragma unroll
         for (int s = 0; s < 6; ++s) {
           ca = mfma64(va[s], vr[s], ca);
           cbk = mfma64(vb[s], vr[s], cbk);
         }
-        if (ir + 1 < r1) load_row(ir + 1, va, vb, vr);   // next row in flight during this row's epilogue
-        const double R = ldsd(q.kray + RH_KR_R * nkr + ir);
-        const double* t2 = wk.kayt + ((size_t)ir * n2 + i2s) * kKayT;
-        const double p1 = t2[2], m1 = t2[3], p2 = t2[4], m2 = t2[5], c2 = t2[6], r2 = t2[7];
+        const double p1 = t2[0], m1 = t2[1], p2 = t2[2], m2 = t2[3], c2 = t2[4], r2 = t2[5];
         const double cR = rho * g * R * 2 / M_PI;
-        const bool wl = ir == r0;
-        double px, py, pz;
-        if (wl) {
-          px = qm(q, RH_QM_WLX, mine);
-          py = qm(q, RH_QM_WLY, mine);
-          pz = qm(q, RH_QM_WLZ, mine);
-        } else {
-          px = ldsd(q.kray + RH_KR_MX * nkr + ir);
-          py = ldsd(q.kray + RH_KR_MY * nkr + ir);
-          pz = ldsd(q.kray + RH_KR_MZ * nkr + ir);
-        }
         const double H = h / R, k2h = k2 * R * H;
-        const double zz1 = (ldsd(q.kray + RH_KR_Z1 * nkr + ir) + h) / h, zz2 = (ldsd(q.kray + RH_KR_Z2 * nkr + ir) + h) / h;
+        const double zz1 = (z1 + h) / h, zz2 = (z2 + h) / h;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int i1 = min(i1b + kr + 4 * r, n2 - 1);
-          const double* t1 = wk.kayt + ((size_t)ir * n2 + i1) * kKayT;
-          const double kap = cR * t1[7] * r2;   // rho g R 2/pi / (k1R k2R)
-          double sre;
-          if (wl) {   // waterline term (:1133-1149): Re(-i kap A) = kap Im(A)
-            sre = kap * ca[r];
-          } else {    // node-interval Bernoulli term (:1155-1200)
-            const double k1h = q.k2[i1] * R * H;
-            const double P1 = t1[2], M1 = t1[3], P2 = t1[4], M2 = t1[5];
-            const double ia = 0.5 / (k1h + k2h);
-            const double a2 = (P2 * p2 - M2 * m2) * ia, a1 = (P1 * p1 - M1 * m1) * ia;
-            double Im, Ip;
-            if (q.w2[i1] == w2) {
-              Im = 0.5 * (a2 - zz2 - a1 + zz1);
-              Ip = 0.5 * (a2 + zz2 - a1 - zz1);
-            } else {
-              const double id = 0.5 / (k1h - k2h);
-              const double d2 = (P2 * m2 - M2 * p2) * id, d1 = (P1 * m1 - M1 * p1) * id;
-              Im = 0.5 * (a2 - d2 - a1 + d1);
-              Ip = 0.5 * (a2 + d2 - a1 - d1);
-            }
-            sre = -kap * (t1[6] * c2) * (Im * ca[r] + Ip * t1[7] * r2 * cbk[r]);   // Re(i kap cc (Im A + Ip/(k1R k2R) B))
-          }
+          const double kap = cR * t1[r][5] * r2;   // rho g R 2/pi / (k1R k2R)
+          // waterline term (:1133-1149): Re(-i kap A) = kap Im(A)
+          const double s_wl = kap * ca[r];
+          // node-interval Bernoulli term (:1155-1200)
+          const double k1h = k1v[r] * R * H;
+          const double P1 = t1[r][0], M1 = t1[r][1], P2 = t1[r][2], M2 = t1[r][3];
+          const double ia = 0.5 / (k1h + k2h);
+          const double a2 = (P2 * p2 - M2 * m2) * ia, a1 = (P1 * p1 - M1 * m1) * ia;
+          const bool same = w1v[r] == w2;      // the diagonal pair: the (k1 - k2) terms are their limits
+          const double id = 0.5 / (k1h - k2h);
+          const double d2 = same ? zz2 : (P2 * m2 - M2 * p2) * id, d1 = same ? zz1 : (P1 * m1 - M1 * p1) * id;
+          const double Im = 0.5 * (a2 - d2 - a1 + d1);
+          const double Ip = 0.5 * (a2 + d2 - a1 - d1);
+          const double s_in = -kap * (t1[r][4] * c2) * (Im * ca[r] + Ip * t1[r][5] * r2 * cbk[r]);   // Re(i kap cc (Im A + Ip/(k1R k2R) B))
+          const double sre = wl ? s_wl : s_in;
           sg[0][r] += sre;
           sg[1][r] += sre * px;
           sg[2][r] += sre * py;
@@ -1082,44 +1112,41 @@ __global__ __launch_bounds__(kKayThreads) __attribute__((amdgpu_waves_per_eu(2))
       __syncthreads();
     }
   }
-  // the tile's Kim & Yue sums to the workspace; k_qtf_kay_sum adds them to the GEMM part
-  double* ks = wk.KS + (size_t)qtf_tile_id(T1, T2, nt) * 12 * 256;
-  for (int e = tid; e < 12 * 256; e += kKayThreads) ks[e] = (&acc[0][0])[e];
+  // the tile's Kim & Yue sums to the workspace; the GEMM epilogue adds them to the pair sums
+  if (live) {
+    double* ks = wk.KS + (size_t)qtf_tile_id(T1, T2, nt) * 12 * 256;
+    for (int e = tid; e < 12 * 256; e += kKayThreads) ks[e] = (&acc[0][0])[e];
+  }
 }
 
-// The final sum of a QTF pair tile: the GEMM part k_qtf_gemm wrote plus the Kim & Yue part
-// k_qtf_kay left in the workspace (the same addition, in the same order, as when k_qtf_kay
-// finished the tile itself), then the Hermitian fill (raft/raft_fowt.py:1639-1640).
-__global__ __launch_bounds__(256) void k_qtf_kay_sum(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf,
-                                                     int rank, int nrank, int mirror) {
-  const int tid = (int)threadIdx.x;
-  const int n2 = q.n2, n2p = qtf_n2p(q), nt = n2p / 16;
-  int T1 = 0, t = rank + nrank * xcd_remap((int)blockIdx.x, (int)gridDim.x);
-  while (t >= nt - T1) {   // block-uniform
+// tile (T1, T2) of the t-th upper-triangle tile in row-major order (block-uniform)
+__device__ __forceinline__ void qtf_tile_of(int t, int nt, int& T1, int& T2) {
+  T1 = 0;
+  while (t >= nt - T1) {
     t -= nt - T1;
     ++T1;
   }
-  const int T2 = T1 + t;
-  const int i1b = 16 * T1, i2b = 16 * T2;
-  const double* ks = wk.KS + (size_t)qtf_tile_id(T1, T2, nt) * 12 * 256;
-  // one pair per thread
-  const int a1 = i1b + (tid >> 4), a2 = i2b + (tid & 15);
-  if (a1 >= n2 || a2 >= n2 || a2 < a1) return;
-  const int e = ((tid >> 4) & 3) * 16 + (tid & 15) + 64 * (tid >> 6);   // element index of pair (a1, a2)
-  rh_c128* up = qtf + ((size_t)a1 * n2 + a2) * 6;
-  rh_c128* lo = qtf + ((size_t)a2 * n2 + a1) * 6;
-#pragma unroll
-  for (int d = 0; d < 6; ++d) {
-    const cd Qd = add(ld(up + d), mk(ks[(2 * d) * 256 + e], ks[(2 * d + 1) * 256 + e]));
-    if (!mirror) {
-      st(up + d, Qd);
-    } else if (a1 == a2) {   // qtf + conj(qtf).T - diag(conj(diag(qtf))) (:1639-1640)
-      st(up + d, sub(add(Qd, cconj(Qd)), cconj(Qd)));
-    } else {
-      st(up + d, Qd);
-      st(lo + d, cconj(Qd));
-    }
-  }
+  T2 = T1 + t;
+}
+
+// The w1-side GEMM coefficients: grid (ceil(n2p / 64), 18 + nq + nmq), 512 threads (lcoef_block).
+__global__ __launch_bounds__(512) void k_qtf_lcoef(rh_qtf_design q, QtfWork wk, const double* __restrict__ M66) {
+  __shared__ double red[8][12][64];
+  lcoef_block(q, wk, M66, (int)blockIdx.x, (int)blockIdx.y, red);
+}
+
+#ifndef RH_KAY_WPE
+#define RH_KAY_WPE 2
+#endif
+// The Kim & Yue sums of this rank's pair tiles (kay_tile), one tile per workgroup; the GEMM
+// epilogue adds them (before round 4 this kernel ran on a second stream beside k_qtf_lcoef +
+// k_qtf_gemm, with two event hand-offs and a final k_qtf_kay_sum launch).
+__global__ __launch_bounds__(kKayThreads) __attribute__((amdgpu_waves_per_eu(RH_KAY_WPE))) void k_qtf_kay(
+    rh_qtf_design q, QtfWork wk, int rank, int nrank) {
+  __shared__ double acc[12][256];
+  int T1, T2;
+  qtf_tile_of(rank + nrank * xcd_remap((int)blockIdx.x, (int)gridDim.x), qtf_n2p(q) / 16, T1, T2);
+  kay_tile(q, wk, T1, T2, true, (int)threadIdx.x, acc);
 }
 
 }  // namespace rh
