@@ -706,13 +706,10 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   if (!gemm) wk.R = nullptr;                                 // the table kernels skip the GEMM operands
   const int n2p = rh::qtf_n2p(*q);
   const int nb = (n2p + 63) / 64;
-  hipLaunchKernelGGL(rh::k_qtf_freq, dim3(nb), dim3(64), 0, s, *q, nw, w, Xi0, M66, wk);
+  // the frequency row, node, waterline and KAY tables (+ GEMM basis and zero K tails): one launch
+  const int trows = 1 + q->nq + q->nmq + q->nkr + (gemm ? q->nq + rh::qtf_npad(*q) : 0);
+  hipLaunchKernelGGL(rh::k_qtf_tables, dim3(nb, trows), dim3(64), 0, s, *q, wk, nw, w, Xi0, M66);
   RH_HIP(hipGetLastError());
-  const int trows = q->nq + q->nmq + q->nkr + (gemm ? q->nq + rh::qtf_npad(*q) : 0);
-  if (trows > 0) {   // node, waterline and KAY tables (+ GEMM basis and zero K tails): one launch
-    hipLaunchKernelGGL(rh::k_qtf_tables, dim3(nb, trows), dim3(64), 0, s, *q, wk);
-    RH_HIP(hipGetLastError());
-  }
   if (gemm) {
     // the w1-side GEMM coefficients, the Kim & Yue tile sums (both need only the tables), then
     // the pair tiles: bilinear + potential GEMMs plus the Kim & Yue sums, and the Hermitian fill

@@ -1,9 +1,9 @@
 // rh_qtf.hip -- slender-body second-order QTF on gfx950.
 //
-//   k_qtf_freq   : per second-order frequency: RAO resampled from the first-order grid
+//   k_qtf_tables : one launch of every per-frequency table kind:
+//   qtf_freq_at  : per second-order frequency: RAO resampled from the first-order grid
 //                  (np.interp, left=right=0, raft/raft_fowt.py:1415-1417), first-order force
 //                  F1st = M a (:1437-1439), rotation generator i w theta (:1556-1557)
-//   k_qtf_tables : one launch of the three per-frequency table kinds below:
 //   qtf_nodes_at : per (node, frequency): incident velocity u, node displacement/velocity,
 //                  grad u (raft/helpers.py:157-195), grad p (:202-225), axial projections
 //   qtf_wl_at    : per (member, frequency): waterline kinematics (raft/raft_fowt.py:1486-1502)
@@ -152,18 +152,13 @@ __device__ __forceinline__ void acc6(cd* Q, const cd* f, double rx, double ry, d
 }
 
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_qtf_freq(rh_qtf_design q, int nw, const double* __restrict__ w,
-                                                  const rh_c128* __restrict__ Xi0, const double* __restrict__ M66,
-                                                  QtfWork wk) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n2 = q.n2;
-  if (f >= n2) {
-    if (wk.R && f < qtf_n2p(q)) qtf_glob_basis(q, wk, f, nullptr);   // zero padding of the GEMM operands
-    return;
-  }
+// The RAO at second-order frequency f: np.interp(w2[f], w, Xi0[d], left=0, right=0)
+// (raft/raft_fowt.py:1415-1417).  Every table row that needs it evaluates it itself (a binary
+// search over the first-order grid), so no row waits for another.
+__device__ __forceinline__ void qtf_resample(const rh_qtf_design& q, int nw, const double* __restrict__ w,
+                                             const rh_c128* __restrict__ Xi0, int f, cd (&X)[6]) {
   const double x = q.w2[f];
-  cd X[6];
-  // np.interp(x, w, Xi0[d], left=0, right=0): j with w[j] <= x < w[j+1]
+  // j with w[j] <= x < w[j+1]
   if (x < w[0] || x > w[nw - 1]) {
 #pragma unroll
     for (int d = 0; d < 6; ++d) X[d] = mk(0, 0);
@@ -184,6 +179,22 @@ __global__ __launch_bounds__(64) void k_qtf_freq(rh_qtf_design q, int nw, const 
       X[d] = mk(sr * (x - w[lo]) + a.r, si * (x - w[lo]) + a.i);
     }
   }
+}
+
+// per second-order frequency: the resampled RAO, the first-order force F1st = M a
+// (:1437-1439) and the rotation generator i w theta (:1556-1557), and the motion rows of the
+// GEMM basis (the frequency row of k_qtf_tables)
+__device__ __forceinline__ void qtf_freq_at(const rh_qtf_design& q, int nw, const double* __restrict__ w,
+                                            const rh_c128* __restrict__ Xi0, const double* __restrict__ M66,
+                                            const QtfWork& wk, int f) {
+  const int n2 = q.n2;
+  if (f >= n2) {
+    if (wk.R && f < qtf_n2p(q)) qtf_glob_basis(q, wk, f, nullptr);   // zero padding of the GEMM operands
+    return;
+  }
+  const double x = q.w2[f];
+  cd X[6];
+  qtf_resample(q, nw, w, Xi0, f, X);
   const double m2 = -(x * x);
   cd A[6];
 #pragma unroll
@@ -231,15 +242,12 @@ __device__ __forceinline__ void airy_u(double w, double k, double beta, double h
   if (eta_out) *eta_out = scl(e, c_ch);   // pDyn with rho = g = 1 (raft/raft_fowt.py:1493)
 }
 
-__device__ __forceinline__ void qtf_nodes_at(const rh_qtf_design& q, const QtfWork& wk, int f, int n) {
+__device__ __forceinline__ void qtf_nodes_at(const rh_qtf_design& q, const QtfWork& wk, int f, int n, const cd (&X)[6]) {
   const int n2 = q.n2;
   if (f >= n2) return;
   const double w = q.w2[f], k = q.k2[f], h = q.depth, beta = q.beta;
   const double x = qn(q, RH_QN_RX, n), y = qn(q, RH_QN_RY, n), z = qn(q, RH_QN_RZ, n);
   const double qv[3] = {qn(q, RH_QN_QX, n), qn(q, RH_QN_QY, n), qn(q, RH_QN_QZ, n)};
-  cd X[6];
-#pragma unroll
-  for (int d = 0; d < 6; ++d) X[d] = ld(wk.freq + (size_t)(FT_XI + d) * n2 + f);
   // getKinematics at the node (raft/helpers.py:95-97): dr = Xi[:3] + th x r ; v = i w dr
   cd dr[3];
   dr[0] = add(X[0], add(scl(X[5], -y), scl(X[4], z)));
@@ -322,14 +330,11 @@ __device__ __forceinline__ void qtf_nodes_at(const rh_qtf_design& q, const QtfWo
   st(T + (size_t)QT_DWDZ * n2, dwdz);
 }
 
-__device__ __forceinline__ void qtf_wl_at(const rh_qtf_design& q, const QtfWork& wk, int f, int m) {
+__device__ __forceinline__ void qtf_wl_at(const rh_qtf_design& q, const QtfWork& wk, int f, int m, const cd (&X)[6]) {
   const int n2 = q.n2;
   if (f >= n2) return;
   rh_c128* T = wk.wl + (size_t)m * WT_COUNT * n2 + f;
   const double w = q.w2[f], k = q.k2[f];
-  cd X[6];
-#pragma unroll
-  for (int d = 0; d < 6; ++d) X[d] = ld(wk.freq + (size_t)(FT_XI + d) * n2 + f);
   cd eta = mk(0, 0), ud[3] = {mk(0, 0), mk(0, 0), mk(0, 0)}, dr2 = mk(0, 0), a[3] = {mk(0, 0), mk(0, 0), mk(0, 0)};
   if (qm(q, RH_QM_WL, m) != 0.0) {
     const double x = qm(q, RH_QM_RIX, m), y = qm(q, RH_QM_RIY, m), z = qm(q, RH_QM_RIZ, m);
@@ -415,19 +420,34 @@ __global__ __launch_bounds__(64) void k_qtf_hankel(int n2, const double* __restr
 // k_qtf_tables: every per-(node | waterline member | KAY row, frequency) table in one launch
 // (blockIdx.y = node, then member, then KAY row), after k_qtf_freq.  One launch instead of
 // three small ones whose grids (a few hundred waves each) left the GPU mostly idle.
-__global__ __launch_bounds__(64) void k_qtf_tables(rh_qtf_design q, QtfWork wk) {
-  // blockIdx.y: node tables, waterline tables, KAY tables; on the MFMA path also the node
-  // GEMM basis and the zero K-tail rows, as rows of their own (more waves in flight)
+__global__ __launch_bounds__(64) void k_qtf_tables(rh_qtf_design q, QtfWork wk, int nw, const double* __restrict__ w,
+                                                    const rh_c128* __restrict__ Xi0, const double* __restrict__ M66) {
+  // blockIdx.y: the frequency row (k_qtf_freq before round 4), node tables, waterline tables,
+  // KAY tables; on the MFMA path also the node GEMM basis and the zero K-tail rows, as rows of
+  // their own (more waves in flight)
   const int f = blockIdx.x * 64 + threadIdx.x;
   const bool basis = wk.R != nullptr && f < qtf_n2p(q);   // MFMA path operands (zero padded to n2p)
   int y = blockIdx.y;
+  if (y == 0) {
+    qtf_freq_at(q, nw, w, Xi0, M66, wk, f);
+    return;
+  }
+  y -= 1;
   if (y < q.nq) {
-    qtf_nodes_at(q, wk, f, y);
+    if (f < q.n2) {
+      cd X[6];
+      qtf_resample(q, nw, w, Xi0, f, X);
+      qtf_nodes_at(q, wk, f, y, X);
+    }
     return;
   }
   y -= q.nq;
   if (y < q.nmq) {
-    qtf_wl_at(q, wk, f, y);
+    if (f < q.n2) {
+      cd X[6];
+      qtf_resample(q, nw, w, Xi0, f, X);
+      qtf_wl_at(q, wk, f, y, X);
+    }
     if (basis) qtf_wl_basis(q, wk, f, y);
     return;
   }
