@@ -94,7 +94,7 @@ def solve_kernel_name(nw):
         return f"rh::k_solve_lds<{1 if nw <= 128 else 2}, 128, true>"
     if nw <= 1024:
         return f"rh::k_solve_lds<{1 if nw <= 512 else 2}, 512, false>"
-    return "rh::k_solve_cases<4>"
+    return "rh::k_solve_cases<8>"      # nw <= 2048 (check_design); 256 threads x 8 bins
 
 
 def flops_per_case(n_loop, nw, nc, nr, nsub):
