@@ -1,0 +1,156 @@
+// rh_a0.hip -- k_a0_sums: phase A of the first drag iteration of a whole batch, as FP64 MFMA GEMMs.
+//
+// A case that starts from XiStart (no Xi_init, first_iter 0) enters iteration 0 with
+// XiLast = XiStart in every DOF and bin (raft/raft_model.py:882).  Its body-motion terms in the
+// phase-A sums of k_solve_lds (rh_solve.hip; raft/raft_fowt.py:1205-1211) are then the same for
+// every case of a design: per node n and projection p (row j = 3 n + p) the relative velocity is
+//     s_j(b) = z_b K_j(b) - i w_b beta_j,
+//     beta_q = XiStart sum_c cq_c,  beta_1 = XiStart (sum_c c1_c + t sum_{c<3} c2_c),
+//     beta_2 = XiStart (sum_c c2_c - t sum_{c<3} c1_c)
+// (cq, c1, c2 the member factors of the node's member, t its axial coordinate), and
+//     sum_b |s_j(b)|^2 = sum_b z_b^2 |K_j(b)|^2 - 2 beta_j sum_b z_b w_b Im K_j(b) + beta_j^2 sum_b w_b^2.
+// The first two sums are, for the cases of one (design, heading), the product of a
+// [case x bin] matrix (z^2 | z w) with a [bin x row] matrix (|K|^2 | -2 beta Im K): a GEMM that
+// reads each wave-table entry once per 16 cases instead of once per case.  k_solve_lds then
+// skips phase A of iteration 0 and takes these sums in phase B.  The bin sums are grouped
+// differently from phase A's per-lane / butterfly order, so the two agree to rounding (the
+// three terms have no cancellation to speak of: the XiStart motion term dominates most rows,
+// and z^2 |K|^2 rows with beta = 0 are sums of squares).
+//
+// Launch: grid (ceil(ncase / 16) case tiles of the launch order, ceil(nw / 128) bin chunks),
+// 256 threads.  A tile's cases are handled one (design, heading) key at a time (a sorted launch
+// order gives one or two keys per tile); each wave takes 16-row blocks of the key's 3 nn rows.
+// Per (case, chunk) the row sums go to the case's Xi_last scratch, which the fast path does not
+// otherwise use: [chunk][3 nn] doubles at the start of the case's [6][nw] complex block.
+#include "rh_device.h"
+
+namespace rh {
+
+constexpr int kA0Cases = 16;       // cases per tile (MFMA rows)
+constexpr int kA0Bins = 128;       // bins per chunk (32 MFMA steps of 4 bins)
+constexpr int kA0Threads = 256;
+constexpr int kA0Pad = kA0Bins + 2;
+
+__host__ __device__ inline int a0_chunks(int nw) { return (nw + kA0Bins - 1) / kA0Bins; }
+// the A(0) sums of a case fit in its Xi_last block ([6][nw] complex = 12 nw doubles)
+__host__ __device__ inline bool a0_fits(int nw, int nn) { return (size_t)a0_chunks(nw) * 3 * nn <= (size_t)12 * nw; }
+__device__ __forceinline__ double* a0_block(const CaseArgs& a, int ic, int nw) {
+  return reinterpret_cast<double*>(a.o.Xi_last + (size_t)ic * 6 * nw);
+}
+
+typedef double a0d4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
+  __shared__ double su[kA0Cases][kA0Pad];   // z^2 of (case, bin of the chunk)
+  __shared__ double sv[kA0Cases][kA0Pad];   // z w
+  __shared__ int kic[kA0Cases], kd[kA0Cases], kh[kA0Cases];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tile = blockIdx.x, chunk = blockIdx.y;
+  const int ncase = a.c.ncase;
+  if (tid < kA0Cases) {
+    const int slot = tile * kA0Cases + tid;
+    const int ic = slot < ncase ? (a.c.order ? a.c.order[slot] : slot) : -1;
+    kic[tid] = ic;
+    kd[tid] = ic >= 0 ? a.c.design[ic] : -1;
+    kh[tid] = ic >= 0 ? a.c.head[ic] : -1;
+  }
+  __syncthreads();
+  const int nw = a.designs[kd[0]].d.nw;   // slot tile*16 < ncase; every design of a launch shares nw
+  const int b0 = chunk * kA0Bins;
+  // wave amplitudes of the tile's cases over the chunk (sea_amplitude, as the solve's prologue)
+  for (int e = tid; e < kA0Cases * kA0Bins; e += kA0Threads) {
+    const int c = e / kA0Bins, bl = e % kA0Bins, b = b0 + bl;
+    const int ic = kic[c];
+    double zz = 0.0, w = 0.0;
+    if (ic >= 0 && b < nw) {
+      const rh_design& d = a.designs[kd[c]].d;
+      w = d.w[b];
+      zz = sea_amplitude(a.c.spectrum[ic], a.c.Hs[ic], a.c.Tp[ic], a.c.gamma[ic], w, d.dw);
+    }
+    su[c][bl] = zz * zz;
+    sv[c][bl] = zz * w;
+  }
+  __syncthreads();
+  const int mr = lane & 15, kr = lane >> 4;
+  const double xs = a.c.XiStart;
+  unsigned done = 0;
+  for (;;) {   // one (design, heading) key of the tile at a time (block-uniform)
+    int first = -1;
+    for (int c = 0; c < kA0Cases; ++c)
+      if (kic[c] >= 0 && !((done >> c) & 1u)) {
+        first = c;
+        break;
+      }
+    if (first < 0) break;
+    const int kdes = kd[first], khead = kh[first];
+    unsigned match = 0;
+    for (int c = 0; c < kA0Cases; ++c)
+      if (kic[c] >= 0 && kd[c] == kdes && kh[c] == khead) match |= 1u << c;
+    done |= match;
+    const rh_design& d = a.designs[kdes].d;
+    const int nn = d.nn, nm = d.nm, nrow = 3 * nn, nrb = (nrow + 15) / 16;
+    if (nn == 0) continue;
+    const unsigned nw16 = (unsigned)nw * 16u;
+    const Buf bK = mkbuf(d.kproj + (size_t)khead * nrow * nw, (unsigned)nrow * nw16);
+    const bool mine = ((match >> mr) & 1u) != 0;   // A row mr belongs to this key
+    double wsq = 0.0;                                // this design's sum of w^2 over the chunk
+#pragma unroll
+    for (int q = 0; q < kA0Bins / 64; ++q) {
+      const int b = b0 + lane + 64 * q;
+      const double w = b < nw ? d.w[b] : 0.0;
+      wsq += w * w;
+    }
+    const double W2 = wave_sum(wsq);
+    for (int rb = wv; rb < nrb; rb += kA0Threads / 64) {
+      const int j = rb * 16 + mr;                    // this lane's row (B column mr)
+      const int jc = j < nrow ? j : nrow - 1;
+      const int n = jc / 3, p = jc - 3 * n;
+      int m = 0;
+      while (m + 1 < nm && d.mstart[m + 1] <= n) ++m;
+      const double t = d.node[RH_NF_T * nn + n];
+      double sq = 0, s1 = 0, s2 = 0, d1 = 0, d2 = 0;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const double cq = d.memb[(RH_MF_CQ0 + c) * nm + m], c1 = d.memb[(RH_MF_C10 + c) * nm + m],
+                     c2 = d.memb[(RH_MF_C20 + c) * nm + m];
+        sq += cq;
+        s1 += c1;
+        s2 += c2;
+        if (c < 3) {
+          d1 += c2;
+          d2 += c1;
+        }
+      }
+      const double beta = xs * (p == 0 ? sq : p == 1 ? s1 + t * d1 : s2 - t * d2);
+      const double m2b = -2.0 * beta;
+      a0d4 acc = {0.0, 0.0, 0.0, 0.0};
+      const unsigned so = (unsigned)jc * nw16;
+      constexpr int kU = 8;   // MFMA steps per batch of loads
+#pragma unroll 1
+      for (int ks0 = 0; ks0 < kA0Bins / 4; ks0 += kU) {
+        cd K[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) K[u] = bld(bK, (unsigned)(b0 + 4 * (ks0 + u) + kr) * 16u, so);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int bl = 4 * (ks0 + u) + kr;
+          const double ua = mine ? su[mr][bl] : 0.0, va = mine ? sv[mr][bl] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, K[u].r * K[u].r + K[u].i * K[u].i, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va, m2b * K[u].i, acc, 0, 0, 0);
+        }
+      }
+      // C[i][j]: lane holds rows i = kr + 4 r (cases) of column j = mr (rows of the table)
+      if (j < nrow) {
+        const double cst = beta * beta * W2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = kr + 4 * r;
+          if ((match >> i) & 1u) a0_block(a, kic[i], nw)[(size_t)chunk * nrow + j] = acc[r] + cst;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace rh

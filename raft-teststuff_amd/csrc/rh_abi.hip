@@ -14,6 +14,7 @@
 #include "rh_kernels.hip"   // single translation unit: kernels + their host launchers
 #include "rh_qtf.hip"
 #include "rh_qtf_mfma.hip"
+#include "rh_a0.hip"
 #include "rh_solve.hip"
 #ifdef RH_VARIANTS
 // Opt-in solve kernels that were measured slower than k_solve_lds on C2: the
@@ -46,6 +47,7 @@ struct rh_ctx {
   int cur = 0;                          // slot of the last staging
   // tuning / cross-check knobs (per context: the ABI has no mutable process globals)
   bool force_general = false;   // rh_set_solver(ctx, 1): always use k_solve_cases (parity cross-checks)
+  bool a0 = true;               // rh_set_a0: iteration-0 phase A of the fast path as a batch GEMM (rh_a0.hip)
 #ifdef RH_VARIANTS
   bool no_group = false;        // rh_set_solver(ctx, 2): ignore group_start (one case per workgroup)
 #ifndef RH_PAIR_ON
@@ -231,6 +233,13 @@ int rh_set_solver(rh_ctx* ctx, int which) {
 }
 
 int rh_group_cases(void) { return kGroupCases; }
+
+int rh_set_a0(rh_ctx* ctx, int on) {
+  if (!ctx) return fail(RH_EINVAL, "rh_set_a0: null context");
+  if (on != 0 && on != 1) return fail(RH_EINVAL, "rh_set_a0: on=%d (0 or 1)", on);
+  ctx->a0 = on != 0;
+  return RH_OK;
+}
 
 int rh_set_qtf_waves(rh_ctx* ctx, int waves) {
   if (!ctx) return fail(RH_EINVAL, "rh_set_qtf_waves: null context");
@@ -425,6 +434,16 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
 #endif
   // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case (256 for nw <= 256), nw <= 1024.
   if (nw <= 2 * rh::kLT && !ctx->force_general) {
+    // Cases that start from XiStart: phase A of iteration 0 for the whole batch as one GEMM
+    // launch (rh_a0.hip), its sums in each case's Xi_last block (unused by the fast path).
+    auto prep_a0 = [&]() -> int {
+      if (!ctx->a0 || cases->first_iter != 0 || cases->Xi_init || !rh::a0_fits(nw, nnmax)) return RH_OK;
+      dim3 g((cases->ncase + rh::kA0Cases - 1) / rh::kA0Cases, rh::a0_chunks(nw));
+      hipLaunchKernelGGL(rh::k_a0_sums, g, dim3(rh::kA0Threads), 0, s, a);
+      RH_HIP(hipGetLastError());
+      a.a0 = 1;
+      return RH_OK;
+    };
 #ifndef RH_SMALL_GRID_128
 #define RH_SMALL_GRID_128 1
 #endif
@@ -437,6 +456,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
       const int nb128 = nw <= rh::kLT / 4 ? 1 : 2;
       const size_t lsm128 = rh::solve_lds_smem(nnmax, nmmax, nb128, rh::kLT / 4, true);
       if (lsm128 <= kMaxLds) {
+        if (int r = prep_a0()) return r;
         dim3 grid(cases->ncase), block(rh::kLT / 4);
         if (nb128 == 1) hipLaunchKernelGGL((rh::k_solve_lds<1, rh::kLT / 4, true>), grid, block, lsm128, s, a);
         else hipLaunchKernelGGL((rh::k_solve_lds<2, rh::kLT / 4, true>), grid, block, lsm128, s, a);
@@ -447,6 +467,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
     const int lt = nw <= rh::kLT / 2 ? rh::kLT / 2 : rh::kLT;   // nw <= 256: 256 threads, two cases per CU
     const size_t lsm = rh::solve_lds_smem(nnmax, nmmax, nb, lt);
     if (lsm <= 160 * 1024) {
+      if (int r = prep_a0()) return r;
       dim3 grid(cases->ncase), block(lt);
       auto kern = lt < rh::kLT ? rh::k_solve_lds<1, rh::kLT / 2> : nb == 1 ? rh::k_solve_lds<1> : rh::k_solve_lds<2>;
 #ifdef RH_VARIANTS

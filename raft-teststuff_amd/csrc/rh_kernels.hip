@@ -408,6 +408,9 @@ struct CaseArgs {
   // (resume = 1) continues only those cases from there.  The default runs one pass.
   int stop_iter = 1 << 30;
   int resume = 0;
+  // 1: k_a0_sums has written every case's iteration-0 phase-A sums to its Xi_last block
+  // (rh_a0.hip); k_solve_lds skips phase A of iteration 0 and reads them in phase B
+  int a0 = 0;
 };
 constexpr int kCaseStopped = 9;   // internal status between the two passes (never returned)
 

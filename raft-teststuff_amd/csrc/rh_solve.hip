@@ -306,6 +306,22 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   PROF_T(tp1);
   PROF_ADD(0, tp1 - tp0);
 
+  // Iteration 0's phase-A sums formed for the whole batch by k_a0_sums (rh_a0.hip): their
+  // chunk sums (in chunk order) take the place of wave 0's partials and the other waves' are 0,
+  // so phase B's wave-order sum returns them unchanged; phase A of that iteration is skipped.
+  bool skip_a = a.a0 != 0 && it0 == 0;   // uniform
+  if (skip_a) {
+    const double* a0s = a0_block(a, ic, nw);
+    const int nch = a0_chunks(nw);
+    for (int e = tid; e < nn * 3; e += LT) {
+      double s = 0;
+      for (int ch = 0; ch < nch; ++ch) s += a0s[(size_t)ch * 3 * nn + e];
+      red[e * LW] = s;
+#pragma unroll
+      for (int w = 1; w < LW; ++w) red[e * LW + w] = 0.0;
+    }
+    __syncthreads();
+  }
   for (int it = it0; it < itend; ++it) {
     PROF_T(ta0);
     PROF_ADD(7, 1);
@@ -426,11 +442,12 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
 #pragma unroll
       for (int r = 0; r < kRingA; ++r) load_node(K[r], r);
       int m = -1, mnext = 0;
-      for (int n = 0; n < nn; n += kRingA) {
+      const int nA = skip_a ? 0 : nn;   // no node steps when iteration 0's sums came from k_a0_sums
+      for (int n = 0; n < nA; n += kRingA) {
 #pragma unroll
         for (int r = 0; r < kRingA; ++r) {
           const int nr = n + r;
-          if (nr < nn) {
+          if (nr < nA) {
             if (nr == mnext) {   // uniform: entering member m+1 (members are node-contiguous)
               do { ++m; mnext = mstart[m + 1]; } while (mnext == nr);
               member_terms(m);
@@ -450,6 +467,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       }
 #endif
     }
+    skip_a = false;
     __syncthreads();
     PROF_T(ta1);
     PROF_ADD(1, ta1 - ta0);

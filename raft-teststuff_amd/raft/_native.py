@@ -111,6 +111,7 @@ def lib():
                                         ctypes.c_int, _p, _p, ctypes.c_longlong, _p],
                 "rh_qtf_hermitian_fill": [_p, ctypes.c_int, _p, _p],
                 "rh_set_solver": [_p, ctypes.c_int],
+                "rh_set_a0": [_p, ctypes.c_int],
                 "rh_set_qtf_waves": [_p, ctypes.c_int],
                 "rh_set_qtf_path": [_p, ctypes.c_int],
                 "rh_qtf_hankel": [_p, ctypes.c_int, _p, ctypes.c_int, _p, _p, _p],

@@ -2,7 +2,8 @@
 (max 0.2 Hz), 512 seeded JONSWAP cases, the default dispatch (k_solve_lds for nw <= 1024, the
 general kernel k_solve_cases beyond).  Prints the kernel that ran, ms per launch (HIP events
 over 10 launches), mean iterations and the SURVEY.md §8(d) roofline fraction.
-usage: python tools/ubench/time_grid.py NW [NW ...]"""
+usage: python tools/ubench/time_grid.py NW[:noa0] [...]   (":noa0": rh_set_a0(ctx, 0) for that run,
+every case forming its iteration-0 phase-A sums in its own workgroup)"""
 import os
 import sys
 
@@ -13,7 +14,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "raft-teststuff_amd"))
 
 
-def run(nw):
+def run(nw, a0=True):
     import json
     import torch
     import bench
@@ -33,6 +34,8 @@ def run(nw):
     cs = CaseSet(np.zeros(len(cases), dtype=np.int32), [c["wave_heading"] for c in cases], ["JONSWAP"] * len(cases),
                  [c["wave_height"] for c in cases], [c["wave_period"] for c in cases], [0.0] * len(cases))
     prep = prepare_batch([dd], cs)
+    from raft import _native as N
+    N.check(N.lib().rh_set_a0(N.context(0), int(a0)), "rh_set_a0")
     want = ("psd", "std", "zeta", "rao")
     for _ in range(3):
         res = solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=want, prepared=prep)
@@ -49,10 +52,11 @@ def run(nw):
     nc, nr = int((circ != 0).sum()), int((circ == 0).sum())
     flops = float(sum(bench.flops_per_case(int(n), dd.nw, nc, nr, dd.nn) for n in iters))
     frac = flops / (ms * 1e-3) / bench.PEAK_FP64
-    print(f"nw={dd.nw:5d} {bench.solve_kernel_name(dd.nw):36s} {ms:8.3f} ms/launch  iters {iters.mean():.2f}  "
+    N.check(N.lib().rh_set_a0(N.context(0), 1), "rh_set_a0")
+    print(f"nw={dd.nw:5d} a0={int(a0)} {bench.solve_kernel_name(dd.nw):36s} {ms:8.3f} ms/launch  iters {iters.mean():.2f}  "
           f"{512 / (ms * 1e-3):.3e} cases/s  frac {frac:.3f}", flush=True)
 
 
 if __name__ == "__main__":
     for a in sys.argv[1:]:
-        run(int(a))
+        run(int(a.split(":")[0]), not a.endswith(":noa0"))
