@@ -2,9 +2,12 @@
 reference's per-node/per-bin loop structure) against the reference itself on the same four C2
 golden cases (tests/golden/c2_nw1000.npz: VolturnUS-S, nw = 1000), one core each.  The
 reference's per-case seconds were recorded while it generated the fixture (out_seconds,
-tests/golden/make_golden.py run_solve).  Prints one line per case and the mean ratio."""
+tests/golden/make_golden.py run_solve).  Prints one line per case and the mean ratio.
+--interleave: time the reference again here, case by case beside the port (tools/ref_time_c2.py in
+a child process with make_golden.py's reference environment), so both see the same machine load."""
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -18,18 +21,34 @@ from conftest import golden_cases  # noqa: E402
 from oracle import raft_oracle as O  # noqa: E402
 
 
+def reference_seconds(ic):
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1",
+               PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "tests", "golden", "refshim"), "/root/reference",
+                                           os.path.join(ROOT, "tests", "golden")]))
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ref_time_c2.py"), str(ic)], env=env,
+                       capture_output=True, text=True, check=True, cwd=ROOT)
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    return float(r["reference_s"]), int(r["iters"])
+
+
 def main():
+    interleave = "--interleave" in sys.argv
     T = dict(np.load(os.path.join(ROOT, "tests", "golden", "c2_nw1000.npz")))
     out = []
     for ic, case in enumerate(golden_cases(T)):
+        if interleave:
+            ref, its = reference_seconds(ic)
+            assert its == T["out_iters"][ic]
         t0 = time.perf_counter()
         r = O.solve_dynamics(T, dict(case), int(T["nIter"]), float(T["XiStart"]), loop=True)
         dt = time.perf_counter() - t0
-        ref = float(T["out_seconds"][ic])
+        if not interleave:
+            ref = float(T["out_seconds"][ic])
         assert r["iters"] == T["out_iters"][ic]
         out.append(dict(case=ic, port_s=dt, reference_s=ref, ratio=dt / ref))
         print(f"case {ic}: port {dt:6.1f} s  reference {ref:6.1f} s  ratio {dt / ref:5.2f}", flush=True)
-    print(json.dumps({"cases": out, "mean_ratio": float(np.mean([o["ratio"] for o in out]))}))
+    print(json.dumps({"cases": out, "interleaved": interleave,
+                      "mean_ratio": float(np.mean([o["ratio"] for o in out]))}))
 
 
 if __name__ == "__main__":
