@@ -194,11 +194,17 @@ def cpu_baselines(qtf_seconds=10.0):
     case = {"value": P / dt, "unit": "cases/s", "cores": P, "kind": "port",
             "sample": f"{P} C2 cases (nw=1000, seeded JONSWAP) through oracle/raft_oracle.py loop=True (the "
                       f"reference's per-node/per-bin loop structure), one per single-threaded process on {P} "
-                      f"cores ({cores_note}), {dt:.1f} s wall, {per_case:.1f} s/case/core; CPU {model}"}
+                      f"cores ({cores_note}), {dt:.1f} s wall, {per_case:.1f} s/case/core; CPU {model}",
+            "calibration": "port / reference time 0.84-1.11 (mean 0.99) on the four C2 golden cases, one core, the "
+                           "reference re-timed case by case beside the port (tools/calibrate_cpu.py --interleave, "
+                           "profiles/r04_v2/calibrate_cpu_interleaved.txt)"}
     qtf = {"value": npairs / dq, "unit": "pairs/s", "cores": P, "kind": "port",
            "sample": f"{npairs} pairs (24-frequency subsets of the C3 400 grid) through oracle/qtf_oracle.py "
                      f"(vectorised over pairs, faster per pair than the reference's 19-23 ms) on {P} cores, "
-                     f"{dq:.1f} s wall ({cores_note}); CPU {model}"}
+                     f"{dq:.1f} s wall ({cores_note}); CPU {model}",
+           "calibration": "uncalibrated, faster than the reference: the port is vectorised over pairs (about 1 "
+                          "ms/pair/core against the reference's per-pair loops at 19-23 ms/pair/core, BASELINE.md), "
+                          "so this baseline overstates the reference's CPU rate about 20x"}
     return case, qtf
 
 
