@@ -32,13 +32,25 @@ PEAK_FP64 = 78.6e12   # MI355X FP64 dense peak (vector = matrix rate), FLOP/s
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_v3", "pmc_summary.json")
 
 
-def pmc_traffic(*kernels):
-    """HBM traffic (bytes per call) summed over the kernels named in `kernels` (one launch
-    each per call) from PMC_SUMMARY, or None if any of them is missing."""
+def pmc_section(workload):
+    """The per-kernel PMC records of one workload ("solve", "qtf", "c4") from PMC_SUMMARY
+    (a summary with one section per workload, tools/gpu_pmc_r04.sh; older flat summaries
+    serve every workload), or None."""
     try:
         with open(PMC_SUMMARY) as fh:
             d = json.load(fh)
     except (OSError, ValueError):
+        return None
+    if all(k in ("solve", "qtf", "c4") for k in d):
+        return d.get(workload)
+    return d
+
+
+def pmc_traffic(workload, *kernels):
+    """HBM traffic (bytes per call) summed over the kernels named in `kernels` (one launch
+    each per call) from the `workload` section of PMC_SUMMARY, or None if any is missing."""
+    d = pmc_section(workload)
+    if d is None:
         return None
     total = 0.0
     for kernel in kernels:
@@ -70,12 +82,10 @@ L2_PEAK = 49.5e12
 
 
 def pmc_l2(kernel, kernel_ms):
-    """L2 request traffic of `kernel` per launch from PMC_SUMMARY: (TCC_HIT + TCC_MISS) x 128 B
-    and its rate over the measured launch time, or None."""
-    try:
-        with open(PMC_SUMMARY) as fh:
-            d = json.load(fh)
-    except (OSError, ValueError):
+    """L2 request traffic of `kernel` per launch from PMC_SUMMARY (C2 section): (TCC_HIT +
+    TCC_MISS) x 128 B and its rate over the measured launch time, or None."""
+    d = pmc_section("solve")
+    if d is None:
         return None
     for name, v in d.items():
         c = v.get("counters", {})
@@ -86,6 +96,13 @@ def pmc_l2(kernel, kernel_ms):
                     "peak_note": "measured stream ceiling of this access pattern (tools/ubench/l2_stream.hip)",
                     "hit_rate": c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])}
     return None
+
+
+def solve_kernels(nw):
+    """Every kernel one rh_solve_cases call launches for this grid: on the fast path the
+    iteration-0 GEMM k_a0_sums (rh_a0.hip, cases starting from XiStart) before the solve."""
+    name = solve_kernel_name(nw)
+    return ("rh::k_a0_sums", name) if "k_solve_lds" in name else (name,)
 
 
 def solve_kernel_name(nw):
@@ -362,7 +379,7 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
                       "parallelism": f"tile-sharded x{world} + all-gather of packed pairs"},
            "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                         "frac": achieved / PEAK_FP64,
-                        "traffic": pmc_traffic("k_qtf_freq", "k_qtf_tables", "k_qtf_lcoef", "k_qtf_gemm", "k_qtf_kay", "k_qtf_kay_sum"),
+                        "traffic": pmc_traffic("qtf", "k_qtf_tables", "k_qtf_lcoef", "k_qtf_kay", "k_qtf_gemm"),
                         "kernel": "rh_qtf_slender%s: k_qtf_freq, k_qtf_tables, k_qtf_lcoef, k_qtf_gemm, k_qtf_kay (second "
                                   "stream), k_qtf_kay_sum (every launch of a QTF on this rank)" % ("_rows" if world > 1 else ""),
                         "kernel_ms": ms, "flops_per_pair": fpp, "pairs_this_rank": mine,
@@ -435,11 +452,15 @@ def bench_c4(device, steps, world, rank, dist, ncase=512):
                        "cases_per_step_per_gpu": ncase, "nw": dd.nw, "fowts": len(m.fowtList),
                        "parallelism": f"case-sharded x{world}"},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP64, "traffic": pmc_traffic(solve_kernel_name(dd.nw)),
-                         "kernel": solve_kernel_name(dd.nw),
+                         "frac": achieved / PEAK_FP64, "traffic": pmc_traffic("c4", *solve_kernels(dd.nw)),
+                         "kernel": solve_kernel_name(dd.nw), "kernels_timed": list(solve_kernels(dd.nw)),
+                         "chain_traffic": pmc_traffic("c4", *solve_kernels(dd.nw), "rh::k_array_resp<2>",
+                                                      "rh::k_motion_stats"),
                          "kernel_ms": kern_ms, "flops_per_launch": flops,
-                         "note": "the (case, FOWT) drag fixed-point launch; SURVEY.md §8(d) formula per (case, FOWT); "
-                                 "traffic = HBM bytes per launch from " + os.path.relpath(PMC_SUMMARY, ROOT)}}
+                         "note": "the (case, FOWT) drag fixed point (kernels_timed); SURVEY.md §8(d) formula per "
+                                 "(case, FOWT); traffic = HBM bytes of those launches, chain_traffic = of the whole "
+                                 "step (fixed point, array response, motion statistics) from "
+                                 + os.path.relpath(PMC_SUMMARY, ROOT)}}
 
 
 C5_DESIGNS = 250
@@ -757,14 +778,16 @@ def main():
                    "nodes_circ_rect": [nc, nr], "nIter": int(m.nIter), "headings": len(dd.headings),
                    "parallelism": f"case-sharded x{world}"},
         "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_FP64, "traffic": pmc_traffic(solve_kernel_name(dd.nw)),
+                     "frac": achieved / PEAK_FP64, "traffic": pmc_traffic("solve", *solve_kernels(dd.nw)),
                      "l2": pmc_l2(solve_kernel_name(dd.nw), kern_ms),
-                     "kernel": solve_kernel_name(dd.nw), "kernel_ms": kern_ms,
+                     "kernel": solve_kernel_name(dd.nw), "kernels_timed": list(solve_kernels(dd.nw)),
+                     "kernel_ms": kern_ms,
                      "wave_tables_ms": tab_ms,
                      "flops_per_launch": flops,
                      "note": "FP64 VALU bound (no MFMA, DESIGN.md §4; peak = MI355X FP64 vector rate); algorithmic "
-                             "FLOPs from SURVEY.md §8(d) over the solve launch (HIP events on its stream); traffic = "
-                             "HBM bytes per launch from " + os.path.relpath(PMC_SUMMARY, ROOT)},
+                             "FLOPs from SURVEY.md §8(d) over the solve call's launches (kernels_timed, HIP events on "
+                             "their stream); traffic = HBM bytes of those launches from "
+                             + os.path.relpath(PMC_SUMMARY, ROOT)},
         "iterations_mean": float(iters.mean()),
         "converged_frac": float((status == 1).mean()),
     }

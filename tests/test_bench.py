@@ -43,3 +43,28 @@ def test_host_cores_respects_affinity():
     import bench
     P, note = bench.host_cores()
     assert 1 <= P <= len(os.sched_getaffinity(0)) and "affinity" in note
+
+
+def test_pmc_lookup_sections_and_exact_names(tmp_path, monkeypatch):
+    """pmc_traffic reads the workload's section of a sectioned summary (tools/gpu_pmc_r04.sh),
+    sums exactly the named kernels (k_qtf_kay is not k_qtf_kay_sum), and returns None when a
+    named kernel is absent; a flat (older) summary serves every workload."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    rec = lambda r, w: {"hbm_read_bytes_corrected": r, "hbm_write_bytes": w}   # noqa: E731
+    sec = {"solve": {"rh::k_a0_sums(rh::CaseArgs)": rec(1.0, 2.0),
+                     "void rh::k_solve_lds<2, 512, false>(rh::CaseArgs)": rec(10.0, 20.0)},
+           "c4": {"rh::k_a0_sums(rh::CaseArgs)": rec(100.0, 0.0)},
+           "qtf": {"rh::k_qtf_kay(rh_qtf_design, rh::QtfWork)": rec(5.0, 5.0),
+                   "rh::k_qtf_kay_sum(rh_qtf_design, rh::QtfWork)": rec(7.0, 7.0)}}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps(sec))
+    monkeypatch.setattr(bench, "PMC_SUMMARY", str(p))
+    assert bench.pmc_traffic("solve", *bench.solve_kernels(1000)) == 33.0
+    assert bench.pmc_traffic("c4", "rh::k_a0_sums") == 100.0
+    assert bench.pmc_traffic("qtf", "k_qtf_kay") == 10.0
+    assert bench.pmc_traffic("c4", *bench.solve_kernels(240)) is None
+    p.write_text(json.dumps(sec["solve"]))
+    assert bench.pmc_traffic("qtf", "rh::k_a0_sums") == 3.0
+    assert bench.solve_kernels(2000) == ("rh::k_solve_cases<8>",)
