@@ -64,9 +64,9 @@ def pmc_traffic(workload, *kernels):
 
 def kernel_name_is(name, kernel):
     """Whether the demangled rocprof kernel `name` ("rh::k_qtf_kay(rh_qtf_design, ...)" or
-    "void rh::k_solve_lds<2, 512, false>(rh::CaseArgs)") is `kernel` exactly (a namespace-
+    "void rh::k_solve_lds<2, 512, false, 1>(rh::CaseArgs)") is `kernel` exactly (a namespace-
     qualified or bare name, template arguments included when `kernel` has them): k_qtf_kay
-    does not match k_qtf_kay_sum, k_solve_lds<2, 512 does not match k_solve_lds<2, 512, false>."""
+    does not match k_qtf_kay_sum, k_solve_lds<2, 512, false does not match k_solve_lds<2, 512, false, 1>."""
     base = name.split("(")[0].strip()
     if base.startswith("void "):
         base = base[5:]
@@ -108,10 +108,10 @@ def solve_kernels(nw):
 def solve_kernel_name(nw):
     """The kernel rh_solve_cases launches for this grid (dispatch in rh_abi.hip)."""
     if nw <= 256:
-        return f"rh::k_solve_lds<{1 if nw <= 128 else 2}, 128, true>"
+        return f"rh::k_solve_lds<{1 if nw <= 128 else 2}, 128, true, 1>"
     if nw <= 1024:
-        return f"rh::k_solve_lds<{1 if nw <= 512 else 2}, 512, false>"
-    return "rh::k_solve_cases<8>"      # nw <= 2048 (check_design); 256 threads x 8 bins
+        return f"rh::k_solve_lds<{1 if nw <= 512 else 2}, 512, false, 1>"
+    return "rh::k_solve_lds<2, 512, false, 2>"      # nw <= 2048 (check_design): two passes, XiLast in Xi_last
 
 
 def flops_per_case(n_loop, nw, nc, nr, nsub):

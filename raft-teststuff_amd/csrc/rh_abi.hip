@@ -432,18 +432,18 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
     }
   }
 #endif
+  // Cases that start from XiStart: phase A of iteration 0 for the whole batch as one GEMM
+  // launch (rh_a0.hip), its sums in each case's Xi_last block (k_solve_lds reads them first).
+  auto prep_a0 = [&]() -> int {
+    if (!ctx->a0 || cases->first_iter != 0 || cases->Xi_init || !rh::a0_fits(nw, nnmax)) return RH_OK;
+    dim3 g((cases->ncase + rh::kA0Cases - 1) / rh::kA0Cases, rh::a0_chunks(nw));
+    hipLaunchKernelGGL(rh::k_a0_sums, g, dim3(rh::kA0Threads), 0, s, a);
+    RH_HIP(hipGetLastError());
+    a.a0 = 1;
+    return RH_OK;
+  };
   // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case (256 for nw <= 256), nw <= 1024.
   if (nw <= 2 * rh::kLT && !ctx->force_general) {
-    // Cases that start from XiStart: phase A of iteration 0 for the whole batch as one GEMM
-    // launch (rh_a0.hip), its sums in each case's Xi_last block (unused by the fast path).
-    auto prep_a0 = [&]() -> int {
-      if (!ctx->a0 || cases->first_iter != 0 || cases->Xi_init || !rh::a0_fits(nw, nnmax)) return RH_OK;
-      dim3 g((cases->ncase + rh::kA0Cases - 1) / rh::kA0Cases, rh::a0_chunks(nw));
-      hipLaunchKernelGGL(rh::k_a0_sums, g, dim3(rh::kA0Threads), 0, s, a);
-      RH_HIP(hipGetLastError());
-      a.a0 = 1;
-      return RH_OK;
-    };
 #ifndef RH_SMALL_GRID_128
 #define RH_SMALL_GRID_128 1
 #endif
@@ -487,6 +487,16 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
       }
 #endif
       hipLaunchKernelGGL(kern, grid, block, lsm, s, a);
+      return designs_used(ctx, s);
+    }
+  }
+  // 1024 < nw <= 2048: the same kernel in two passes of 1024 bins, XiLast in the Xi_last block
+  // (192 KB at nw = 2048 is beyond the LDS), DESIGN.md §4.
+  if (nw <= 4 * rh::kLT && !ctx->force_general) {
+    const size_t lsm = rh::solve_lds_smem(nnmax, nmmax, 2, rh::kLT, false, 2);
+    if (lsm <= kMaxLds) {
+      if (int r = prep_a0()) return r;
+      hipLaunchKernelGGL((rh::k_solve_lds<2, rh::kLT, false, 2>), dim3(cases->ncase), dim3(rh::kLT), lsm, s, a);
       return designs_used(ctx, s);
     }
   }

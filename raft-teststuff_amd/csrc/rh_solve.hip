@@ -196,16 +196,16 @@ __device__ __forceinline__ double t3to6_block(const double* Bm, double rx, doubl
 
 // Every table the loops read is staged here: a global load inside the node loops would share
 // the vector-memory counter with the prefetched wave-table loads and force them to drain.
-__host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB, int LT = kLT, bool ser = false) {
+__host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB, int LT = kLT, bool ser = false, int NP = 1) {
   const int LW = LT / 64;
-  return sizeof(double) * ((size_t)12 * LT * NB      // XiLast [6][512 NB] complex
+  return sizeof(double) * ((size_t)(NP == 1 ? 12 * LT * NB : 0)   // XiLast [6][512 NB] complex (one pass)
                            + (size_t)(ser && nn * 3 * LW < 27 ? 27 : nn * 3 * LW)   // per-wave node sums (SER: >= 27 entries)
                            + (ser ? (size_t)0 : (size_t)nn * 36)   // per-node B_drag contributions
                            + (size_t)nn * 9           // Bmat
                            + (size_t)nn * 5           // member-factored drag coefficients
                            + (size_t)nn               // node axial coordinate t
                            + (size_t)nm * 18          // member cq, c1, c2
-                           + (size_t)2 * LT * NB     // w and zeta per (padded) bin
+                           + (size_t)2 * LT * NB * NP   // w and zeta per (padded) bin
                            + 36 + 108 + LW * 6 + 36  // B_drag, M|B|C image, std partials, B_lin+B_drag
                            + LW)                     // convergence-margin partials
          + sizeof(int) * ((size_t)nm + 4);            // member node ranges, vote words
@@ -214,7 +214,13 @@ __host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB, int LT 
 // LT threads per case: 512 (8 waves), or 256 for nw <= 256 (two cases per CU; C4 has 240 bins),
 // or 128 (SER: four cases per CU, B_drag summed node-serially per entry instead of through a
 // per-node LDS image, so a workgroup needs about 40 KB of LDS).
-template <int NB, int LT = kLT, bool SER = false>
+// NP > 1 (grids beyond LT NB bins, nw <= 2048): the bins are taken in NP passes of LT NB, and
+// XiLast ([6][nw] complex, 192 KB at nw = 2048) no longer fits the LDS: it lives in the case's
+// Xi_last block, read and written only by the thread that owns the bin.  Phase A loads a pass's
+// XiLast into registers before its node loop (no global load between the ring's wave-table
+// loads) and adds each pass's node sums to the LDS partials in pass order; phase C reads and
+// writes it around each bin's solve.
+template <int NB, int LT = kLT, bool SER = false, int NP = 1>
 __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(CaseArgs a) {
   constexpr int LW = LT / 64;
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -246,9 +252,12 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   const bool has_fx = a.c.fext != nullptr;
   const Buf bFx = mkbuf(has_fx ? a.c.fext + c6 : nullptr, has_fx ? 6u * nw16 : 0u);
 
-  constexpr int NWP = LT * NB;                    // padded bins held in LDS
-  cd* xl = reinterpret_cast<cd*>(smem);            // [6][NWP]
-  double* red = smem + 12 * NWP;                   // [nn*3][LW]
+  constexpr int NWP = LT * NB;                    // padded bins of one pass
+  constexpr int NBT = NB * NP;                     // bins per thread over all passes
+  constexpr bool GX = NP > 1;                      // XiLast in the Xi_last block, not in LDS
+  cd* xl = reinterpret_cast<cd*>(smem);            // [6][NWP] (one pass only)
+  rh_c128* XL = a.o.Xi_last + c6;                  // [6][nw] (GX)
+  double* red = smem + (GX ? 0 : 12 * NWP);        // [nn*3][LW]
   double* bm = red + (SER && nn * 3 * LW < 27 ? 27 : nn * 3 * LW);   // [nn][9]
   double* al = bm + nn * 9;                        // [nn][5]
   double* bd = al + nn * 5;                        // [36]
@@ -258,9 +267,9 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   double* bdn = bsum + 36;                         // [36][nn] (not with SER)
   double* nt = bdn + (SER ? 0 : 36 * nn);          // [nn]
   double* mbf = nt + nn;                           // [18][nm]
-  double* lw = mbf + 18 * nm;                      // [NWP] w per bin (pad bins: w[nw-1])
-  double* lz = lw + NWP;                           // [NWP] zeta per bin (pad bins: 0)
-  double* mred = lz + NWP;                         // [LW] per-wave max of tolCheck
+  double* lw = mbf + 18 * nm;                      // [NP NWP] w per bin (pad bins: w[nw-1])
+  double* lz = lw + NP * NWP;                      // [NP NWP] zeta per bin (pad bins: 0)
+  double* mred = lz + NP * NWP;                    // [LW] per-wave max of tolCheck
   int* mstart = reinterpret_cast<int*>(mred + LW);  // [nm+1]
   int* sflag = mstart + nm + 1;                      // [2] vote words of even / odd iterations
   load_mbc(d, mbc, tid);
@@ -268,47 +277,11 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   for (int e = tid; e < 18 * nm; e += LT) mbf[e] = d.memb[e];   // RH_MF_CQ0..C20 are fields 0..17
   for (int e = tid; e <= nm; e += LT) mstart[e] = d.mstart[e];
   if (tid < 2) sflag[tid] = 0;
-
-  // Per-bin scalars live in LDS, not in registers: nothing per-thread stays live across the
-  // phases, so the register-heavy solve of phase C does not push other values to scratch.
-  // Bin j of this thread is b = tid + 512 j; loads use the clamped bin min(b, nw-1) so no
-  // load is predicated, and pad bins (b >= nw) carry zeta = 0 and XiLast = 0.
-  auto voff = [&](int b) { return (unsigned)(b < nw ? b : nw - 1) * 16u; };
-  {
-    const int spec = a.c.spectrum[ic];
-    const double Hs = a.c.Hs[ic], Tp = a.c.Tp[ic], gam = a.c.gamma[ic];
-    const rh_c128* XI0 = resume ? a.o.Xi_last + c6 : a.c.Xi_init ? a.c.Xi_init + c6 : nullptr;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int b = tid + LT * j;
-      const bool okb = b < nw;
-      const double w = d.w[okb ? b : nw - 1];
-      const double zz = sea_amplitude(spec, Hs, Tp, gam, w, d.dw);
-      lw[b] = w;
-      lz[b] = okb ? zz : 0.0;
-      if (okb && a.o.zeta) a.o.zeta[(size_t)ic * nw + b] = zz;
-#pragma unroll
-      for (int c = 0; c < 6; ++c)
-        xl[c * NWP + b] = okb ? (XI0 ? ld(XI0 + c * nw + b) : mk(a.c.XiStart, 0.0)) : mk(0.0, 0.0);
-    }
-  }
-  rh_c128* Xo = a.o.Xi + c6;
-  rh_c128* XP = a.o.Xi_prev ? a.o.Xi_prev + c6 : nullptr;
-  const double rho = d.rho;
-  const int nloop = a.c.nIter + 1;
-  const double tol = a.c.tol;
-  int status = RH_CASE_NOT_CONVERGED, iters = nloop;
-  // closest call of the convergence test (rh_solve_out.margin); pass 2 continues pass 1's
-  double margin = resume && a.o.margin ? a.o.margin[ic] : INFINITY;
   const int it0 = resume ? stop_iter : a.c.first_iter;
-  const int itend = resume || stop_iter >= nloop ? nloop : stop_iter;
-  __syncthreads();
-  PROF_T(tp1);
-  PROF_ADD(0, tp1 - tp0);
-
   // Iteration 0's phase-A sums formed for the whole batch by k_a0_sums (rh_a0.hip): their
   // chunk sums (in chunk order) take the place of wave 0's partials and the other waves' are 0,
   // so phase B's wave-order sum returns them unchanged; phase A of that iteration is skipped.
+  // (Read before the prologue: with GX the same Xi_last block then receives XiLast.)
   bool skip_a = a.a0 != 0 && it0 == 0;   // uniform
   if (skip_a) {
     const double* a0s = a0_block(a, ic, nw);
@@ -322,6 +295,49 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     }
     __syncthreads();
   }
+
+  // Per-bin scalars live in LDS, not in registers: nothing per-thread stays live across the
+  // phases, so the register-heavy solve of phase C does not push other values to scratch.
+  // Bin j of this thread is b = tid + LT j; loads use the clamped bin min(b, nw-1) so no
+  // load is predicated, and pad bins (b >= nw) carry zeta = 0 and XiLast = 0.
+  auto voff = [&](int b) { return (unsigned)(b < nw ? b : nw - 1) * 16u; };
+  {
+    const int spec = a.c.spectrum[ic];
+    const double Hs = a.c.Hs[ic], Tp = a.c.Tp[ic], gam = a.c.gamma[ic];
+    const rh_c128* XI0 = resume ? a.o.Xi_last + c6 : a.c.Xi_init ? a.c.Xi_init + c6 : nullptr;
+#pragma unroll
+    for (int j = 0; j < NBT; ++j) {
+      const int b = tid + LT * j;
+      const bool okb = b < nw;
+      const double w = d.w[okb ? b : nw - 1];
+      const double zz = sea_amplitude(spec, Hs, Tp, gam, w, d.dw);
+      lw[b] = w;
+      lz[b] = okb ? zz : 0.0;
+      if (okb && a.o.zeta) a.o.zeta[(size_t)ic * nw + b] = zz;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const cd x0 = okb ? (XI0 ? ld(XI0 + c * nw + b) : mk(a.c.XiStart, 0.0)) : mk(0.0, 0.0);
+        if constexpr (GX) {
+          if (okb && !resume) st(XL + c * nw + b, x0);
+        } else {
+          xl[c * NWP + b] = x0;
+        }
+      }
+    }
+  }
+  rh_c128* Xo = a.o.Xi + c6;
+  rh_c128* XP = a.o.Xi_prev ? a.o.Xi_prev + c6 : nullptr;
+  const double rho = d.rho;
+  const int nloop = a.c.nIter + 1;
+  const double tol = a.c.tol;
+  int status = RH_CASE_NOT_CONVERGED, iters = nloop;
+  // closest call of the convergence test (rh_solve_out.margin); pass 2 continues pass 1's
+  double margin = resume && a.o.margin ? a.o.margin[ic] : INFINITY;
+  const int itend = resume || stop_iter >= nloop ? nloop : stop_iter;
+  __syncthreads();
+  PROF_T(tp1);
+  PROF_ADD(0, tp1 - tp0);
+
   for (int it = it0; it < itend; ++it) {
     PROF_T(ta0);
     PROF_ADD(7, 1);
@@ -330,13 +346,27 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     //   Bq = iw cq.Xi, B1 = iw c1.Xi, B2 = iw c2.Xi, E1 = iw p2.th, E2 = -iw p1.th
     // and per node s_q = z Kq - Bq, s_1 = z K1 - (B1 + t E1), s_2 = z K2 - (B2 + t E2)
     // (raft/raft_fowt.py:1205-1211).
-    {
+#pragma unroll 1
+    for (int p = 0; p < NP; ++p) {   // passes of NWP bins (NP == 1: the whole grid)
+      const int pb = tid + NWP * p;  // this thread's first bin of the pass
       unsigned vb[NB];
       double bz[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        vb[j] = voff(tid + LT * j);
-        bz[j] = lz[tid + LT * j];
+        vb[j] = voff(pb + LT * j);
+        bz[j] = lz[pb + LT * j];
+      }
+      cd XR[GX ? NB : 1][6];         // GX: the pass's XiLast, loaded before the node loop
+      if constexpr (GX) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const int b = pb + LT * j, bc = b < nw ? b : nw - 1;
+#pragma unroll
+          for (int c = 0; c < 6; ++c) {
+            const cd v = ld(XL + c * nw + bc);
+            XR[j][c] = b < nw ? v : mk(0.0, 0.0);
+          }
+        }
       }
       cd Bq[NB], B1[NB], B2[NB], E1[NB], E2[NB];
       auto member_terms = [&](int m) {
@@ -349,10 +379,13 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
         }
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-          const int b = tid + LT * j;
+          const int b = pb + LT * j;
           cd X[6];
 #pragma unroll
-          for (int c = 0; c < 6; ++c) X[c] = xl[c * NWP + b];
+          for (int c = 0; c < 6; ++c) {
+            if constexpr (GX) X[c] = XR[j][c];
+            else X[c] = xl[c * NWP + b];
+          }
           cd Aq = mk(0, 0), A1 = mk(0, 0), A2 = mk(0, 0);
 #pragma unroll
           for (int c = 0; c < 6; ++c) {
@@ -408,6 +441,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       // node n + kB as soon as n is summed.
       constexpr int kB = RH_A_BATCH;
       static_assert(3 * kB <= 16, "tbfly16 reduces at most 16 values");
+      static_assert(NP == 1, "RH_A_BATCH: single-pass grids only");
       cd K[kB][3][NB];
 #pragma unroll
       for (int r = 0; r < kB; ++r) load_node(K[r], r);
@@ -461,7 +495,10 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
 #else
             const double tot = tbfly3(s0, s1, s2, ln);
 #endif
-            if (ln < 3) red[(nr * 3 + tbfly3_index(ln)) * LW + wv_s] = tot;
+            if (ln < 3) {
+              double& r = red[(nr * 3 + tbfly3_index(ln)) * LW + wv_s];
+              r = (GX && p > 0) ? r + tot : tot;   // passes add in pass order
+            }
           }
         }
       }
@@ -554,7 +591,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     // the last allowed iteration stores every entry of the unrelaxed iterate (uniform)
     const bool last_it = __builtin_amdgcn_readfirstlane(it + 1 == nloop ? 1 : 0) != 0;
 #pragma unroll 1
-    for (int j = 0; j < NB; ++j) {
+    for (int j = 0; j < NBT; ++j) {
       // per-bin scalars picked without dynamic register indexing (the loop is not unrolled,
       // so only one bin's LU is ever live)
       const int bj = tid + LT * j;
@@ -684,7 +721,13 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
         const cd x = F[c];
-        const cd xlast = xl[c * NWP + b];
+        cd xlast;
+        if constexpr (GX) {
+          const cd v = ld(XL + c * nw + (okj ? b : nw - 1));
+          xlast = okj ? v : mk(0.0, 0.0);
+        } else {
+          xlast = xl[c * NWP + b];
+        }
         my_nan |= okj && ((x.r != x.r) || (x.i != x.i));
         // tolCheck = |Xi - XiLast| / (|Xi| + tol) < tol  (raft/raft_model.py:961-962)
         // (magnitudes as sqrt(re^2 + im^2): within an ulp of np.abs's hypot, far cheaper)
@@ -700,7 +743,12 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
         }
         if (okj && XP) st(XP + c * nw + b, xlast);
         // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged (pads: 0)
-        xl[c * NWP + b] = add(scl(xlast, 0.2), scl(x, 0.8));
+        const cd xr = add(scl(xlast, 0.2), scl(x, 0.8));
+        if constexpr (GX) {
+          if (okj) st(XL + c * nw + b, xr);
+        } else {
+          xl[c * NWP + b] = xr;
+        }
       }
 #ifdef RH_PROF
       tc_sol += clock64() - tc1;
@@ -766,7 +814,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     // pass 1 stops here: park the relaxed iterate (the next iteration's XiLast) and the margin
     // so far; pass 2 continues the case from iteration itend with the same bits
 #pragma unroll 1
-    for (int j = 0; j < NB; ++j) {
+    for (int j = 0; j < NB && !GX; ++j) {   // (GX: XiLast is already in Xi_last)
       const int b = tid + LT * j;
       if (b >= nw) continue;
 #pragma unroll 1
@@ -797,7 +845,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     for (int e = tid; e < nn * 9; e += LT) a.o.Bmat[(size_t)ic * nn * 9 + e] = bm[e];
   if (a.o.Z) {   // final impedance fowt.Z (raft/raft_model.py:1013) from the last B_drag, streamed
 #pragma unroll 1
-    for (int j = 0; j < NB; ++j) {
+    for (int j = 0; j < NBT; ++j) {
       const int b = tid + LT * j;
       if (b >= nw) continue;
       const double w = lw[b], w2 = -(w * w);
@@ -812,7 +860,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   }
   double ss[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
+  for (int j = 0; j < NBT; ++j) {
     const int b = tid + LT * j;
     if (b >= nw) continue;
     const double z = lz[b];

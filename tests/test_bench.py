@@ -54,7 +54,7 @@ def test_pmc_lookup_sections_and_exact_names(tmp_path, monkeypatch):
     import bench
     rec = lambda r, w: {"hbm_read_bytes_corrected": r, "hbm_write_bytes": w}   # noqa: E731
     sec = {"solve": {"rh::k_a0_sums(rh::CaseArgs)": rec(1.0, 2.0),
-                     "void rh::k_solve_lds<2, 512, false>(rh::CaseArgs)": rec(10.0, 20.0)},
+                     "void rh::k_solve_lds<2, 512, false, 1>(rh::CaseArgs)": rec(10.0, 20.0)},
            "c4": {"rh::k_a0_sums(rh::CaseArgs)": rec(100.0, 0.0)},
            "qtf": {"rh::k_qtf_kay(rh_qtf_design, rh::QtfWork)": rec(5.0, 5.0),
                    "rh::k_qtf_kay_sum(rh_qtf_design, rh::QtfWork)": rec(7.0, 7.0)}}
@@ -67,4 +67,4 @@ def test_pmc_lookup_sections_and_exact_names(tmp_path, monkeypatch):
     assert bench.pmc_traffic("c4", *bench.solve_kernels(240)) is None
     p.write_text(json.dumps(sec["solve"]))
     assert bench.pmc_traffic("qtf", "rh::k_a0_sums") == 3.0
-    assert bench.solve_kernels(2000) == ("rh::k_solve_cases<8>",)
+    assert bench.solve_kernels(2000) == ("rh::k_a0_sums", "rh::k_solve_lds<2, 512, false, 2>")

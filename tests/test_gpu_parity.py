@@ -405,11 +405,12 @@ def test_margin_output_and_knobs():
     np.testing.assert_allclose(a["margin"], b["margin"], rtol=1e-9, atol=1e-15)
 
 
-@pytest.mark.parametrize("nw", [77, 255, 256, 333, 513, 1000])
+@pytest.mark.parametrize("nw", [77, 255, 256, 333, 513, 1000, 1025, 1500, 2048])
 def test_odd_grids(nw):
     """Grids that leave pad lanes: nw not a multiple of 64 (every block size), odd nw, nw just
-    past a block size (whole pad waves).  The default kernel (k_solve_lds, including its
-    128-thread form) against the general kernel k_solve_cases on the same batch: identical
+    past a block size (whole pad waves), and grids beyond 1024 bins (k_solve_lds in two passes
+    with XiLast in the Xi_last block).  The default kernel (k_solve_lds, including its 128-thread
+    and two-pass forms) against the general kernel k_solve_cases on the same batch: identical
     iteration counts and statuses, Xi within 1e-12."""
     from raft import _native as N
     T = load_golden("c2_nw200")

@@ -22,7 +22,8 @@ def test_isa_gate():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_check.py")], capture_output=True, text=True,
                        timeout=600)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
-    assert "k_solve_lds<2, 512, false>" in p.stdout and "k_solve_lds<2, 128, true>" in p.stdout and "FAIL" not in p.stdout
+    assert all(f"k_solve_lds<{k}>" in p.stdout for k in ("2, 512, false, 1", "2, 128, true, 1", "2, 512, false, 2"))
+    assert "FAIL" not in p.stdout
     assert "k_qtf_lcoef" in p.stdout and "k_array_resp<2>" in p.stdout
     ratchets = [ln for ln in p.stdout.splitlines() if "ratchet" in ln]
     assert ratchets and all("k_solve_cases<" in ln for ln in ratchets), ratchets

@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out; mkdir -p $OUT; cd $R
 timeout -k 10 420 python -u -m pytest tests/test_gpu_parity.py -x -v -m gpu --timeout 200 --timeout-method thread > $OUT/r04_parity.log 2>&1
 rc=$?; echo "parity rc=$rc"; tail -3 $OUT/r04_parity.log; if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 300 python tools/ubench/time_grid.py 1000 1000:noa0 1000 1000:noa0 200 200:noa0 2000 > $OUT/time_grid.log 2>&1 || exit $?
+timeout -k 10 300 python tools/ubench/time_grid.py 1000 1000:noa0 1000 1000:noa0 200 200:noa0 2000 2000:noa0 2000:gen 1500 > $OUT/time_grid.log 2>&1 || exit $?
 cat $OUT/time_grid.log
 timeout -k 10 600 python -u -m pytest tests/test_gpu_qtf.py tests/test_gpu_qtf12d.py tests/test_gpu_sweep.py tests/test_gpu_rccl.py -x -v -m gpu --timeout 200 --timeout-method thread > $OUT/r04_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/r04_tests.log; if [ $rc -ne 0 ]; then exit $rc; fi

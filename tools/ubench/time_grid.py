@@ -1,9 +1,10 @@
 """C2-shaped batches on other frequency grids: VolturnUS-S_example with min_freq = 0.2 / nw
-(max 0.2 Hz), 512 seeded JONSWAP cases, the default dispatch (k_solve_lds for nw <= 1024, the
-general kernel k_solve_cases beyond).  Prints the kernel that ran, ms per launch (HIP events
+(max 0.2 Hz), 512 seeded JONSWAP cases, the default dispatch (k_solve_lds: one pass for
+nw <= 1024, two passes with XiLast in the Xi_last block up to 2048).  Prints the kernel that ran, ms per launch (HIP events
 over 10 launches), mean iterations and the SURVEY.md §8(d) roofline fraction.
-usage: python tools/ubench/time_grid.py NW[:noa0] [...]   (":noa0": rh_set_a0(ctx, 0) for that run,
-every case forming its iteration-0 phase-A sums in its own workgroup)"""
+usage: python tools/ubench/time_grid.py NW[:noa0|:gen] [...]   (":noa0": rh_set_a0(ctx, 0) for that run,
+every case forming its iteration-0 phase-A sums in its own workgroup; ":gen": the general kernel
+k_solve_cases, rh_set_solver(ctx, 1))"""
 import os
 import sys
 
@@ -14,7 +15,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "raft-teststuff_amd"))
 
 
-def run(nw, a0=True):
+def run(nw, a0=True, gen=False):
     import json
     import torch
     import bench
@@ -36,6 +37,7 @@ def run(nw, a0=True):
     prep = prepare_batch([dd], cs)
     from raft import _native as N
     N.check(N.lib().rh_set_a0(N.context(0), int(a0)), "rh_set_a0")
+    N.check(N.lib().rh_set_solver(N.context(0), int(gen)), "rh_set_solver")
     want = ("psd", "std", "zeta", "rao")
     for _ in range(3):
         res = solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=want, prepared=prep)
@@ -53,10 +55,12 @@ def run(nw, a0=True):
     flops = float(sum(bench.flops_per_case(int(n), dd.nw, nc, nr, dd.nn) for n in iters))
     frac = flops / (ms * 1e-3) / bench.PEAK_FP64
     N.check(N.lib().rh_set_a0(N.context(0), 1), "rh_set_a0")
-    print(f"nw={dd.nw:5d} a0={int(a0)} {bench.solve_kernel_name(dd.nw):36s} {ms:8.3f} ms/launch  iters {iters.mean():.2f}  "
+    N.check(N.lib().rh_set_solver(N.context(0), 0), "rh_set_solver")
+    kname = "rh::k_solve_cases (general)" if gen else bench.solve_kernel_name(dd.nw)
+    print(f"nw={dd.nw:5d} a0={int(a0)} {kname:36s} {ms:8.3f} ms/launch  iters {iters.mean():.2f}  "
           f"{512 / (ms * 1e-3):.3e} cases/s  frac {frac:.3f}", flush=True)
 
 
 if __name__ == "__main__":
     for a in sys.argv[1:]:
-        run(int(a.split(":")[0]), not a.endswith(":noa0"))
+        run(int(a.split(":")[0]), not a.endswith(":noa0"), a.endswith(":gen"))
