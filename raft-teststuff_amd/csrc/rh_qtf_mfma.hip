@@ -798,28 +798,36 @@ __device__ __forceinline__ void lcoef_block(const rh_qtf_design& q, const QtfWor
 // P1 = Ar Br, P2 = Ai Bi, P3 = (Ar + Ai)(Br + Bi); Re = P1 - P2, Im = P3 - P1 - P2.  nsteps is a
 // multiple of 4: the loads of the next four steps are in flight while the MFMAs of the current
 // four run.
+#ifndef RH_QTF_PF
+#define RH_QTF_PF 4   // k-steps per operand batch (tools/ubench variant: 8)
+#endif
 __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const rh_c128* __restrict__ B, size_t step,
                                             int nsteps, d4& p1, d4& p2, d4& p3) {
+  constexpr int PF = RH_QTF_PF;
   d4 q1 = {0, 0, 0, 0}, q2 = q1, q3 = q1;
-  cd a[4], b[4];
+  cd a[PF], b[PF];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    a[j] = ld(A + j * step);
-    b[j] = ld(B + j * step);
+  for (int j = 0; j < PF; ++j) {
+    const int sj = (PF > 4 && j >= nsteps) ? nsteps - 1 : j;
+    a[j] = ld(A + sj * step);
+    b[j] = ld(B + sj * step);
   }
 #pragma unroll 1
-  for (int s = 0; s < nsteps; s += 4) {
-    cd an[4], bn[4];
-    const bool more = s + 4 < nsteps;
+  for (int s = 0; s < nsteps; s += PF) {
+    cd an[PF], bn[PF];
+    const bool more = s + PF < nsteps;
     if (more) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        an[j] = ld(A + (s + 4 + j) * step);
-        bn[j] = ld(B + (s + 4 + j) * step);
+      for (int j = 0; j < PF; ++j) {
+        // nsteps is a multiple of 4: a deeper batch (variant) stops at the last step
+        const int sj = (PF > 4 && s + PF + j >= nsteps) ? nsteps - 1 : s + PF + j;
+        an[j] = ld(A + sj * step);
+        bn[j] = ld(B + sj * step);
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; j += 2) {   // two accumulator sets: six independent MFMA chains
+    for (int j = 0; j < PF; j += 2) {   // two accumulator sets: six independent MFMA chains
+      if (PF > 4 && s + j >= nsteps) break;   // uniform (variant only)
       p1 = mfma64(a[j].r, b[j].r, p1);
       p2 = mfma64(a[j].i, b[j].i, p2);
       p3 = mfma64(a[j].r + a[j].i, b[j].r + b[j].i, p3);
@@ -829,7 +837,7 @@ __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const
     }
     if (more) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < PF; ++j) {
         a[j] = an[j];
         b[j] = bn[j];
       }

@@ -12,6 +12,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_qtf.py tests/test_gpu_qtf12
 rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/r04_tests.log; if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 120 python tools/ubench/qtf_time.py default --save $OUT/qtf_ref.npy > $OUT/qtf_time.log 2>&1 || exit $?
 RAFTHIP_LIB=$R/raft-teststuff_amd/variants/lib_kay1.so timeout -k 10 120 python tools/ubench/qtf_time.py kay_wpe1 --check $OUT/qtf_ref.npy >> $OUT/qtf_time.log 2>&1 || exit $?
+RAFTHIP_LIB=$R/raft-teststuff_amd/variants/lib_qpf8.so timeout -k 10 120 python tools/ubench/qtf_time.py gemm_pf8 --check $OUT/qtf_ref.npy >> $OUT/qtf_time.log 2>&1 || exit $?
 timeout -k 10 120 python tools/ubench/qtf_time.py default2 >> $OUT/qtf_time.log 2>&1 || exit $?
 cat $OUT/qtf_time.log
 cd /tmp && export TMPDIR=/tmp
