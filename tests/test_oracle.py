@@ -166,3 +166,38 @@ def test_kat_jonswap_auto_gamma_branches():
         S = O.jonswap(w, hs, tp, 0)
         m0 = np.trapezoid(S, w) if hasattr(np, "trapezoid") else np.trapz(S, w)
         assert 0.5 < 4 * np.sqrt(m0) / hs < 1.1
+
+
+@pytest.mark.parametrize("tag", ["c2_nw1000", "c2_nw200", "c1_OC3spar"])
+def test_iteration0_sums_separable_form(tag):
+    """The algebra of k_solve_lds's iteration-0 shortcut (csrc/rh_a0.hip), on the reference's
+    own node tables and sea states: with XiLast = XiStart in every DOF and bin, the node's
+    motion displacement dr is real and bin-independent, so per projection e (q, p1, p2)
+        sum_b |e.(u_b - i w_b dr)|^2 = sum z^2 |e.u^|^2 - 2 (e.dr) sum z w Im(e.u^) + (e.dr)^2 sum w^2
+    (u = z u^, u^ the unit-amplitude kinematics that kproj tabulates).  The direct and the
+    separable sums agree to rounding on every node and projection: the expansion cancels
+    nothing that matters at the RTOL of the parity tests."""
+    T = load_golden(tag)
+    nodes = O.Nodes(T)
+    w = T["w"]
+    xs = float(T["XiStart"]) or 0.1
+    cases = list(golden_cases(T))[:2] + [dict(wave_heading=h, wave_period=p, wave_height=hh, wave_spectrum="JONSWAP")
+                                        for h, p, hh in [(0, 6.0, 1.0), (60, 17.5, 9.5)]]
+    worst = 0.0
+    for case in cases:
+        beta, S, zeta = O.sea_state(case, w, float(T["dw"]))
+        u, _, _, _ = O.hydro_excitation(T, nodes, beta[:1], zeta[:1])
+        z = zeta[0].real
+        Xi = np.full([6, len(w)], xs, dtype=complex)
+        for j in range(nodes.n):
+            dr, _, _ = O.kinematics(nodes.r_rel[j], Xi, w)
+            vrel = u[0, j] - 1j * w * dr
+            uhat = np.divide(u[0, j], z, out=np.zeros_like(u[0, j]), where=z > 0)
+            for e in (nodes.q[j], nodes.p1[j], nodes.p2[j]):
+                direct = np.sum(np.abs(e @ vrel) ** 2)
+                K = e @ uhat
+                b = float(np.real(e @ dr[:, 0]))
+                sep = np.sum(z * z * np.abs(K) ** 2) - 2 * b * np.sum(z * w * K.imag) + b * b * np.sum(w * w)
+                worst = max(worst, abs(sep - direct) / direct)
+    print(f"{tag}: worst relative difference {worst:.2e}")
+    assert worst < 1e-12, worst
