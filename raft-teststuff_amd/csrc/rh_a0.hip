@@ -18,7 +18,7 @@
 // and z^2 |K|^2 rows with beta = 0 are sums of squares).
 //
 // Launch: grid (ceil(ncase / 16) case tiles of the launch order, ceil(nw / 128) bin chunks),
-// 256 threads.  A tile's cases are handled one (design, heading) key at a time (a sorted launch
+// 512 threads.  A tile's cases are handled one (design, heading) key at a time (a sorted launch
 // order gives one or two keys per tile); each wave takes 16-row blocks of the key's 3 nn rows.
 // Per (case, chunk) the row sums go to the case's Xi_last scratch, which the fast path does not
 // otherwise use: [chunk][3 nn] doubles at the start of the case's [6][nw] complex block.
@@ -28,8 +28,9 @@ namespace rh {
 
 constexpr int kA0Cases = 16;       // cases per tile (MFMA rows)
 constexpr int kA0Bins = 128;       // bins per chunk (32 MFMA steps of 4 bins)
-constexpr int kA0Threads = 256;
+constexpr int kA0Threads = 512;    // 8 waves: one 16-row block of the node projections each
 constexpr int kA0Pad = kA0Bins + 2;
+constexpr int kA0MaxRows = 3 * 1024;   // 3 nn, nn <= kMaxNodes (rh_abi.hip check_design)
 
 __host__ __device__ inline int a0_chunks(int nw) { return (nw + kA0Bins - 1) / kA0Bins; }
 // the A(0) sums of a case fit in its Xi_last block ([6][nw] complex = 12 nw doubles)
@@ -40,9 +41,35 @@ __device__ __forceinline__ double* a0_block(const CaseArgs& a, int ic, int nw) {
 
 typedef double a0d4 __attribute__((ext_vector_type(4)));
 
+// beta_j / XiStart of table row j = 3 n + p (node n, projection p): the member factors of the
+// node's member summed over the six DOFs (XiLast = XiStart (1, ..., 1)), plus t times the
+// rotation part for the two transverse projections (header comment).
+__device__ __forceinline__ double a0_beta_unit(const rh_design& d, int j) {
+  const int nn = d.nn, nm = d.nm;
+  const int n = j / 3, p = j - 3 * n;
+  int m = 0;
+  while (m + 1 < nm && d.mstart[m + 1] <= n) ++m;
+  const double t = d.node[RH_NF_T * nn + n];
+  double sq = 0, s1 = 0, s2 = 0, d1 = 0, d2 = 0;
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    const double cq = d.memb[(RH_MF_CQ0 + c) * nm + m], c1 = d.memb[(RH_MF_C10 + c) * nm + m],
+                 c2 = d.memb[(RH_MF_C20 + c) * nm + m];
+    sq += cq;
+    s1 += c1;
+    s2 += c2;
+    if (c < 3) {
+      d1 += c2;
+      d2 += c1;
+    }
+  }
+  return p == 0 ? sq : p == 1 ? s1 + t * d1 : s2 - t * d2;
+}
+
 __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
   __shared__ double su[kA0Cases][kA0Pad];   // z^2 of (case, bin of the chunk)
   __shared__ double sv[kA0Cases][kA0Pad];   // z w
+  __shared__ double sbeta[kA0MaxRows];      // beta_j of the current key's design
   __shared__ int kic[kA0Cases], kd[kA0Cases], kh[kA0Cases];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -71,7 +98,6 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
     su[c][bl] = zz * zz;
     sv[c][bl] = zz * w;
   }
-  __syncthreads();
   const int mr = lane & 15, kr = lane >> 4;
   const double xs = a.c.XiStart;
   unsigned done = 0;
@@ -89,8 +115,11 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
       if (kic[c] >= 0 && kd[c] == kdes && kh[c] == khead) match |= 1u << c;
     done |= match;
     const rh_design& d = a.designs[kdes].d;
-    const int nn = d.nn, nm = d.nm, nrow = 3 * nn, nrb = (nrow + 15) / 16;
+    const int nn = d.nn, nrow = 3 * nn, nrb = (nrow + 15) / 16;
     if (nn == 0) continue;
+    __syncthreads();   // the previous key's rows have read sbeta (and, first time, su / sv are written)
+    for (int j = tid; j < nrow; j += kA0Threads) sbeta[j] = xs * a0_beta_unit(d, j);
+    __syncthreads();
     const unsigned nw16 = (unsigned)nw * 16u;
     const Buf bK = mkbuf(d.kproj + (size_t)khead * nrow * nw, (unsigned)nrow * nw16);
     const bool mine = ((match >> mr) & 1u) != 0;   // A row mr belongs to this key
@@ -105,40 +134,21 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
     for (int rb = wv; rb < nrb; rb += kA0Threads / 64) {
       const int j = rb * 16 + mr;                    // this lane's row (B column mr)
       const int jc = j < nrow ? j : nrow - 1;
-      const int n = jc / 3, p = jc - 3 * n;
-      int m = 0;
-      while (m + 1 < nm && d.mstart[m + 1] <= n) ++m;
-      const double t = d.node[RH_NF_T * nn + n];
-      double sq = 0, s1 = 0, s2 = 0, d1 = 0, d2 = 0;
-#pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        const double cq = d.memb[(RH_MF_CQ0 + c) * nm + m], c1 = d.memb[(RH_MF_C10 + c) * nm + m],
-                     c2 = d.memb[(RH_MF_C20 + c) * nm + m];
-        sq += cq;
-        s1 += c1;
-        s2 += c2;
-        if (c < 3) {
-          d1 += c2;
-          d2 += c1;
-        }
-      }
-      const double beta = xs * (p == 0 ? sq : p == 1 ? s1 + t * d1 : s2 - t * d2);
+      const double beta = sbeta[jc];
       const double m2b = -2.0 * beta;
-      a0d4 acc = {0.0, 0.0, 0.0, 0.0};
+      // every wave-table operand of the row block in flight at once (32 complex per lane)
+      constexpr int kS = kA0Bins / 4;
       const unsigned so = (unsigned)jc * nw16;
-      constexpr int kU = 8;   // MFMA steps per batch of loads
-#pragma unroll 1
-      for (int ks0 = 0; ks0 < kA0Bins / 4; ks0 += kU) {
-        cd K[kU];
+      cd K[kS];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) K[u] = bld(bK, (unsigned)(b0 + 4 * (ks0 + u) + kr) * 16u, so);
+      for (int u = 0; u < kS; ++u) K[u] = bld(bK, (unsigned)(b0 + 4 * u + kr) * 16u, so);
+      a0d4 accu = {0.0, 0.0, 0.0, 0.0}, accv = accu;   // two independent MFMA chains
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-          const int bl = 4 * (ks0 + u) + kr;
-          const double ua = mine ? su[mr][bl] : 0.0, va = mine ? sv[mr][bl] : 0.0;
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, K[u].r * K[u].r + K[u].i * K[u].i, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va, m2b * K[u].i, acc, 0, 0, 0);
-        }
+      for (int u = 0; u < kS; ++u) {
+        const int bl = 4 * u + kr;
+        const double ua = mine ? su[mr][bl] : 0.0, va = mine ? sv[mr][bl] : 0.0;
+        accu = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, K[u].r * K[u].r + K[u].i * K[u].i, accu, 0, 0, 0);
+        accv = __builtin_amdgcn_mfma_f64_16x16x4f64(va, m2b * K[u].i, accv, 0, 0, 0);
       }
       // C[i][j]: lane holds rows i = kr + 4 r (cases) of column j = mr (rows of the table)
       if (j < nrow) {
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = kr + 4 * r;
-          if ((match >> i) & 1u) a0_block(a, kic[i], nw)[(size_t)chunk * nrow + j] = acc[r] + cst;
+          if ((match >> i) & 1u) a0_block(a, kic[i], nw)[(size_t)chunk * nrow + j] = (accu[r] + accv[r]) + cst;
         }
       }
     }

@@ -1196,7 +1196,11 @@ __global__ __launch_bounds__(64) void k_system_solve_reg(int nw, const rh_c128* 
 // Xi = Z_sys^-1 F solved by the 6x6 blocks as in k_system_solve_reg.  Nothing per (case,
 // bin) goes through HBM but Xi: no Z and no F array.  For two FOWTs the excitation of the
 // second is formed after the first block is factored (A is then dead), so F2 never lives
-// beside A's factors.
+// beside A's factors.  The drag excitation is member-factored over the projected table kproj
+// (drag_exc_members' arithmetic; the node coefficients {qT Bmat q, p1T Bmat p1, p2T Bmat p2}
+// recovered from the case's Bmat in LDS, since Bmat = a_q qqT + a_1 p1p1T + a_2 p2p2T), with
+// a 4-node prefetch ring: the LU's register peak holds the kernel at one wave per SIMD, so the
+// node loop must hide its own load latency.
 // ----------------------------------------------------------------------------------------
 struct ArrayArgs {
   const DevDesign* designs;
@@ -1208,13 +1212,22 @@ struct ArrayArgs {
   const double* Bmat;          // [ncase * NF][nn][9] (equal nn over the FOWTs)
   const double* K;             // [6 NF][6 NF] array stiffness, or NULL
   rh_c128* Xi;                 // [ncase][6 NF][nw]
+  int nn_max, nm_max;          // largest node / member counts of the designs (dynamic LDS layout)
 };
+__host__ __device__ inline size_t array_resp_smem(int NF, int nn_max, int nm_max) {
+  return sizeof(double) * (size_t)NF * (5 * nn_max + 18 * nm_max) + sizeof(int) * (size_t)NF * (nm_max + 1);
+}
 
 template <int NF>
 __global__ __launch_bounds__(64) void k_array_resp(ArrayArgs a) {
   constexpr int N = 6 * NF;
   __shared__ double ks[N * N];        // K_array (uniform reads)
   __shared__ double mz[NF][4][36];    // per FOWT: M, B_lin (frequency-independent designs), C, B_drag
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  const int nnA = a.nn_max, nmA = a.nm_max;
+  double* alf = dyn;                                          // [NF][nnA][5] node drag coefficients
+  double* mbf = alf + (size_t)NF * nnA * 5;                   // [NF][18][nmA] member factors cq, c1, c2
+  int* mst = reinterpret_cast<int*>(mbf + (size_t)NF * 18 * nmA);   // [NF][nmA + 1] member node ranges
   const int tid = (int)threadIdx.x;
   const int ic = blockIdx.y;
   for (int e = tid; e < N * N; e += 64) ks[e] = a.K ? a.K[e] : 0.0;
@@ -1227,6 +1240,28 @@ __global__ __launch_bounds__(64) void k_array_resp(ArrayArgs a) {
       mz[f][2][tid] = d.C[tid];
       mz[f][3][tid] = a.B_drag[((size_t)ic * NF + f) * 36 + tid];
     }
+    const int nn = d.nn, nm = d.nm;
+    const double* Bm = a.Bmat + ((size_t)ic * NF + f) * nn * 9;
+    for (int n = tid; n < nn; n += 64) {
+      double c[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {   // e^T Bmat e for e = q, p1, p2
+        const int fx = k == 0 ? RH_NF_QX : k == 1 ? RH_NF_P1X : RH_NF_P2X;
+        const double ex = nf(d.node, nn, fx, n), ey = nf(d.node, nn, fx + 1, n), ez = nf(d.node, nn, fx + 2, n);
+        const double* B = Bm + 9 * n;
+        c[k] = ex * (B[0] * ex + B[1] * ey + B[2] * ez) + ey * (B[3] * ex + B[4] * ey + B[5] * ez) +
+               ez * (B[6] * ex + B[7] * ey + B[8] * ez);
+      }
+      const double t = nf(d.node, nn, RH_NF_T, n);
+      double* A = alf + ((size_t)f * nnA + n) * 5;
+      A[0] = c[0];
+      A[1] = c[1];
+      A[2] = c[2];
+      A[3] = t * c[1];
+      A[4] = t * c[2];
+    }
+    for (int e = tid; e < 18 * nm; e += 64) mbf[((size_t)f * 18 + e / nm) * nmA + e % nm] = d.memb[e];
+    for (int e = tid; e <= nm; e += 64) mst[f * (nmA + 1) + e] = d.mstart[e];
   }
   __syncthreads();
   const rh_design& d0 = a.designs[a.design_idx[ic * NF]].d;
@@ -1264,17 +1299,72 @@ __global__ __launch_bounds__(64) void k_array_resp(ArrayArgs a) {
         }
     }
   };
-  // F_wave of FOWT f (raft/raft_model.py:1049-1061; k_heading_resp with a.F)
+  // F_wave of FOWT f (raft/raft_model.py:1049-1061): zeta (F_iner + F_drag), the drag part
+  // member-factored (drag_exc_members) with the node loads 4 nodes ahead
   auto excite = [&](int f, cd (&F)[6]) {
     const size_t e = (size_t)ic * NF + f;
     const rh_design& d = a.designs[a.design_idx[e]].d;
     const int nn = d.nn, head = a.head[e];
-    const rh_c128* Uh = d.uhat + (size_t)head * nn * 3 * nw;
-    const rh_c128* Fe = d.finer + (size_t)head * 6 * nw;
-    const double z = a.zeta[e * nw + b];
-    drag_exc_bin(d.node, nn, a.Bmat + e * nn * 9, Uh, nw, b, F);
+    const unsigned nw16 = (unsigned)nw * 16u, vb = (unsigned)b * 16u;
+    const Buf bK = mkbuf(d.kproj + (size_t)head * nn * 3 * nw, (unsigned)nn * 3u * nw16);
+    const Buf bFe = mkbuf(d.finer + (size_t)head * 6 * nw, 6u * nw16);
+    cd fe[6];
 #pragma unroll
-    for (int c = 0; c < 6; ++c) F[c] = add(scl(ld(Fe + c * nw + b), z), scl(F[c], z));
+    for (int c = 0; c < 6; ++c) fe[c] = bld(bFe, vb, c * nw16);
+    const double z = a.zeta[e * nw + b];
+    const double* A = alf + (size_t)f * nnA * 5;
+    const double* MB = mbf + (size_t)f * 18 * nmA;
+    const int* ms = mst + f * (nmA + 1);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
+    cd SQ = mk(0, 0), S1 = mk(0, 0), S2 = mk(0, 0), T1 = mk(0, 0), T2 = mk(0, 0);
+    int m = 0, mnext = nn > 0 ? ms[1] : 0;
+    auto fold = [&]() {   // close member m: F += its node sums (drag_exc_members)
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const double cq = MB[(RH_MF_CQ0 + i) * nmA + m], c1 = MB[(RH_MF_C10 + i) * nmA + m],
+                     c2 = MB[(RH_MF_C20 + i) * nmA + m];
+        F[i] = add(F[i], add(add(scl(SQ, cq), scl(S1, c1)), scl(S2, c2)));
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const double p1 = MB[(RH_MF_C10 + i) * nmA + m], p2 = MB[(RH_MF_C20 + i) * nmA + m];
+        F[3 + i] = add(F[3 + i], sub(scl(T1, p2), scl(T2, p1)));
+      }
+      SQ = S1 = S2 = T1 = T2 = mk(0, 0);
+    };
+    constexpr int R = 4;
+    auto load = [&](cd (&K)[3], int n) {
+      const unsigned so = (unsigned)(n < nn ? n : nn - 1) * 3u * nw16;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) K[p] = bld(bK, vb, so + (unsigned)p * nw16);
+    };
+    cd K[R][3];
+#pragma unroll
+    for (int r = 0; r < R; ++r) load(K[r], r);
+    for (int n = 0; n < nn; n += R) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int nr = n + r;
+        if (nr < nn) {
+          while (nr == mnext) {   // uniform: member m ended before node nr
+            fold();
+            ++m;
+            mnext = ms[m + 1];
+          }
+          const double* An = A + 5 * nr;
+          SQ = add(SQ, scl(K[r][0], An[0]));
+          S1 = add(S1, scl(K[r][1], An[1]));
+          S2 = add(S2, scl(K[r][2], An[2]));
+          T1 = add(T1, scl(K[r][1], An[3]));
+          T2 = add(T2, scl(K[r][2], An[4]));
+          load(K[r], nr + R);
+        }
+      }
+    }
+    if (nn > 0) fold();
+#pragma unroll
+    for (int c = 0; c < 6; ++c) F[c] = add(scl(fe[c], z), scl(F[c], z));
   };
   if constexpr (NF == 1) {
     cd A[6][6], x[6];
