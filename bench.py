@@ -380,12 +380,12 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
            "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                         "frac": achieved / PEAK_FP64,
                         "traffic": pmc_traffic("qtf", "k_qtf_tables", "k_qtf_lcoef", "k_qtf_kay", "k_qtf_gemm"),
-                        "kernel": "rh_qtf_slender%s: k_qtf_freq, k_qtf_tables, k_qtf_lcoef, k_qtf_gemm, k_qtf_kay (second "
-                                  "stream), k_qtf_kay_sum (every launch of a QTF on this rank)" % ("_rows" if world > 1 else ""),
+                        "kernel": "rh_qtf_slender%s: k_qtf_tables, k_qtf_lcoef, k_qtf_kay, k_qtf_gemm (every launch of a "
+                                  "QTF on this rank)" % ("_rows" if world > 1 else ""),
                         "kernel_ms": ms, "flops_per_pair": fpp, "pairs_this_rank": mine,
                         "note": "FP64: the pair sum as MFMA GEMMs (k_qtf_gemm) + VALU Kim & Yue epilogue (DESIGN.md "
                                 "§4); peak = MI355X FP64 dense (matrix = vector rate); algorithmic FLOPs from SURVEY.md "
-                                "§8(d) over this rank's pairs; traffic = HBM bytes of all six launches of a QTF (PMC)"}}
+                                "§8(d) over this rank's pairs; traffic = HBM bytes of all four launches of a QTF (PMC)"}}
     return out
 
 
@@ -799,7 +799,7 @@ def main():
                           "note": "per step: all_gather_into_tensor (RCCL) of every rank's std, PSD and iteration "
                                   "counts on a second stream, overlapping the next step's solve"}
     if not args.no_qtf:
-        line["qtf"] = bench_qtf(device, max(3, args.steps // 4), 1, world, rank, dist)
+        line["qtf"] = bench_qtf(device, max(20, args.steps // 4), 10, world, rank, dist)
     if not args.no_c4:
         line["c4"] = bench_c4(device, max(3, args.steps // 4), world, rank, dist)
     if not args.no_c5:

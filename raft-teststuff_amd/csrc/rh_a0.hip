@@ -26,11 +26,17 @@
 
 namespace rh {
 
+#ifndef RH_A0_ABL
+#define RH_A0_ABL 0   // timing ablations (tools/ubench variants): 1 no spectrum, 2 no member lookup, 4 no MFMA
+#endif
 constexpr int kA0Cases = 16;       // cases per tile (MFMA rows)
 constexpr int kA0Bins = 128;       // bins per chunk (32 MFMA steps of 4 bins)
 constexpr int kA0Threads = 512;    // 8 waves: one 16-row block of the node projections each
 constexpr int kA0Pad = kA0Bins + 2;
 constexpr int kA0MaxRows = 3 * 1024;   // 3 nn, nn <= kMaxNodes (rh_abi.hip check_design)
+constexpr int kSub = 32;                // bins per LDS-staged sub-chunk of a row block
+constexpr int kSubP = kSub + 1;         // its padded row length (complex)
+constexpr int kStageLd = 16 * kSub / 64;   // loads per lane per sub-chunk (two rows x 32 bins each)
 
 __host__ __device__ inline int a0_chunks(int nw) { return (nw + kA0Bins - 1) / kA0Bins; }
 // the A(0) sums of a case fit in its Xi_last block ([6][nw] complex = 12 nw doubles)
@@ -70,6 +76,7 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
   __shared__ double su[kA0Cases][kA0Pad];   // z^2 of (case, bin of the chunk)
   __shared__ double sv[kA0Cases][kA0Pad];   // z w
   __shared__ double sbeta[kA0MaxRows];      // beta_j of the current key's design
+  __shared__ double2 stage[kA0Threads / 64][16 * kSubP];   // per wave: 16 rows x 32 bins of kproj
   __shared__ int kic[kA0Cases], kd[kA0Cases], kh[kA0Cases];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -93,7 +100,11 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
     if (ic >= 0 && b < nw) {
       const rh_design& d = a.designs[kd[c]].d;
       w = d.w[b];
+#if RH_A0_ABL & 1   // timing ablation: no spectrum (wrong results)
+      zz = a.c.Hs[ic];
+#else
       zz = sea_amplitude(a.c.spectrum[ic], a.c.Hs[ic], a.c.Tp[ic], a.c.gamma[ic], w, d.dw);
+#endif
     }
     su[c][bl] = zz * zz;
     sv[c][bl] = zz * w;
@@ -118,7 +129,11 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
     const int nn = d.nn, nrow = 3 * nn, nrb = (nrow + 15) / 16;
     if (nn == 0) continue;
     __syncthreads();   // the previous key's rows have read sbeta (and, first time, su / sv are written)
+#if RH_A0_ABL & 2   // timing ablation: no member lookup (wrong results)
+    for (int j = tid; j < nrow; j += kA0Threads) sbeta[j] = xs;
+#else
     for (int j = tid; j < nrow; j += kA0Threads) sbeta[j] = xs * a0_beta_unit(d, j);
+#endif
     __syncthreads();
     const unsigned nw16 = (unsigned)nw * 16u;
     const Buf bK = mkbuf(d.kproj + (size_t)khead * nrow * nw, (unsigned)nrow * nw16);
@@ -136,19 +151,42 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
       const int jc = j < nrow ? j : nrow - 1;
       const double beta = sbeta[jc];
       const double m2b = -2.0 * beta;
-      // every wave-table operand of the row block in flight at once (32 complex per lane)
-      constexpr int kS = kA0Bins / 4;
-      const unsigned so = (unsigned)jc * nw16;
-      cd K[kS];
+      // The MFMA B fragment is 16 rows x 4 bins; read straight from the [row][bin] table it would
+      // touch 16 rows 16 KB apart per load (nw = 1000), all in one memory channel.  So each wave
+      // stages its row block through LDS in sub-chunks of 32 bins: coalesced loads of two rows x
+      // 32 bins per instruction, the next sub-chunk in flight while the current one's MFMAs run.
+      double2* stg = stage[wv];
+      cd L[kStageLd];
+      auto load_sub = [&](int sc) {
 #pragma unroll
-      for (int u = 0; u < kS; ++u) K[u] = bld(bK, (unsigned)(b0 + 4 * u + kr) * 16u, so);
+        for (int i = 0; i < kStageLd; ++i) {
+          const int row = rb * 16 + 2 * i + (lane >> 5);
+          L[i] = bld(bK, (unsigned)(b0 + kSub * sc + (lane & 31)) * 16u, (unsigned)(row < nrow ? row : nrow - 1) * nw16);
+        }
+      };
+      load_sub(0);
       a0d4 accu = {0.0, 0.0, 0.0, 0.0}, accv = accu;   // two independent MFMA chains
+#pragma unroll 1
+      for (int sc = 0; sc < kA0Bins / kSub; ++sc) {
 #pragma unroll
-      for (int u = 0; u < kS; ++u) {
-        const int bl = 4 * u + kr;
-        const double ua = mine ? su[mr][bl] : 0.0, va = mine ? sv[mr][bl] : 0.0;
-        accu = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, K[u].r * K[u].r + K[u].i * K[u].i, accu, 0, 0, 0);
-        accv = __builtin_amdgcn_mfma_f64_16x16x4f64(va, m2b * K[u].i, accv, 0, 0, 0);
+        for (int i = 0; i < kStageLd; ++i) stg[(2 * i + (lane >> 5)) * kSubP + (lane & 31)] = make_double2(L[i].r, L[i].i);
+        if (sc + 1 < kA0Bins / kSub) load_sub(sc + 1);
+#if RH_A0_ABL & 4   // timing ablation: staged operands consumed by one add each, no MFMA (wrong results)
+#pragma unroll
+        for (int u = 0; u < kSub / 4; ++u) {
+          const double2 K = stg[mr * kSubP + 4 * u + kr];
+          accu[0] += K.x + K.y;
+        }
+#else
+#pragma unroll
+        for (int u = 0; u < kSub / 4; ++u) {
+          const double2 K = stg[mr * kSubP + 4 * u + kr];
+          const int bl = kSub * sc + 4 * u + kr;
+          const double ua = mine ? su[mr][bl] : 0.0, va = mine ? sv[mr][bl] : 0.0;
+          accu = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, K.x * K.x + K.y * K.y, accu, 0, 0, 0);
+          accv = __builtin_amdgcn_mfma_f64_16x16x4f64(va, m2b * K.y, accv, 0, 0, 0);
+        }
+#endif
       }
       // C[i][j]: lane holds rows i = kr + 4 r (cases) of column j = mr (rows of the table)
       if (j < nrow) {

@@ -705,16 +705,21 @@ int rh_array_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf
       return fail(RH_EINVAL, "rh_array_response: all designs must share nw and the submerged node count");
     nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
   }
-  const size_t lsm = rh::array_resp_smem(nf, nn, nmmax);
-  if (lsm + 48 * 1024 > kMaxLds)
+  const size_t lsm = rh::array_exc_smem(nn, nmmax);
+  if (lsm > kMaxLds)
     return fail(RH_EINVAL, "rh_array_response: %d nodes / %d members need %zu B of LDS", nn, nmmax, lsm);
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
   rh::ArrayArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, B_drag, Bmat, K, Xi, nn, nmmax};
-  const dim3 g((nw + 63) / 64, ncase);
-  if (nf == 1) hipLaunchKernelGGL(rh::k_array_resp<1>, g, dim3(64), lsm, s, a);
-  else hipLaunchKernelGGL(rh::k_array_resp<2>, g, dim3(64), lsm, s, a);
+  const dim3 ge(ncase * nf), g((nw + 63) / 64, ncase);   // excitation per (case, FOWT), then the solve
+  if (nf == 1) {
+    hipLaunchKernelGGL(rh::k_array_exc<1>, ge, dim3(rh::kArrExcThreads), lsm, s, a);
+    hipLaunchKernelGGL(rh::k_array_resp<1>, g, dim3(64), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(rh::k_array_exc<2>, ge, dim3(rh::kArrExcThreads), lsm, s, a);
+    hipLaunchKernelGGL(rh::k_array_resp<2>, g, dim3(64), 0, s, a);
+  }
   return designs_used(ctx, s);
 }
 

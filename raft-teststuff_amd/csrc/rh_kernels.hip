@@ -1187,20 +1187,23 @@ __global__ __launch_bounds__(64) void k_system_solve_reg(int nw, const rh_c128* 
 
 
 // ----------------------------------------------------------------------------------------
-// k_array_resp: the coupled-array response of every (case, bin), one lane per bin
-// (raft/raft_model.py:1021-1065 for a batch of single-sea-state cases): for each FOWT f of
-// the case, its wave excitation with the final drag linearisation (k_heading_resp's
-// arithmetic, raft/raft_model.py:1049-1061) and its impedance rebuilt from the design's
-// M / B_lin / C and the case's B_drag (the expression of fowt.Z, raft/raft_model.py:944,
-// 1013: the bits the fixed point's Z output had), then Z_sys = blockdiag(Z_f) + K_array and
-// Xi = Z_sys^-1 F solved by the 6x6 blocks as in k_system_solve_reg.  Nothing per (case,
-// bin) goes through HBM but Xi: no Z and no F array.  For two FOWTs the excitation of the
-// second is formed after the first block is factored (A is then dead), so F2 never lives
-// beside A's factors.  The drag excitation is member-factored over the projected table kproj
-// (drag_exc_members' arithmetic; the node coefficients {qT Bmat q, p1T Bmat p1, p2T Bmat p2}
-// recovered from the case's Bmat in LDS, since Bmat = a_q qqT + a_1 p1p1T + a_2 p2p2T), with
-// a 4-node prefetch ring: the LU's register peak holds the kernel at one wave per SIMD, so the
-// node loop must hide its own load latency.
+// The coupled-array response of every (case, bin) (raft/raft_model.py:1021-1065 for a batch of
+// single-sea-state cases), in two launches with nothing per (case, bin) in HBM but Xi:
+//   k_array_exc:  for each (case, FOWT) the wave excitation with the final drag linearisation,
+//                 F_f = zeta (F_iner + F_drag) (raft/raft_model.py:1049-1061), written into
+//                 the FOWT's rows of Xi;
+//   k_array_resp: per (case, bin) lane, each FOWT's impedance rebuilt from the design's
+//                 M / B_lin / C and the case's B_drag (the expression of fowt.Z,
+//                 raft/raft_model.py:944, 1013), Z_sys = blockdiag(Z_f) + K_array, and
+//                 Xi = Z_sys^-1 F solved by the 6x6 blocks as in k_system_solve_reg, reading
+//                 the lane's F from Xi and overwriting it with the solution.
+// The excitation is its own launch because the block solve's register peak and its LDS slab
+// hold k_array_resp at one wave per SIMD, where the node loop of the excitation could not hide
+// its wave-table loads (one fused kernel: 190 us per C4 step against 58 us for the excitation
+// alone and 78 us for the rest, profiles/r04_v2).  The drag part is member-factored over the
+// projected table kproj (drag_exc_members' arithmetic), the node coefficients
+// {qT Bmat q, p1T Bmat p1, p2T Bmat p2} recovered from the case's Bmat
+// (Bmat = a_q qqT + a_1 p1p1T + a_2 p2p2T), with the node loads 4 nodes ahead.
 // ----------------------------------------------------------------------------------------
 struct ArrayArgs {
   const DevDesign* designs;
@@ -1211,11 +1214,115 @@ struct ArrayArgs {
   const double* B_drag;        // [ncase * NF][36]
   const double* Bmat;          // [ncase * NF][nn][9] (equal nn over the FOWTs)
   const double* K;             // [6 NF][6 NF] array stiffness, or NULL
-  rh_c128* Xi;                 // [ncase][6 NF][nw]
+  rh_c128* Xi;                 // [ncase][6 NF][nw]: F from k_array_exc, then the response
   int nn_max, nm_max;          // largest node / member counts of the designs (dynamic LDS layout)
 };
-__host__ __device__ inline size_t array_resp_smem(int NF, int nn_max, int nm_max) {
-  return sizeof(double) * (size_t)NF * (5 * nn_max + 18 * nm_max) + sizeof(int) * (size_t)NF * (nm_max + 1);
+constexpr int kArrExcThreads = 256;
+__host__ __device__ inline size_t array_exc_smem(int nn_max, int nm_max) {
+  return sizeof(double) * (size_t)(5 * nn_max + 18 * nm_max) + sizeof(int) * (size_t)(nm_max + 1);
+}
+
+// one (case, FOWT) entry per workgroup: blockIdx.x = ic * NF + f, every bin of the grid
+template <int NF>
+__global__ __launch_bounds__(kArrExcThreads) void k_array_exc(ArrayArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  const int nnA = a.nn_max, nmA = a.nm_max;
+  double* alf = dyn;                                          // [nnA][5] node drag coefficients
+  double* mbf = alf + (size_t)nnA * 5;                        // [18][nmA] member factors cq, c1, c2
+  int* ms = reinterpret_cast<int*>(mbf + (size_t)18 * nmA);   // [nmA + 1] member node ranges
+  const int tid = (int)threadIdx.x;
+  const size_t e = blockIdx.x;
+  const int ic = (int)(e / NF), f = (int)(e % NF);
+  const rh_design& d = a.designs[a.design_idx[e]].d;
+  const int nn = d.nn, nm = d.nm, nw = d.nw, head = a.head[e];
+  const double* Bm = a.Bmat + e * nn * 9;
+  for (int n = tid; n < nn; n += kArrExcThreads) {
+    double c[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {   // e^T Bmat e for e = q, p1, p2
+      const int fx = k == 0 ? RH_NF_QX : k == 1 ? RH_NF_P1X : RH_NF_P2X;
+      const double ex = nf(d.node, nn, fx, n), ey = nf(d.node, nn, fx + 1, n), ez = nf(d.node, nn, fx + 2, n);
+      const double* B = Bm + 9 * n;
+      c[k] = ex * (B[0] * ex + B[1] * ey + B[2] * ez) + ey * (B[3] * ex + B[4] * ey + B[5] * ez) +
+             ez * (B[6] * ex + B[7] * ey + B[8] * ez);
+    }
+    const double t = nf(d.node, nn, RH_NF_T, n);
+    double* A = alf + (size_t)n * 5;
+    A[0] = c[0];
+    A[1] = c[1];
+    A[2] = c[2];
+    A[3] = t * c[1];
+    A[4] = t * c[2];
+  }
+  for (int i = tid; i < 18 * nm; i += kArrExcThreads) mbf[(size_t)(i / nm) * nmA + i % nm] = d.memb[i];
+  for (int i = tid; i <= nm; i += kArrExcThreads) ms[i] = d.mstart[i];
+  __syncthreads();
+  const unsigned nw16 = (unsigned)nw * 16u;
+  const Buf bK = mkbuf(d.kproj + (size_t)head * nn * 3 * nw, (unsigned)nn * 3u * nw16);
+  const Buf bFe = mkbuf(d.finer + (size_t)head * 6 * nw, 6u * nw16);
+  rh_c128* Fo = a.Xi + ((size_t)ic * 6 * NF + 6 * f) * nw;
+#pragma unroll 1
+  for (int b0 = 0; b0 < nw; b0 += kArrExcThreads) {
+    if (!__builtin_amdgcn_ballot_w64(b0 + tid < nw)) continue;   // whole wave past the grid (uniform)
+    const int b = b0 + tid < nw ? b0 + tid : nw - 1;
+    const unsigned vb = (unsigned)b * 16u;
+    cd fe[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) fe[c] = bld(bFe, vb, c * nw16);
+    const double z = a.zeta[e * nw + b];
+    cd F[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
+    cd SQ = mk(0, 0), S1 = mk(0, 0), S2 = mk(0, 0), T1 = mk(0, 0), T2 = mk(0, 0);
+    int m = 0, mnext = nn > 0 ? ms[1] : 0;
+    auto fold = [&]() {   // close member m: F += its node sums (drag_exc_members)
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const double cq = mbf[(RH_MF_CQ0 + i) * nmA + m], c1 = mbf[(RH_MF_C10 + i) * nmA + m],
+                     c2 = mbf[(RH_MF_C20 + i) * nmA + m];
+        F[i] = add(F[i], add(add(scl(SQ, cq), scl(S1, c1)), scl(S2, c2)));
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const double p1 = mbf[(RH_MF_C10 + i) * nmA + m], p2 = mbf[(RH_MF_C20 + i) * nmA + m];
+        F[3 + i] = add(F[3 + i], sub(scl(T1, p2), scl(T2, p1)));
+      }
+      SQ = S1 = S2 = T1 = T2 = mk(0, 0);
+    };
+    constexpr int R = 4;
+    auto load = [&](cd (&K)[3], int n) {
+      const unsigned so = (unsigned)(n < nn ? n : nn - 1) * 3u * nw16;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) K[p] = bld(bK, vb, so + (unsigned)p * nw16);
+    };
+    cd K[R][3];
+#pragma unroll
+    for (int r = 0; r < R; ++r) load(K[r], r);
+    for (int n = 0; n < nn; n += R) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int nr = n + r;
+        if (nr < nn) {
+          while (nr == mnext) {   // uniform: member m ended before node nr
+            fold();
+            ++m;
+            mnext = ms[m + 1];
+          }
+          const double* An = alf + 5 * nr;
+          SQ = add(SQ, scl(K[r][0], An[0]));
+          S1 = add(S1, scl(K[r][1], An[1]));
+          S2 = add(S2, scl(K[r][2], An[2]));
+          T1 = add(T1, scl(K[r][1], An[3]));
+          T2 = add(T2, scl(K[r][2], An[4]));
+          load(K[r], nr + R);
+        }
+      }
+    }
+    if (nn > 0) fold();
+    if (b0 + tid < nw)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) st(Fo + (size_t)c * nw + b, add(scl(fe[c], z), scl(F[c], z)));
+  }
 }
 
 template <int NF>
@@ -1223,11 +1330,6 @@ __global__ __launch_bounds__(64) void k_array_resp(ArrayArgs a) {
   constexpr int N = 6 * NF;
   __shared__ double ks[N * N];        // K_array (uniform reads)
   __shared__ double mz[NF][4][36];    // per FOWT: M, B_lin (frequency-independent designs), C, B_drag
-  extern __shared__ __attribute__((aligned(16))) double dyn[];
-  const int nnA = a.nn_max, nmA = a.nm_max;
-  double* alf = dyn;                                          // [NF][nnA][5] node drag coefficients
-  double* mbf = alf + (size_t)NF * nnA * 5;                   // [NF][18][nmA] member factors cq, c1, c2
-  int* mst = reinterpret_cast<int*>(mbf + (size_t)NF * 18 * nmA);   // [NF][nmA + 1] member node ranges
   const int tid = (int)threadIdx.x;
   const int ic = blockIdx.y;
   for (int e = tid; e < N * N; e += 64) ks[e] = a.K ? a.K[e] : 0.0;
@@ -1240,28 +1342,6 @@ __global__ __launch_bounds__(64) void k_array_resp(ArrayArgs a) {
       mz[f][2][tid] = d.C[tid];
       mz[f][3][tid] = a.B_drag[((size_t)ic * NF + f) * 36 + tid];
     }
-    const int nn = d.nn, nm = d.nm;
-    const double* Bm = a.Bmat + ((size_t)ic * NF + f) * nn * 9;
-    for (int n = tid; n < nn; n += 64) {
-      double c[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {   // e^T Bmat e for e = q, p1, p2
-        const int fx = k == 0 ? RH_NF_QX : k == 1 ? RH_NF_P1X : RH_NF_P2X;
-        const double ex = nf(d.node, nn, fx, n), ey = nf(d.node, nn, fx + 1, n), ez = nf(d.node, nn, fx + 2, n);
-        const double* B = Bm + 9 * n;
-        c[k] = ex * (B[0] * ex + B[1] * ey + B[2] * ez) + ey * (B[3] * ex + B[4] * ey + B[5] * ez) +
-               ez * (B[6] * ex + B[7] * ey + B[8] * ez);
-      }
-      const double t = nf(d.node, nn, RH_NF_T, n);
-      double* A = alf + ((size_t)f * nnA + n) * 5;
-      A[0] = c[0];
-      A[1] = c[1];
-      A[2] = c[2];
-      A[3] = t * c[1];
-      A[4] = t * c[2];
-    }
-    for (int e = tid; e < 18 * nm; e += 64) mbf[((size_t)f * 18 + e / nm) * nmA + e % nm] = d.memb[e];
-    for (int e = tid; e <= nm; e += 64) mst[f * (nmA + 1) + e] = d.mstart[e];
   }
   __syncthreads();
   const rh_design& d0 = a.designs[a.design_idx[ic * NF]].d;
@@ -1299,72 +1379,9 @@ __global__ __launch_bounds__(64) void k_array_resp(ArrayArgs a) {
         }
     }
   };
-  // F_wave of FOWT f (raft/raft_model.py:1049-1061): zeta (F_iner + F_drag), the drag part
-  // member-factored (drag_exc_members) with the node loads 4 nodes ahead
-  auto excite = [&](int f, cd (&F)[6]) {
-    const size_t e = (size_t)ic * NF + f;
-    const rh_design& d = a.designs[a.design_idx[e]].d;
-    const int nn = d.nn, head = a.head[e];
-    const unsigned nw16 = (unsigned)nw * 16u, vb = (unsigned)b * 16u;
-    const Buf bK = mkbuf(d.kproj + (size_t)head * nn * 3 * nw, (unsigned)nn * 3u * nw16);
-    const Buf bFe = mkbuf(d.finer + (size_t)head * 6 * nw, 6u * nw16);
-    cd fe[6];
+  auto excite = [&](int f, cd (&F)[6]) {   // F_f of this lane's bin, from k_array_exc
 #pragma unroll
-    for (int c = 0; c < 6; ++c) fe[c] = bld(bFe, vb, c * nw16);
-    const double z = a.zeta[e * nw + b];
-    const double* A = alf + (size_t)f * nnA * 5;
-    const double* MB = mbf + (size_t)f * 18 * nmA;
-    const int* ms = mst + f * (nmA + 1);
-#pragma unroll
-    for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
-    cd SQ = mk(0, 0), S1 = mk(0, 0), S2 = mk(0, 0), T1 = mk(0, 0), T2 = mk(0, 0);
-    int m = 0, mnext = nn > 0 ? ms[1] : 0;
-    auto fold = [&]() {   // close member m: F += its node sums (drag_exc_members)
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const double cq = MB[(RH_MF_CQ0 + i) * nmA + m], c1 = MB[(RH_MF_C10 + i) * nmA + m],
-                     c2 = MB[(RH_MF_C20 + i) * nmA + m];
-        F[i] = add(F[i], add(add(scl(SQ, cq), scl(S1, c1)), scl(S2, c2)));
-      }
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const double p1 = MB[(RH_MF_C10 + i) * nmA + m], p2 = MB[(RH_MF_C20 + i) * nmA + m];
-        F[3 + i] = add(F[3 + i], sub(scl(T1, p2), scl(T2, p1)));
-      }
-      SQ = S1 = S2 = T1 = T2 = mk(0, 0);
-    };
-    constexpr int R = 4;
-    auto load = [&](cd (&K)[3], int n) {
-      const unsigned so = (unsigned)(n < nn ? n : nn - 1) * 3u * nw16;
-#pragma unroll
-      for (int p = 0; p < 3; ++p) K[p] = bld(bK, vb, so + (unsigned)p * nw16);
-    };
-    cd K[R][3];
-#pragma unroll
-    for (int r = 0; r < R; ++r) load(K[r], r);
-    for (int n = 0; n < nn; n += R) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int nr = n + r;
-        if (nr < nn) {
-          while (nr == mnext) {   // uniform: member m ended before node nr
-            fold();
-            ++m;
-            mnext = ms[m + 1];
-          }
-          const double* An = A + 5 * nr;
-          SQ = add(SQ, scl(K[r][0], An[0]));
-          S1 = add(S1, scl(K[r][1], An[1]));
-          S2 = add(S2, scl(K[r][2], An[2]));
-          T1 = add(T1, scl(K[r][1], An[3]));
-          T2 = add(T2, scl(K[r][2], An[4]));
-          load(K[r], nr + R);
-        }
-      }
-    }
-    if (nn > 0) fold();
-#pragma unroll
-    for (int c = 0; c < 6; ++c) F[c] = add(scl(fe[c], z), scl(F[c], z));
+    for (int c = 0; c < 6; ++c) F[c] = ld(Xo + (size_t)(6 * f + c) * nw + b);
   };
   if constexpr (NF == 1) {
     cd A[6][6], x[6];
@@ -1401,7 +1418,7 @@ __global__ __launch_bounds__(64) void k_array_resp(ArrayArgs a) {
     }
     auto X = [&](int i, int j) { return mk(xs[((6 * i + j) * 2) * 64 + tid], xs[((6 * i + j) * 2 + 1) * 64 + tid]); };
     cd g[6];
-    excite(1, g);                             // f2, formed once A is dead
+    excite(1, g);                             // f2, loaded once A is dead
     cd S[6][6];
     int ps[6];
     zload(1, S);                              // S = D - K21 X
