@@ -17,7 +17,7 @@
 // three terms have no cancellation to speak of: the XiStart motion term dominates most rows,
 // and z^2 |K|^2 rows with beta = 0 are sums of squares).
 //
-// Launch: grid (ceil(ncase / 16) case tiles of the launch order, ceil(nw / 128) bin chunks),
+// Launch: grid (ceil(ncase / 16) case tiles of the launch order, ceil(nw / 64) bin chunks),
 // 512 threads.  A tile's cases are handled one (design, heading) key at a time (a sorted launch
 // order gives one or two keys per tile); each wave takes 16-row blocks of the key's 3 nn rows.
 // Per (case, chunk) the row sums go to the case's Xi_last scratch, which the fast path does not
@@ -30,15 +30,15 @@ namespace rh {
 #define RH_A0_ABL 0   // timing ablations (tools/ubench variants): 1 no spectrum, 2 no member lookup, 4 no MFMA
 #endif
 constexpr int kA0Cases = 16;       // cases per tile (MFMA rows)
-constexpr int kA0Bins = 128;       // bins per chunk (32 MFMA steps of 4 bins)
+constexpr int kA0Bins = 64;        // bins per chunk (16 MFMA steps of 4 bins)
 constexpr int kA0Threads = 512;    // 8 waves: one 16-row block of the node projections each
 constexpr int kA0Pad = kA0Bins + 2;
-constexpr int kA0MaxRows = 3 * 1024;   // 3 nn, nn <= kMaxNodes (rh_abi.hip check_design)
-constexpr int kSub = 32;                // bins per LDS-staged sub-chunk of a row block
+constexpr int kSub = 16;                // bins per LDS-staged sub-chunk of a row block
 constexpr int kSubP = kSub + 1;         // its padded row length (complex)
-constexpr int kStageLd = 16 * kSub / 64;   // loads per lane per sub-chunk (two rows x 32 bins each)
+constexpr int kStageLd = 16 * kSub / 64;   // loads per lane per sub-chunk (four rows x 16 bins each)
 
 __host__ __device__ inline int a0_chunks(int nw) { return (nw + kA0Bins - 1) / kA0Bins; }
+__host__ __device__ inline size_t a0_smem(int nn_max) { return sizeof(double) * (size_t)3 * (nn_max > 0 ? nn_max : 1); }
 // the A(0) sums of a case fit in its Xi_last block ([6][nw] complex = 12 nw doubles)
 __host__ __device__ inline bool a0_fits(int nw, int nn) { return (size_t)a0_chunks(nw) * 3 * nn <= (size_t)12 * nw; }
 __device__ __forceinline__ double* a0_block(const CaseArgs& a, int ic, int nw) {
@@ -75,7 +75,7 @@ __device__ __forceinline__ double a0_beta_unit(const rh_design& d, int j) {
 __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
   __shared__ double su[kA0Cases][kA0Pad];   // z^2 of (case, bin of the chunk)
   __shared__ double sv[kA0Cases][kA0Pad];   // z w
-  __shared__ double sbeta[kA0MaxRows];      // beta_j of the current key's design
+  extern __shared__ __attribute__((aligned(16))) double sbeta[];   // [3 nn_max] beta_j of the current key's design
   __shared__ double2 stage[kA0Threads / 64][16 * kSubP];   // per wave: 16 rows x 32 bins of kproj
   __shared__ int kic[kA0Cases], kd[kA0Cases], kh[kA0Cases];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -153,15 +153,16 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
       const double m2b = -2.0 * beta;
       // The MFMA B fragment is 16 rows x 4 bins; read straight from the [row][bin] table it would
       // touch 16 rows 16 KB apart per load (nw = 1000), all in one memory channel.  So each wave
-      // stages its row block through LDS in sub-chunks of 32 bins: coalesced loads of two rows x
-      // 32 bins per instruction, the next sub-chunk in flight while the current one's MFMAs run.
+      // stages its row block through LDS in sub-chunks of 16 bins: loads of four rows x 16 bins
+      // (256 contiguous bytes each) per instruction, the next sub-chunk in flight while the current
+      // one's MFMAs run.
       double2* stg = stage[wv];
       cd L[kStageLd];
       auto load_sub = [&](int sc) {
 #pragma unroll
         for (int i = 0; i < kStageLd; ++i) {
-          const int row = rb * 16 + 2 * i + (lane >> 5);
-          L[i] = bld(bK, (unsigned)(b0 + kSub * sc + (lane & 31)) * 16u, (unsigned)(row < nrow ? row : nrow - 1) * nw16);
+          const int row = rb * 16 + 4 * i + (lane >> 4);
+          L[i] = bld(bK, (unsigned)(b0 + kSub * sc + (lane & 15)) * 16u, (unsigned)(row < nrow ? row : nrow - 1) * nw16);
         }
       };
       load_sub(0);
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
 #pragma unroll 1
       for (int sc = 0; sc < kA0Bins / kSub; ++sc) {
 #pragma unroll
-        for (int i = 0; i < kStageLd; ++i) stg[(2 * i + (lane >> 5)) * kSubP + (lane & 31)] = make_double2(L[i].r, L[i].i);
+        for (int i = 0; i < kStageLd; ++i) stg[(4 * i + (lane >> 4)) * kSubP + (lane & 15)] = make_double2(L[i].r, L[i].i);
         if (sc + 1 < kA0Bins / kSub) load_sub(sc + 1);
 #if RH_A0_ABL & 4   // timing ablation: staged operands consumed by one add each, no MFMA (wrong results)
 #pragma unroll

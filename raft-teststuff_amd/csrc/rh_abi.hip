@@ -437,7 +437,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   auto prep_a0 = [&]() -> int {
     if (!ctx->a0 || cases->first_iter != 0 || cases->Xi_init || !rh::a0_fits(nw, nnmax)) return RH_OK;
     dim3 g((cases->ncase + rh::kA0Cases - 1) / rh::kA0Cases, rh::a0_chunks(nw));
-    hipLaunchKernelGGL(rh::k_a0_sums, g, dim3(rh::kA0Threads), 0, s, a);
+    hipLaunchKernelGGL(rh::k_a0_sums, g, dim3(rh::kA0Threads), rh::a0_smem(nnmax), s, a);
     RH_HIP(hipGetLastError());
     a.a0 = 1;
     return RH_OK;
