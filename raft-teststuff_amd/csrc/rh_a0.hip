@@ -27,15 +27,14 @@
 namespace rh {
 
 #ifndef RH_A0_ABL
-#define RH_A0_ABL 0   // timing ablations (tools/ubench variants): 1 no spectrum, 2 no member lookup, 4 no MFMA
+#define RH_A0_ABL 0   // timing ablations (tools/ubench variants): 1 no spectrum, 4 no MFMA
 #endif
 constexpr int kA0Cases = 16;       // cases per tile (MFMA rows)
 constexpr int kA0Bins = 64;        // bins per chunk (16 MFMA steps of 4 bins)
-constexpr int kA0Threads = 512;    // 8 waves: one 16-row block of the node projections each
+constexpr int kA0Threads = 512;    // 8 waves, each taking 16-row blocks of the node projections
 constexpr int kA0Pad = kA0Bins + 2;
-constexpr int kSub = 16;                // bins per LDS-staged sub-chunk of a row block
-constexpr int kSubP = kSub + 1;         // its padded row length (complex)
-constexpr int kStageLd = 16 * kSub / 64;   // loads per lane per sub-chunk (four rows x 16 bins each)
+constexpr int kRowP = kA0Bins + 1;          // padded staged row (complex)
+constexpr int kRbLd = 16 * kA0Bins / 64;    // loads per lane per row block (one row x 64 bins each)
 
 __host__ __device__ inline int a0_chunks(int nw) { return (nw + kA0Bins - 1) / kA0Bins; }
 __host__ __device__ inline size_t a0_smem(int nn_max) { return sizeof(double) * (size_t)3 * (nn_max > 0 ? nn_max : 1); }
@@ -72,11 +71,17 @@ __device__ __forceinline__ double a0_beta_unit(const rh_design& d, int j) {
   return p == 0 ? sq : p == 1 ? s1 + t * d1 : s2 - t * d2;
 }
 
+// Data flow of a workgroup (latency-bound, so the loads are issued as early as possible):
+// each wave issues the loads of its first 16-row block (one row x 64 bins = 1 KB per load)
+// before the workgroup computes the tile's wave amplitudes and the rows' beta; a row block then
+// goes through the wave's LDS stage (the MFMA B fragment is 16 rows x 4 bins, which straight from
+// the [row][bin] table would be 16 scattered 64-byte pieces per load) while the wave's next row
+// block is already in flight.
 __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
   __shared__ double su[kA0Cases][kA0Pad];   // z^2 of (case, bin of the chunk)
   __shared__ double sv[kA0Cases][kA0Pad];   // z w
-  extern __shared__ __attribute__((aligned(16))) double sbeta[];   // [3 nn_max] beta_j of the current key's design
-  __shared__ double2 stage[kA0Threads / 64][16 * kSubP];   // per wave: 16 rows x 32 bins of kproj
+  __shared__ double2 stage[kA0Threads / 64][16 * kRowP];   // per wave: one 16-row block of kproj
+  extern __shared__ __attribute__((aligned(16))) double sbeta[];   // [3 nn_max] beta_j of the current key
   __shared__ int kic[kA0Cases], kd[kA0Cases], kh[kA0Cases];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -92,25 +97,11 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
   __syncthreads();
   const int nw = a.designs[kd[0]].d.nw;   // slot tile*16 < ncase; every design of a launch shares nw
   const int b0 = chunk * kA0Bins;
-  // wave amplitudes of the tile's cases over the chunk (sea_amplitude, as the solve's prologue)
-  for (int e = tid; e < kA0Cases * kA0Bins; e += kA0Threads) {
-    const int c = e / kA0Bins, bl = e % kA0Bins, b = b0 + bl;
-    const int ic = kic[c];
-    double zz = 0.0, w = 0.0;
-    if (ic >= 0 && b < nw) {
-      const rh_design& d = a.designs[kd[c]].d;
-      w = d.w[b];
-#if RH_A0_ABL & 1   // timing ablation: no spectrum (wrong results)
-      zz = a.c.Hs[ic];
-#else
-      zz = sea_amplitude(a.c.spectrum[ic], a.c.Hs[ic], a.c.Tp[ic], a.c.gamma[ic], w, d.dw);
-#endif
-    }
-    su[c][bl] = zz * zz;
-    sv[c][bl] = zz * w;
-  }
+  const unsigned nw16 = (unsigned)nw * 16u;
   const int mr = lane & 15, kr = lane >> 4;
   const double xs = a.c.XiStart;
+  double2* stg = stage[wv];
+  bool amplitudes = false;
   unsigned done = 0;
   for (;;) {   // one (design, heading) key of the tile at a time (block-uniform)
     int first = -1;
@@ -128,65 +119,60 @@ __global__ __launch_bounds__(kA0Threads) void k_a0_sums(CaseArgs a) {
     const rh_design& d = a.designs[kdes].d;
     const int nn = d.nn, nrow = 3 * nn, nrb = (nrow + 15) / 16;
     if (nn == 0) continue;
-    __syncthreads();   // the previous key's rows have read sbeta (and, first time, su / sv are written)
-#if RH_A0_ABL & 2   // timing ablation: no member lookup (wrong results)
-    for (int j = tid; j < nrow; j += kA0Threads) sbeta[j] = xs;
-#else
-    for (int j = tid; j < nrow; j += kA0Threads) sbeta[j] = xs * a0_beta_unit(d, j);
-#endif
-    __syncthreads();
-    const unsigned nw16 = (unsigned)nw * 16u;
     const Buf bK = mkbuf(d.kproj + (size_t)khead * nrow * nw, (unsigned)nrow * nw16);
-    const bool mine = ((match >> mr) & 1u) != 0;   // A row mr belongs to this key
-    double wsq = 0.0;                                // this design's sum of w^2 over the chunk
+    cd L[kRbLd];
+    auto load_rb = [&](int rb) {
 #pragma unroll
-    for (int q = 0; q < kA0Bins / 64; ++q) {
-      const int b = b0 + lane + 64 * q;
-      const double w = b < nw ? d.w[b] : 0.0;
-      wsq += w * w;
-    }
-    const double W2 = wave_sum(wsq);
-    for (int rb = wv; rb < nrb; rb += kA0Threads / 64) {
-      const int j = rb * 16 + mr;                    // this lane's row (B column mr)
-      const int jc = j < nrow ? j : nrow - 1;
-      const double beta = sbeta[jc];
-      const double m2b = -2.0 * beta;
-      // The MFMA B fragment is 16 rows x 4 bins; read straight from the [row][bin] table it would
-      // touch 16 rows 16 KB apart per load (nw = 1000), all in one memory channel.  So each wave
-      // stages its row block through LDS in sub-chunks of 16 bins: loads of four rows x 16 bins
-      // (256 contiguous bytes each) per instruction, the next sub-chunk in flight while the current
-      // one's MFMAs run.
-      double2* stg = stage[wv];
-      cd L[kStageLd];
-      auto load_sub = [&](int sc) {
-#pragma unroll
-        for (int i = 0; i < kStageLd; ++i) {
-          const int row = rb * 16 + 4 * i + (lane >> 4);
-          L[i] = bld(bK, (unsigned)(b0 + kSub * sc + (lane & 15)) * 16u, (unsigned)(row < nrow ? row : nrow - 1) * nw16);
-        }
-      };
-      load_sub(0);
-      a0d4 accu = {0.0, 0.0, 0.0, 0.0}, accv = accu;   // two independent MFMA chains
-#pragma unroll 1
-      for (int sc = 0; sc < kA0Bins / kSub; ++sc) {
-#pragma unroll
-        for (int i = 0; i < kStageLd; ++i) stg[(4 * i + (lane >> 4)) * kSubP + (lane & 15)] = make_double2(L[i].r, L[i].i);
-        if (sc + 1 < kA0Bins / kSub) load_sub(sc + 1);
-#if RH_A0_ABL & 4   // timing ablation: staged operands consumed by one add each, no MFMA (wrong results)
-#pragma unroll
-        for (int u = 0; u < kSub / 4; ++u) {
-          const double2 K = stg[mr * kSubP + 4 * u + kr];
-          accu[0] += K.x + K.y;
-        }
+      for (int i = 0; i < kRbLd; ++i) {
+        const int row = rb * 16 + i;
+        L[i] = bld(bK, (unsigned)(b0 + lane) * 16u, (unsigned)(row < nrow ? row : nrow - 1) * nw16);
+      }
+    };
+    int rb = wv;
+    if (rb < nrb) load_rb(rb);
+    if (!amplitudes) {   // the tile's wave amplitudes over the chunk (sea_amplitude, as the solve's prologue)
+      amplitudes = true;
+      for (int e = tid; e < kA0Cases * kA0Bins; e += kA0Threads) {
+        const int c = e / kA0Bins, bl = e % kA0Bins, b = b0 + bl;
+        const int ic = kic[c];
+        double zz = 0.0, w = 0.0;
+        if (ic >= 0 && b < nw) {
+          const rh_design& dc = a.designs[kd[c]].d;
+          w = dc.w[b];
+#if RH_A0_ABL & 1   // timing ablation: no spectrum (wrong results)
+          zz = a.c.Hs[ic];
 #else
-#pragma unroll
-        for (int u = 0; u < kSub / 4; ++u) {
-          const double2 K = stg[mr * kSubP + 4 * u + kr];
-          const int bl = kSub * sc + 4 * u + kr;
-          const double ua = mine ? su[mr][bl] : 0.0, va = mine ? sv[mr][bl] : 0.0;
-          accu = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, K.x * K.x + K.y * K.y, accu, 0, 0, 0);
-          accv = __builtin_amdgcn_mfma_f64_16x16x4f64(va, m2b * K.y, accv, 0, 0, 0);
+          zz = sea_amplitude(a.c.spectrum[ic], a.c.Hs[ic], a.c.Tp[ic], a.c.gamma[ic], w, dc.dw);
+#endif
         }
+        su[c][bl] = zz * zz;
+        sv[c][bl] = zz * w;
+      }
+    }
+    __syncthreads();   // the previous key's rows have read sbeta
+    for (int j = tid; j < nrow; j += kA0Threads) sbeta[j] = xs * a0_beta_unit(d, j);
+    __syncthreads();
+    const bool mine = ((match >> mr) & 1u) != 0;   // A row mr belongs to this key
+    const double wl = b0 + lane < nw ? d.w[b0 + lane] : 0.0;
+    const double W2 = wave_sum(wl * wl);              // this design's sum of w^2 over the chunk
+    for (; rb < nrb; rb += kA0Threads / 64) {
+#pragma unroll
+      for (int i = 0; i < kRbLd; ++i) stg[i * kRowP + lane] = make_double2(L[i].r, L[i].i);
+      if (rb + kA0Threads / 64 < nrb) load_rb(rb + kA0Threads / 64);
+      const int j = rb * 16 + mr;                    // this lane's row (B column mr)
+      const double beta = sbeta[j < nrow ? j : nrow - 1];
+      const double m2b = -2.0 * beta;
+      a0d4 accu = {0.0, 0.0, 0.0, 0.0}, accv = accu;   // two independent MFMA chains
+#pragma unroll
+      for (int u = 0; u < kA0Bins / 4; ++u) {
+        const double2 K = stg[mr * kRowP + 4 * u + kr];
+        const int bl = 4 * u + kr;
+#if RH_A0_ABL & 4   // timing ablation: staged operands consumed by one add each, no MFMA (wrong results)
+        accu[0] += K.x + K.y;
+#else
+        const double ua = mine ? su[mr][bl] : 0.0, va = mine ? sv[mr][bl] : 0.0;
+        accu = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, K.x * K.x + K.y * K.y, accu, 0, 0, 0);
+        accv = __builtin_amdgcn_mfma_f64_16x16x4f64(va, m2b * K.y, accv, 0, 0, 0);
 #endif
       }
       // C[i][j]: lane holds rows i = kr + 4 r (cases) of column j = mr (rows of the table)
