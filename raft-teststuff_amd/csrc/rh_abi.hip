@@ -435,9 +435,11 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   // Cases that start from XiStart: phase A of iteration 0 for the whole batch as one GEMM
   // launch (rh_a0.hip), its sums in each case's Xi_last block (k_solve_lds reads them first).
   auto prep_a0 = [&]() -> int {
-    if (!ctx->a0 || cases->first_iter != 0 || cases->Xi_init || !rh::a0_fits(nw, nnmax)) return RH_OK;
-    dim3 g((cases->ncase + rh::kA0Cases - 1) / rh::kA0Cases, rh::a0_chunks(nw));
-    hipLaunchKernelGGL(rh::k_a0_sums, g, dim3(rh::kA0Threads), rh::a0_smem(nnmax), s, a);
+    if (!ctx->a0 || cases->first_iter != 0 || cases->Xi_init || !rh::a0_fits(nw, nnmax) ||
+        rh::kA0StaticLds + rh::a0_smem(nnmax, nmmax) > kMaxLds)
+      return RH_OK;
+    dim3 g((cases->ncase + rh::kA0Cases - 1) / rh::kA0Cases, (rh::a0_chunks(nw) + rh::kA0Cpb - 1) / rh::kA0Cpb);
+    hipLaunchKernelGGL(rh::k_a0_sums, g, dim3(rh::kA0Threads), rh::a0_smem(nnmax, nmmax), s, a);
     RH_HIP(hipGetLastError());
     a.a0 = 1;
     return RH_OK;
