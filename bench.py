@@ -98,11 +98,11 @@ def pmc_l2(kernel, kernel_ms):
     return None
 
 
-def solve_kernels(nw):
-    """Every kernel one rh_solve_cases call launches for this grid: on the fast path the
-    iteration-0 GEMM k_a0_sums (rh_a0.hip, cases starting from XiStart) before the solve."""
+def solve_kernels(nw, a0=False):
+    """Every kernel one rh_solve_cases call launches for this grid: with the opt-in iteration-0
+    GEMM (rh_set_a0, rh_a0.hip; off by default) k_a0_sums runs before the fast-path solve."""
     name = solve_kernel_name(nw)
-    return ("rh::k_a0_sums", name) if "k_solve_lds" in name else (name,)
+    return ("rh::k_a0_sums", name) if a0 and "k_solve_lds" in name else (name,)
 
 
 def solve_kernel_name(nw):

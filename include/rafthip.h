@@ -167,12 +167,12 @@ int rh_version(void);
  * kernel, the lane-pair kernel and the two-pass launch, all measured slower) */
 int rh_set_solver(rh_ctx* ctx, int which);
 
-/* Iteration-0 sums as a batch GEMM on this context (not part of the reference API; default 1):
- * when the fast path solves cases that start from XiStart (no Xi_init, first_iter 0), phase A
- * of their first iteration is formed for the whole batch by one MFMA launch (k_a0_sums) before
- * the solve, in each case's Xi_last block.  0 = every case forms it in its own workgroup.  The
+/* Iteration-0 sums as a batch GEMM on this context (not part of the reference API; default 0):
+ * 1 = when the fast path solves cases that start from XiStart (no Xi_init, first_iter 0), phase
+ * A of their first iteration is formed for the whole batch by one MFMA launch (k_a0_sums) before
+ * the solve, in each case's Xi_last block; 0 = every case forms it in its own workgroup.  The
  * two agree to rounding (the bin sums are grouped differently), with the same iteration counts
- * on the parity cases; used by the parity tests and for A/B timing. */
+ * on the parity cases.  Opt-in: measured slower on C2 and C4. */
 int rh_set_a0(rh_ctx* ctx, int on);
 
 /* Maximum cases per group of rh_cases.group_start: 1 in the shipped library (no grouped

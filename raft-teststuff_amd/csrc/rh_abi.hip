@@ -47,7 +47,8 @@ struct rh_ctx {
   int cur = 0;                          // slot of the last staging
   // tuning / cross-check knobs (per context: the ABI has no mutable process globals)
   bool force_general = false;   // rh_set_solver(ctx, 1): always use k_solve_cases (parity cross-checks)
-  bool a0 = true;               // rh_set_a0: iteration-0 phase A of the fast path as a batch GEMM (rh_a0.hip)
+  bool a0 = false;              // rh_set_a0: iteration-0 phase A of the fast path as a batch GEMM (rh_a0.hip;
+                                // opt-in: measured slower than the per-case phase A)
 #ifdef RH_VARIANTS
   bool no_group = false;        // rh_set_solver(ctx, 2): ignore group_start (one case per workgroup)
 #ifndef RH_PAIR_ON

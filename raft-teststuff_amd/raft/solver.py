@@ -165,7 +165,7 @@ def balanced_order(cases, head, nxcd=8):
     collects the long cases, and within a slice the long ones are dispatched first.  The
     order changes placement only, never results.  Measured on the C2 bench batch (512
     cases, 2 per CU): the last CU finishes after 9.5 instead of 10.5 case-iterations
-    (tools/ubench/makespan.py).  Finally each slice is grouped by (design, heading), stably."""
+    (tools/ubench/makespan.py)."""
     order = np.lexsort((-cases.Tp, head, cases.design_idx))
     G = len(order)
     q, r = G // nxcd, G % nxcd
@@ -183,12 +183,6 @@ def balanced_order(cases, head, nxcd=8):
             to_a[2 * m:] = True          # ... and the larger slice takes what is left
         out[a0:a1] = seg[to_a]
         out[a1:a2] = seg[~to_a]
-    # inside each XCD slice, cases of one (design, heading) are made contiguous again (stable:
-    # longest period first within each), so the 16-case tiles of the iteration-0 GEMM
-    # (csrc/rh_a0.hip, tiles of consecutive launch slots) mostly hold a single wave table
-    for x in range(nxcd):
-        sl = out[bounds[x]:bounds[x + 1]]
-        out[bounds[x]:bounds[x + 1]] = sl[np.lexsort((head[sl], cases.design_idx[sl]))]
     return out.astype(np.int32)
 
 

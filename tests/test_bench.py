@@ -61,10 +61,11 @@ def test_pmc_lookup_sections_and_exact_names(tmp_path, monkeypatch):
     p = tmp_path / "pmc.json"
     p.write_text(json.dumps(sec))
     monkeypatch.setattr(bench, "PMC_SUMMARY", str(p))
-    assert bench.pmc_traffic("solve", *bench.solve_kernels(1000)) == 33.0
+    assert bench.pmc_traffic("solve", *bench.solve_kernels(1000, a0=True)) == 33.0
+    assert bench.pmc_traffic("solve", *bench.solve_kernels(1000)) == 30.0
     assert bench.pmc_traffic("c4", "rh::k_a0_sums") == 100.0
     assert bench.pmc_traffic("qtf", "k_qtf_kay") == 10.0
-    assert bench.pmc_traffic("c4", *bench.solve_kernels(240)) is None
+    assert bench.pmc_traffic("c4", *bench.solve_kernels(240, a0=True)) is None
     p.write_text(json.dumps(sec["solve"]))
     assert bench.pmc_traffic("qtf", "rh::k_a0_sums") == 3.0
-    assert bench.solve_kernels(2000) == ("rh::k_a0_sums", "rh::k_solve_lds<2, 512, false, 2>")
+    assert bench.solve_kernels(2000) == ("rh::k_solve_lds<2, 512, false, 2>",)

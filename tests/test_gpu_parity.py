@@ -295,21 +295,22 @@ def test_fast_and_general_kernels_agree(tag, design, settings, ncase):
                                                        ("c2_nw200", "VolturnUS-S_example", None, 53),
                                                        ("c1_OC3spar", "OC3spar", None, 17)])
 def test_a0_gemm_agrees_with_per_case_phase_a(tag, design, settings, ncase):
-    """Iteration 0's phase-A sums as one batch GEMM (k_a0_sums, rh_set_a0(ctx, 1), the default)
-    against every workgroup forming them itself (rh_set_a0(ctx, 0)): identical iteration counts
-    and statuses, outputs within 1e-12 (only the grouping of the bin sums differs).  Random
-    headings, so the 16-case tiles hold several (design, heading) keys; ncase not a multiple of 16."""
+    """Iteration 0's phase-A sums as one batch GEMM (k_a0_sums, opt-in rh_set_a0(ctx, 1))
+    against every workgroup forming them itself (the default, rh_set_a0(ctx, 0)): identical
+    iteration counts and statuses, outputs within 1e-12 (only the grouping of the bin sums
+    differs).  Random headings, so the 16-case tiles hold several (design, heading) keys; ncase
+    not a multiple of 16."""
     from raft import _native as N
     T = load_golden(tag)
     m, f = make_model(design, T, settings)
     cases = random_cases(ncase, 7)
     want = ("psd", "std", "zeta", "B_drag", "margin")
-    a = m.analyzeCasesBatch(cases, want=want)
-    N.check(N.lib().rh_set_a0(N.context(0), 0), "rh_set_a0")
+    b = m.analyzeCasesBatch(cases, want=want)
+    N.check(N.lib().rh_set_a0(N.context(0), 1), "rh_set_a0")
     try:
-        b = m.analyzeCasesBatch(cases, want=want)
+        a = m.analyzeCasesBatch(cases, want=want)
     finally:
-        N.check(N.lib().rh_set_a0(N.context(0), 1), "rh_set_a0")
+        N.check(N.lib().rh_set_a0(N.context(0), 0), "rh_set_a0")
     np.testing.assert_array_equal(a["iters"], b["iters"])
     np.testing.assert_array_equal(a["status"], b["status"])
     for ic in range(ncase):

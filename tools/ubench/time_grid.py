@@ -2,9 +2,9 @@
 (max 0.2 Hz), 512 seeded JONSWAP cases, the default dispatch (k_solve_lds: one pass for
 nw <= 1024, two passes with XiLast in the Xi_last block up to 2048).  Prints the kernel that ran, ms per launch (HIP events
 over 10 launches), mean iterations and the SURVEY.md §8(d) roofline fraction.
-usage: python tools/ubench/time_grid.py NW[:noa0|:gen] [...]   (":noa0": rh_set_a0(ctx, 0) for that run,
-every case forming its iteration-0 phase-A sums in its own workgroup; ":gen": the general kernel
-k_solve_cases, rh_set_solver(ctx, 1))"""
+usage: python tools/ubench/time_grid.py NW[:a0|:gen] [...]   (":a0": rh_set_a0(ctx, 1) for that run,
+the opt-in batch GEMM of the iteration-0 phase-A sums; ":gen": the general kernel k_solve_cases,
+rh_set_solver(ctx, 1))"""
 import os
 import sys
 
@@ -54,7 +54,7 @@ def run(nw, a0=True, gen=False):
     nc, nr = int((circ != 0).sum()), int((circ == 0).sum())
     flops = float(sum(bench.flops_per_case(int(n), dd.nw, nc, nr, dd.nn) for n in iters))
     frac = flops / (ms * 1e-3) / bench.PEAK_FP64
-    N.check(N.lib().rh_set_a0(N.context(0), 1), "rh_set_a0")
+    N.check(N.lib().rh_set_a0(N.context(0), 0), "rh_set_a0")
     N.check(N.lib().rh_set_solver(N.context(0), 0), "rh_set_solver")
     kname = "rh::k_solve_cases (general)" if gen else bench.solve_kernel_name(dd.nw)
     print(f"nw={dd.nw:5d} a0={int(a0)} {kname:36s} {ms:8.3f} ms/launch  iters {iters.mean():.2f}  "
@@ -63,4 +63,4 @@ def run(nw, a0=True, gen=False):
 
 if __name__ == "__main__":
     for a in sys.argv[1:]:
-        run(int(a.split(":")[0]), not a.endswith(":noa0"), a.endswith(":gen"))
+        run(int(a.split(":")[0]), a.endswith(":a0"), a.endswith(":gen"))
