@@ -134,7 +134,9 @@ typedef struct {
 
 /* Outputs of rh_solve_cases (device buffers; NULL = not wanted). */
 typedef struct {
-  rh_c128* Xi;            /* [ncase][6][nw] response to sea state 0 (required)  */
+  rh_c128* Xi;            /* [ncase][6][nw] response to sea state 0, or NULL when only the
+                             linearisation is wanted (then psd, std and rao must be NULL too;
+                             nw <= 1024 only) */
   rh_c128* Xi_last;       /* [ncase][6][nw] scratch for the relaxed iterate (required) */
   int* iters;             /* [ncase] linear solves executed (required)         */
   int* status;            /* [ncase] RH_CASE_* (required)                      */

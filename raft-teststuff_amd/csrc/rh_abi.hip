@@ -380,8 +380,12 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   if (cases->ncase == 0) return RH_OK;
   if (!cases->design || !cases->head || !cases->spectrum || !cases->Hs || !cases->Tp || !cases->gamma)
     return fail(RH_EINVAL, "rh_solve_cases: null case array");
-  if (!out->Xi || !out->Xi_last || !out->iters || !out->status)
-    return fail(RH_EINVAL, "rh_solve_cases: Xi, Xi_last, iters and status outputs are required");
+  if (!out->Xi_last || !out->iters || !out->status)
+    return fail(RH_EINVAL, "rh_solve_cases: Xi_last, iters and status outputs are required");
+  if (!out->Xi && (out->psd || out->std || out->rao))
+    return fail(RH_EINVAL, "rh_solve_cases: psd, std and rao need the Xi output");
+  if (!out->Xi && designs[0].nw > 2 * rh::kLT)
+    return fail(RH_EINVAL, "rh_solve_cases: grids beyond %d bins need the Xi output", 2 * rh::kLT);
   if (cases->nIter < 0) return fail(RH_EINVAL, "rh_solve_cases: nIter=%d", cases->nIter);
   if (cases->first_iter < 0 || cases->first_iter > cases->nIter)
     return fail(RH_EINVAL, "rh_solve_cases: first_iter=%d outside [0, nIter=%d]", cases->first_iter, cases->nIter);

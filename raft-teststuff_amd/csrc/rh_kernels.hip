@@ -447,7 +447,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
     zt[j] = (b < nw) ? sea_amplitude(spec, Hs, Tp, gam, d.w[b], d.dw) : 0.0;
     if (b < nw && a.o.zeta) a.o.zeta[(size_t)ic * nw + b] = zt[j];
   }
-  rh_c128* Xo = a.o.Xi + (size_t)ic * 6 * nw;
+  rh_c128* Xo = a.o.Xi ? a.o.Xi + (size_t)ic * 6 * nw : nullptr;   // NULL: no response wanted
   rh_c128* XL = a.o.Xi_last + (size_t)ic * 6 * nw;
   const rh_c128* XI0 = a.c.Xi_init ? a.c.Xi_init + (size_t)ic * 6 * nw : nullptr;
 #pragma unroll
@@ -613,7 +613,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
           my_nan |= (x.r != x.r) || (x.i != x.i);
           my_ok = my_ok && (t < tol);
           my_tmax = fmax(my_tmax, t);
-          st(Xo + c * nw + b, x);
+          if (Xo) st(Xo + c * nw + b, x);
           if (XP) st(XP + c * nw + b, xlast);
           // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged
           st(XL + c * nw + b, add(scl(xlast, 0.2), scl(x, 0.8)));

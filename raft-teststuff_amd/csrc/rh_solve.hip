@@ -325,7 +325,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       }
     }
   }
-  rh_c128* Xo = a.o.Xi + c6;
+  rh_c128* Xo = a.o.Xi ? a.o.Xi + c6 : nullptr;   // NULL: the caller wants no response (C4 fixed point)
   rh_c128* XP = a.o.Xi_prev ? a.o.Xi_prev + c6 : nullptr;
   const double rho = d.rho;
   const int nloop = a.c.nIter + 1;
@@ -738,7 +738,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
         // iteration: the one whose test every (bin, DOF) passed, or the last allowed one
         // (raft/raft_model.py:996-1000).  So an entry is stored only when it passed its own test
         // or the loop is at its last iteration; the others are never read.
-        if (okj && (tt < tol || last_it)) {   // stores only
+        if (okj && (GX || Xo) && (tt < tol || last_it)) {   // stores only (Xi may be NULL with NP == 1)
           st_nt(Xo + c * nw + b, x);   // streamed: only the last iteration's value is kept
         }
         if (okj && XP) st(XP + c * nw + b, xlast);
@@ -862,7 +862,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
 #pragma unroll
   for (int j = 0; j < NBT; ++j) {
     const int b = tid + LT * j;
-    if (b >= nw) continue;
+    if (b >= nw || !Xo) continue;   // (psd, std and rao need Xi: checked by the caller)
     const double z = lz[b];
 #pragma unroll
     for (int c = 0; c < 6; ++c) {

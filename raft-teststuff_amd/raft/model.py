@@ -582,7 +582,7 @@ class Model:
         dds, cs, prep, dev = P["dds"], P["cs"], P["prep"], P["dev"]
         if marks:
             marks[0].record(torch.cuda.current_stream(dev))
-        res = solve_batch(dds, cs, self.nIter, self.XiStart, tol, want=("zeta", "Bmat", "B_drag"), prepared=prep)
+        res = solve_batch(dds, cs, self.nIter, self.XiStart, tol, want=("zeta", "Bmat", "B_drag", "noXi"), prepared=prep)
         if marks:
             marks[1].record(torch.cuda.current_stream(dev))
         arr = P["arr"]

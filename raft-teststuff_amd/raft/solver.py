@@ -53,8 +53,10 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
                 fext=None, stream=None, prepared=None, Xi_init=None, first_iter=0):
     """Run rh_solve_cases.  `designs`: list of DeviceDesign (same nw); `cases`: CaseSet.
     Returns a BatchResult of device tensors (stream-ordered; caller synchronises).
-    want may include "Xi_prev" (the un-relaxed XiLast of the final iteration) and "margin"
-    (the closest call of the convergence test per case, rh_solve_out.margin); Xi_init /
+    want may include "Xi_prev" (the un-relaxed XiLast of the final iteration), "margin"
+    (the closest call of the convergence test per case, rh_solve_out.margin) and "noXi" (no
+    response output: the linearisation only, for callers that form the response themselves,
+    Model.analyzeArrayBatch; then no psd / std / rao either); Xi_init /
     first_iter restart a fixed point from such a state (potSecOrder=1 second pass)."""
     d0 = designs[0]
     torch = d0.torch
@@ -68,7 +70,8 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     out = BatchResult()
     c128 = dict(dtype=torch.complex128, device=dev)
     f64 = dict(dtype=torch.float64, device=dev)
-    out["Xi"] = torch.empty([ncase, 6, nw], **c128)
+    if "noXi" not in want or nw > 1024:   # "noXi": the linearisation only (zeta / Bmat / B_drag);
+        out["Xi"] = torch.empty([ncase, 6, nw], **c128)   # the two-pass grids store it regardless
     xl = torch.empty([ncase, 6, nw], **c128)
     out["iters"] = torch.empty([ncase], dtype=torch.int32, device=dev)
     out["status"] = torch.empty([ncase], dtype=torch.int32, device=dev)
@@ -104,7 +107,7 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     cs.Xi_init, cs.first_iter = N.ptr(Xi_init), int(first_iter)
     cs.group_start, cs.ngroup = N.ptr(prep["group_start"]), int(prep["ngroup"])
     o = N.RhSolveOut()
-    o.Xi, o.Xi_last, o.iters, o.status = N.ptr(out["Xi"]), N.ptr(xl), N.ptr(out["iters"]), N.ptr(out["status"])
+    o.Xi, o.Xi_last, o.iters, o.status = N.ptr(out.get("Xi")), N.ptr(xl), N.ptr(out["iters"]), N.ptr(out["status"])
     for k in ["zeta", "B_drag", "Bmat", "psd", "std", "rao", "Z", "Xi_prev", "margin"]:
         setattr(o, k, N.ptr(out.get(k)))
     arr = (N.RhDesign * len(designs))(*[d.struct() for d in designs])

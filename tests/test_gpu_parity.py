@@ -436,3 +436,24 @@ def test_odd_grids(nw):
         smax = np.abs(b["std"]).max(axis=1, keepdims=True)
         assert np.all(np.abs(a["std"] - b["std"]) <= 1e-12 * smax)
         np.testing.assert_allclose(a["margin"], b["margin"], rtol=1e-9, atol=1e-15)
+
+
+def test_linearisation_only_solve_without_xi():
+    """rh_solve_out.Xi = NULL (solver.solve_batch want "noXi", what Model.analyzeArrayBatch asks
+    for): the same iteration counts, B_drag, Bmat and zeta bit for bit as with the response
+    stored; psd / std / rao without Xi are refused."""
+    from raft import _native as N
+    from raft.solver import CaseSet, solve_batch
+    T = load_golden("c2_nw200")
+    m, f = make_model("VolturnUS-S_example", T)
+    cases = random_cases(40, 13)
+    cs = CaseSet(np.zeros(len(cases), dtype=np.int32), [c["wave_heading"] for c in cases], ["JONSWAP"] * len(cases),
+                 [c["wave_height"] for c in cases], [c["wave_period"] for c in cases], [0.0] * len(cases))
+    dd = f.device_design()
+    a = solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=("zeta", "B_drag", "Bmat")).host()
+    b = solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=("zeta", "B_drag", "Bmat", "noXi")).host()
+    assert "Xi" not in b
+    for k in ("iters", "status", "zeta", "B_drag", "Bmat"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    with pytest.raises(Exception, match="need the Xi output"):
+        solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=("psd", "noXi"))
