@@ -190,7 +190,9 @@ int rh_group_cases(void);
 int rh_set_qtf_waves(rh_ctx* ctx, int waves);
 
 /* QTF pair-sum path of this context: 0 (default) = FP64 MFMA GEMMs when the grid is sorted
- * (rh_qtf_design.order == 1), 1 = the per-pair kernel k_qtf_pairs (parity cross-checks). */
+ * (rh_qtf_design.order == 1; 32 x 32 pair tiles for a whole QTF, 16 x 16 for a row-sharded
+ * one), 1 = the per-pair kernel k_qtf_pairs (parity cross-checks), 2 = the GEMMs on 16 x 16
+ * tiles only (A/B and cross-checks). */
 int rh_set_qtf_path(rh_ctx* ctx, int path);
 
 /* Unit-amplitude wave kinematics and strip-theory inertial excitation per heading.

@@ -64,6 +64,7 @@ struct rh_ctx {
   int ncu = 0;                  // compute units of the device (rh_ctx_create)
   int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
   bool qtf_direct = false;      // rh_set_qtf_path(ctx, 1): the per-pair kernel even on a sorted grid
+  bool qtf_t32 = true;          // rh_set_qtf_path(ctx, 2): 16 x 16 GEMM tiles for whole QTFs too (A/B)
   // per-stream scratch of rh_wave_tables (per-node forces, k_wave_tables_nodes ->
   // k_wave_force_sum): one buffer per stream, so stream order alone protects its reuse
   struct Scratch {
@@ -252,8 +253,11 @@ int rh_set_qtf_waves(rh_ctx* ctx, int waves) {
 
 int rh_set_qtf_path(rh_ctx* ctx, int path) {
   if (!ctx) return fail(RH_EINVAL, "rh_set_qtf_path: null context");
-  if (path != 0 && path != 1) return fail(RH_EINVAL, "rh_set_qtf_path: path=%d (0 = MFMA GEMMs when order == 1, 1 = per-pair kernel)", path);
+  if (path < 0 || path > 2)
+    return fail(RH_EINVAL, "rh_set_qtf_path: path=%d (0 = MFMA GEMMs when order == 1, 1 = per-pair kernel, "
+                           "2 = MFMA GEMMs on 16 x 16 tiles only)", path);
   ctx->qtf_direct = path == 1;
+  ctx->qtf_t32 = path == 0;
   return RH_OK;
 }
 
@@ -769,7 +773,12 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
     if (blocks > 0) {
       hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, s, *q, wk, rank, nrank);
       RH_HIP(hipGetLastError());
-      hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(2 * blocks), dim3(384), 0, s, *q, wk, qtf, rank, nrank, mirror);
+      if (nrank == 1 && mirror && ctx->qtf_t32) {   // a whole QTF: 32 x 32 pair tiles
+        const int nt32 = (nt + 1) / 2;
+        hipLaunchKernelGGL(rh::k_qtf_gemm32, dim3(nt32 * (nt32 + 1)), dim3(384), 0, s, *q, wk, qtf);
+      } else {
+        hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(2 * blocks), dim3(384), 0, s, *q, wk, qtf, rank, nrank, mirror);
+      }
       RH_HIP(hipGetLastError());
     }
     return RH_OK;

@@ -801,10 +801,15 @@ __device__ __forceinline__ void lcoef_block(const rh_qtf_design& q, const QtfWor
 #ifndef RH_QTF_PF
 #define RH_QTF_PF 4   // k-steps per operand batch (tools/ubench variant: 8)
 #endif
+#ifndef RH_QTF_SPLIT
+#define RH_QTF_SPLIT 0   // 1: even / odd k-steps in two accumulator sets (tools/ubench variant)
+#endif
 __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const rh_c128* __restrict__ B, size_t step,
                                             int nsteps, d4& p1, d4& p2, d4& p3) {
   constexpr int PF = RH_QTF_PF;
+#if RH_QTF_SPLIT
   d4 q1 = {0, 0, 0, 0}, q2 = q1, q3 = q1;
+#endif
   cd a[PF], b[PF];
 #pragma unroll
   for (int j = 0; j < PF; ++j) {
@@ -826,14 +831,20 @@ __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const
       }
     }
 #pragma unroll
-    for (int j = 0; j < PF; j += 2) {   // two accumulator sets: six independent MFMA chains
+    for (int j = 0; j < PF; j += 2) {
       if (PF > 4 && s + j >= nsteps) break;   // uniform (variant only)
       p1 = mfma64(a[j].r, b[j].r, p1);
       p2 = mfma64(a[j].i, b[j].i, p2);
       p3 = mfma64(a[j].r + a[j].i, b[j].r + b[j].i, p3);
+#if RH_QTF_SPLIT   // two accumulator sets (six independent MFMA chains): the round-2/3 order
       q1 = mfma64(a[j + 1].r, b[j + 1].r, q1);
       q2 = mfma64(a[j + 1].i, b[j + 1].i, q2);
       q3 = mfma64(a[j + 1].r + a[j + 1].i, b[j + 1].r + b[j + 1].i, q3);
+#else              // one chain per product, the k-step order of k_qtf_gemm32: sharded == whole, bit for bit
+      p1 = mfma64(a[j + 1].r, b[j + 1].r, p1);
+      p2 = mfma64(a[j + 1].i, b[j + 1].i, p2);
+      p3 = mfma64(a[j + 1].r + a[j + 1].i, b[j + 1].r + b[j + 1].i, p3);
+#endif
     }
     if (more) {
 #pragma unroll
@@ -843,13 +854,25 @@ __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const
       }
     }
   }
+#if RH_QTF_SPLIT
   p1 += q1;
   p2 += q2;
   p3 += q3;
+#endif
 }
 
 // row-major index of upper-triangle tile (T1, T2), T2 >= T1, of an nt x nt tile grid
 __device__ __forceinline__ int qtf_tile_id(int T1, int T2, int nt) { return T1 * nt - T1 * (T1 - 1) / 2 + (T2 - T1); }
+// tile (T1, T2) of the t-th upper-triangle tile in row-major order (block-uniform)
+__device__ __forceinline__ void qtf_tile_of(int t, int nt, int& T1, int& T2) {
+  T1 = 0;
+  while (t >= nt - T1) {
+    t -= nt - T1;
+    ++T1;
+  }
+  T2 = T1 + t;
+}
+
 
 // Q_d over the bilinear terms and the two potential channels for one tile and three DOFs.
 // Workgroup = 6 waves: wave w takes DOF 3 dg + (w % 3) (dg = the block's DOF half) and half
@@ -948,6 +971,161 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
     } else {
       st(up, Qf);
       st(qtf + ((size_t)i2 * n2 + i1) * 6 + d, cconj(Qf));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// 32 x 32 pair tiles for a whole (unsharded) QTF: each wave computes the four 16 x 16
+// sub-tiles of its DOF, so one pair of A fragments and one pair of B fragments feed 12 MFMAs
+// per k-step instead of one pair feeding 3 (k_qtf_gemm is latency-bound on its operand loads,
+// DESIGN.md §5).  Workgroup = 6 waves as in k_qtf_gemm (3 DOFs of the block's DOF half x two
+// halves of K, the second half's partial sums reaching the first through LDS); blocks are
+// (32-tile, DOF half) pairs.  Sub-tiles below the diagonal and beyond the grid are computed
+// (uniform control) but not stored; the Kim & Yue sums of k_qtf_kay are per 16 x 16 tile.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void cgemm4_steps(const rh_c128* __restrict__ A0, const rh_c128* __restrict__ A1,
+                                             const rh_c128* __restrict__ B0, const rh_c128* __restrict__ B1,
+                                             size_t step, int nsteps, d4 (&p)[4][3]) {
+  cd a[2][2], b[2][2];   // [step in batch][fragment]
+  auto ldk = [&](int s, cd (&x)[2][2], cd (&y)[2][2], int j) {
+    x[j][0] = ld(A0 + (size_t)s * step);
+    x[j][1] = ld(A1 + (size_t)s * step);
+    y[j][0] = ld(B0 + (size_t)s * step);
+    y[j][1] = ld(B1 + (size_t)s * step);
+  };
+  ldk(0, a, b, 0);
+  ldk(1, a, b, 1);
+#pragma unroll 1
+  for (int s = 0; s < nsteps; s += 2) {
+    cd an[2][2], bn[2][2];
+    const bool more = s + 2 < nsteps;
+    if (more) {
+      ldk(s + 2, an, bn, 0);
+      ldk(s + 3, an, bn, 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          d4 (&q)[3] = p[2 * x + y];
+          q[0] = mfma64(a[j][x].r, b[j][y].r, q[0]);
+          q[1] = mfma64(a[j][x].i, b[j][y].i, q[1]);
+          q[2] = mfma64(a[j][x].r + a[j][x].i, b[j][y].r + b[j][y].i, q[2]);
+        }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          a[j][x] = an[j][x];
+          b[j][x] = bn[j][x];
+        }
+    }
+  }
+}
+
+__global__ __launch_bounds__(384) void k_qtf_gemm32(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf) {
+  __shared__ double part[3][4][16][64];   // half 1's partial sums: [DOF][sub-tile][value][lane]
+  __shared__ double pscal[4][4][256];     // per sub-tile and pair: aux2 (w1 - w2) alpha+, alpha- (complex)
+  const int lane = (int)threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int half = w / 3, dl = w % 3;
+  const int n2 = q.n2, n2p = qtf_n2p(q), nt = n2p / 16, nt32 = (nt + 1) / 2, kp = qtf_kp(q), kq = qtf_kq(q);
+  const int slot = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int d = 3 * (slot & 1) + dl;
+  int T1, T2;
+  qtf_tile_of(slot >> 1, nt32, T1, T2);
+  const int mr = lane & 15, kr = lane >> 4;
+  const int i1b = 32 * T1, i2b = 32 * T2;
+  const int c10 = min(i1b + mr, n2p - 1), c11 = min(i1b + 16 + mr, n2p - 1);   // operand columns (clamped
+  const int c20 = min(i2b + mr, n2p - 1), c21 = min(i2b + 16 + mr, n2p - 1);   // past the padded grid)
+  const size_t step = (size_t)4 * n2p;
+  const int ns = kp / 4, ns0 = 4 * ((ns / 4 + 1) / 2);
+  const int k0 = half == 0 ? 0 : ns0, nk = half == 0 ? ns0 : ns - ns0;
+  d4 pb[4][3], pc[4][3];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) pb[t][g] = pc[t][g] = d4{0, 0, 0, 0};
+  if (nk > 0) {
+    const size_t ra = ((size_t)d * kp + 4 * k0 + kr) * n2p, rb = ((size_t)4 * k0 + kr) * n2p;
+    cgemm4_steps(wk.L + ra + c10, wk.L + ra + c11, wk.R + rb + c20, wk.R + rb + c21, step, nk, pb);
+  }
+  {
+    const size_t ra = (((size_t)half * 6 + d) * kq + kr) * n2p, rb = ((size_t)half * kq + kr) * n2p;
+    cgemm4_steps(wk.Lp + ra + c10, wk.Lp + ra + c11, wk.Rp + rb + c20, wk.Rp + rb + c21, step, kq / 4, pc);
+  }
+  const double h = q.depth, g = q.g, bt = q.beta * kDeg2Rad, cb = cos(bt), sb = sin(bt);
+  if (half == 1) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        part[dl][t][r][lane] = pb[t][0][r] - pb[t][1][r];
+        part[dl][t][4 + r][lane] = pb[t][2][r] - pb[t][0][r] - pb[t][1][r];
+        part[dl][t][8 + r][lane] = pc[t][0][r] - pc[t][1][r];
+        part[dl][t][12 + r][lane] = pc[t][2][r] - pc[t][0][r] - pc[t][1][r];
+      }
+    // the pair scalars of the second-order potential (raft/helpers.py:254-291), as k_qtf_gemm
+    for (int e = (int)threadIdx.x - 192; e < 1024; e += 192) {
+      const int t = e >> 8, x = t >> 1, y = t & 1, el = e & 255;
+      const int i1 = min(i1b + 16 * x + (el >> 4), n2 - 1), i2 = min(i2b + 16 * y + (el & 15), n2 - 1);
+      const double w1 = q.w2[i1], k1 = q.k2[i1], w2 = q.w2[i2], k2 = q.k2[i2];
+      cd sp = mk(0, 0), sm = mk(0, 0);
+      if ((w1 != w2) && (k1 > 0) && (k2 > 0)) {
+        const double kx = k1 * cb - k2 * cb, ky = k1 * sb - k2 * sb;
+        const double nk = sqrt(kx * kx + ky * ky);
+        const double t1 = tanh(k1 * h), t2 = tanh(k2 * h), tnh = tanh(nk * h);
+        const double den12 = (w1 - w2) * (w1 - w2) / g - nk * tnh;
+        const double den21 = (w2 - w1) * (w2 - w1) / g - nk * tnh;
+        const double n12 = (k1 * k1) * (1 - t1 * t1) - 2 * k1 * k2 * (1 + t1 * t2);
+        const double n21 = (k2 * k2) * (1 - t2 * t2) - 2 * k2 * k1 * (1 + t2 * t1);
+        const cd g12 = scl(mk(0, -g / (2 * w1)), n12 / den12);
+        const cd g21 = scl(mk(0, -g / (2 * w2)), n21 / den21);
+        const cd a2w = scl(scl(add(g21, cconj(g12)), 0.5), w1 - w2);
+        const double e2 = exp(-2.0 * nk * h), ap = 1.0 / (1.0 + e2), am = e2 * ap;
+        sp = scl(a2w, ap);
+        sm = scl(a2w, am);
+      }
+      pscal[t][0][el] = sp.r;
+      pscal[t][1][el] = sp.i;
+      pscal[t][2][el] = sm.r;
+      pscal[t][3][el] = sm.i;
+    }
+  }
+  __syncthreads();
+  if (half == 1) return;
+  // + each sub-tile's Kim & Yue sums (k_qtf_kay), then the upper-triangle entry and its
+  // Hermitian mirror (raft/raft_fowt.py:1639-1640), the arithmetic of k_qtf_gemm's epilogue
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int x = t >> 1, y = t & 1;
+    const int s1 = 2 * T1 + x, s2 = 2 * T2 + y;   // 16 x 16 sub-tile
+    if (s1 >= nt || s2 >= nt || s2 < s1) continue;   // uniform
+    const double* ks = wk.KS + (size_t)qtf_tile_id(s1, s2, nt) * 12 * 256;
+    const int i2 = 16 * s2 + mr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i1 = 16 * s1 + kr + 4 * r;
+      if (i1 >= n2 || i2 >= n2 || i2 < i1) continue;
+      const int e = (kr + 4 * r) * 16 + mr;
+      const double mre = pb[t][0][r] - pb[t][1][r], mim = pb[t][2][r] - pb[t][0][r] - pb[t][1][r];
+      const double cre = pc[t][0][r] - pc[t][1][r], cim = pc[t][2][r] - pc[t][0][r] - pc[t][1][r];
+      const cd Pp = mk(cre, cim), Pm = mk(part[dl][t][8 + r][lane], part[dl][t][12 + r][lane]);
+      const cd Qd = add(mk(mre + part[dl][t][r][lane], mim + part[dl][t][4 + r][lane]),
+                        add(mul(mk(pscal[t][0][e], pscal[t][1][e]), Pp), mul(mk(pscal[t][2][e], pscal[t][3][e]), Pm)));
+      const int ek = kr * 16 + mr + 64 * r;   // kay_tile's element of this pair
+      const cd Qf = add(Qd, mk(ks[(2 * d) * 256 + ek], ks[(2 * d + 1) * 256 + ek]));
+      rh_c128* up = qtf + ((size_t)i1 * n2 + i2) * 6 + d;
+      if (i1 == i2) {
+        st(up, sub(add(Qf, cconj(Qf)), cconj(Qf)));
+      } else {
+        st(up, Qf);
+        st(qtf + ((size_t)i2 * n2 + i1) * 6 + d, cconj(Qf));
+      }
     }
   }
 }
@@ -1127,15 +1305,6 @@ __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& 
   }
 }
 
-// tile (T1, T2) of the t-th upper-triangle tile in row-major order (block-uniform)
-__device__ __forceinline__ void qtf_tile_of(int t, int nt, int& T1, int& T2) {
-  T1 = 0;
-  while (t >= nt - T1) {
-    t -= nt - T1;
-    ++T1;
-  }
-  T2 = T1 + t;
-}
 
 // The w1-side GEMM coefficients: grid (ceil(n2p / 64), 18 + nq + nmq), 512 threads (lcoef_block).
 __global__ __launch_bounds__(512) void k_qtf_lcoef(rh_qtf_design q, QtfWork wk, const double* __restrict__ M66) {

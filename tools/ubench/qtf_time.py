@@ -19,12 +19,15 @@ def main():
     ap.add_argument("--save")
     ap.add_argument("--check")
     ap.add_argument("--n", type=int, default=50)
+    ap.add_argument("--path", type=int, default=0, help="rh_set_qtf_path (0 default, 2 = 16 x 16 GEMM tiles)")
     a = ap.parse_args()
     import torch
     import bench
     from raft.qtf import QtfDevice
     T, f, dd, X, M66, w2, k2 = bench.build_qtf(0)
     qd = QtfDevice(f, w2, k2, 0.0, 0)
+    from raft import _native as N
+    N.check(N.lib().rh_set_qtf_path(N.context(0), a.path), "rh_set_qtf_path")
     for _ in range(5):
         q = qd.qtf(dd.w, X, M66)
     torch.cuda.synchronize()
