@@ -861,6 +861,46 @@ __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const
 #endif
 }
 
+// The pair scalars of the second-order potential (raft/helpers.py:254-291) of pair (w1, w2):
+// aux2 (w1 - w2) alpha+ and aux2 (w1 - w2) alpha-, with
+// cosh(nk (z+h)) / cosh(nk h) = alpha+ e^{nk z} + alpha- e^{-nk z}.  Shared by both GEMM kernels,
+// with contraction off, so that they produce the same bits.
+__device__ __forceinline__ void qtf_pot_scalars(double w1, double k1, double w2, double k2, double cb, double sb,
+                                                double h, double g, cd& sp, cd& sm) {
+#pragma clang fp contract(off)
+  sp = cd{0.0, 0.0};
+  sm = cd{0.0, 0.0};
+  if ((w1 != w2) && (k1 > 0) && (k2 > 0)) {
+    const double kx = k1 * cb - k2 * cb, ky = k1 * sb - k2 * sb;
+    const double nk = sqrt(kx * kx + ky * ky);
+    const double t1 = tanh(k1 * h), t2 = tanh(k2 * h), tnh = tanh(nk * h);
+    const double den12 = (w1 - w2) * (w1 - w2) / g - nk * tnh;
+    const double den21 = (w2 - w1) * (w2 - w1) / g - nk * tnh;
+    const double n12 = (k1 * k1) * (1 - t1 * t1) - 2 * k1 * k2 * (1 + t1 * t2);
+    const double n21 = (k2 * k2) * (1 - t2 * t2) - 2 * k2 * k1 * (1 + t2 * t1);
+    const double f12 = n12 / den12, f21 = n21 / den21;
+    // g12 = i (-g / (2 w1)) f12, g21 = i (-g / (2 w2)) f21: purely imaginary
+    const double g12i = (-g / (2 * w1)) * f12, g21i = (-g / (2 * w2)) * f21;
+    // a2w = 0.5 (g21 + conj(g12)) (w1 - w2)
+    const double a2wi = ((g21i - g12i) * 0.5) * (w1 - w2);
+    const double e2 = exp(-2.0 * nk * h), ap = 1.0 / (1.0 + e2), am = e2 * ap;
+    sp = cd{0.0 * ap, a2wi * ap};
+    sm = cd{0.0 * am, a2wi * am};
+  }
+}
+
+// The final sum of a pair entry, shared by k_qtf_gemm and k_qtf_gemm32 and written out with
+// contraction off, so that both kernels (the row-sharded and the whole QTF) produce the same
+// bits: (bilinear part + second half) + (alpha+ P+ + alpha- P-) + Kim & Yue.
+__device__ __forceinline__ cd qtf_pair_sum(double mre, double mim, double hre, double him, double ppr, double ppi,
+                                           double pmr, double pmi, double spr, double spi, double smr, double smi,
+                                           double ksr, double ksi) {
+#pragma clang fp contract(off)
+  const double pr = (spr * ppr - spi * ppi) + (smr * pmr - smi * pmi);
+  const double pi = (spr * ppi + spi * ppr) + (smr * pmi + smi * pmr);
+  return cd{((mre + hre) + pr) + ksr, ((mim + him) + pi) + ksi};
+}
+
 // row-major index of upper-triangle tile (T1, T2), T2 >= T1, of an nt x nt tile grid
 __device__ __forceinline__ int qtf_tile_id(int T1, int T2, int nt) { return T1 * nt - T1 * (T1 - 1) / 2 + (T2 - T1); }
 // tile (T1, T2) of the t-th upper-triangle tile in row-major order (block-uniform)
@@ -923,23 +963,8 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
     // cosh(nk (z+h)) / cosh(nk h) = alpha+ e^{nk z} + alpha- e^{-nk z}
     for (int e = (int)threadIdx.x - 192; e < 256; e += 192) {
       const int i1 = min(i1b + (e >> 4), n2 - 1), i2 = min(i2b + (e & 15), n2 - 1);
-      const double w1 = q.w2[i1], k1 = q.k2[i1], w2 = q.w2[i2], k2 = q.k2[i2];
-      cd sp = mk(0, 0), sm = mk(0, 0);
-      if ((w1 != w2) && (k1 > 0) && (k2 > 0)) {
-        const double kx = k1 * cb - k2 * cb, ky = k1 * sb - k2 * sb;
-        const double nk = sqrt(kx * kx + ky * ky);
-        const double t1 = tanh(k1 * h), t2 = tanh(k2 * h), tnh = tanh(nk * h);
-        const double den12 = (w1 - w2) * (w1 - w2) / g - nk * tnh;
-        const double den21 = (w2 - w1) * (w2 - w1) / g - nk * tnh;
-        const double n12 = (k1 * k1) * (1 - t1 * t1) - 2 * k1 * k2 * (1 + t1 * t2);
-        const double n21 = (k2 * k2) * (1 - t2 * t2) - 2 * k2 * k1 * (1 + t2 * t1);
-        const cd g12 = scl(mk(0, -g / (2 * w1)), n12 / den12);
-        const cd g21 = scl(mk(0, -g / (2 * w2)), n21 / den21);
-        const cd a2w = scl(scl(add(g21, cconj(g12)), 0.5), w1 - w2);
-        const double e2 = exp(-2.0 * nk * h), ap = 1.0 / (1.0 + e2), am = e2 * ap;
-        sp = scl(a2w, ap);
-        sm = scl(a2w, am);
-      }
+      cd sp, sm;
+      qtf_pot_scalars(q.w2[i1], q.k2[i1], q.w2[i2], q.k2[i2], cb, sb, h, g, sp, sm);
       pscal[0][e] = sp.r;
       pscal[1][e] = sp.i;
       pscal[2][e] = sm.r;
@@ -958,11 +983,10 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
     const int i1 = i1b + kr + 4 * r;
     if (i1 >= n2 || i2 >= n2 || i2 < i1) continue;
     const int e = (kr + 4 * r) * 16 + mr;
-    const cd Pp = mk(cre[r], cim[r]), Pm = mk(part[dl][8 + r][lane], part[dl][12 + r][lane]);
-    const cd Qd = add(mk(mre[r] + part[dl][r][lane], mim[r] + part[dl][4 + r][lane]),
-                      add(mul(mk(pscal[0][e], pscal[1][e]), Pp), mul(mk(pscal[2][e], pscal[3][e]), Pm)));
     const int ek = kr * 16 + mr + 64 * r;   // kay_tile's element of this pair
-    const cd Qf = add(Qd, mk(ks[(2 * d) * 256 + ek], ks[(2 * d + 1) * 256 + ek]));
+    const cd Qf = qtf_pair_sum(mre[r], mim[r], part[dl][r][lane], part[dl][4 + r][lane], cre[r], cim[r],
+                               part[dl][8 + r][lane], part[dl][12 + r][lane], pscal[0][e], pscal[1][e], pscal[2][e],
+                               pscal[3][e], ks[(2 * d) * 256 + ek], ks[(2 * d + 1) * 256 + ek]);
     rh_c128* up = qtf + ((size_t)i1 * n2 + i2) * 6 + d;
     if (!mirror) {
       st(up, Qf);
@@ -1073,23 +1097,8 @@ __global__ __launch_bounds__(384) void k_qtf_gemm32(rh_qtf_design q, QtfWork wk,
     for (int e = (int)threadIdx.x - 192; e < 1024; e += 192) {
       const int t = e >> 8, x = t >> 1, y = t & 1, el = e & 255;
       const int i1 = min(i1b + 16 * x + (el >> 4), n2 - 1), i2 = min(i2b + 16 * y + (el & 15), n2 - 1);
-      const double w1 = q.w2[i1], k1 = q.k2[i1], w2 = q.w2[i2], k2 = q.k2[i2];
-      cd sp = mk(0, 0), sm = mk(0, 0);
-      if ((w1 != w2) && (k1 > 0) && (k2 > 0)) {
-        const double kx = k1 * cb - k2 * cb, ky = k1 * sb - k2 * sb;
-        const double nk = sqrt(kx * kx + ky * ky);
-        const double t1 = tanh(k1 * h), t2 = tanh(k2 * h), tnh = tanh(nk * h);
-        const double den12 = (w1 - w2) * (w1 - w2) / g - nk * tnh;
-        const double den21 = (w2 - w1) * (w2 - w1) / g - nk * tnh;
-        const double n12 = (k1 * k1) * (1 - t1 * t1) - 2 * k1 * k2 * (1 + t1 * t2);
-        const double n21 = (k2 * k2) * (1 - t2 * t2) - 2 * k2 * k1 * (1 + t2 * t1);
-        const cd g12 = scl(mk(0, -g / (2 * w1)), n12 / den12);
-        const cd g21 = scl(mk(0, -g / (2 * w2)), n21 / den21);
-        const cd a2w = scl(scl(add(g21, cconj(g12)), 0.5), w1 - w2);
-        const double e2 = exp(-2.0 * nk * h), ap = 1.0 / (1.0 + e2), am = e2 * ap;
-        sp = scl(a2w, ap);
-        sm = scl(a2w, am);
-      }
+      cd sp, sm;
+      qtf_pot_scalars(q.w2[i1], q.k2[i1], q.w2[i2], q.k2[i2], cb, sb, h, g, sp, sm);
       pscal[t][0][el] = sp.r;
       pscal[t][1][el] = sp.i;
       pscal[t][2][el] = sm.r;
@@ -1114,11 +1123,10 @@ __global__ __launch_bounds__(384) void k_qtf_gemm32(rh_qtf_design q, QtfWork wk,
       const int e = (kr + 4 * r) * 16 + mr;
       const double mre = pb[t][0][r] - pb[t][1][r], mim = pb[t][2][r] - pb[t][0][r] - pb[t][1][r];
       const double cre = pc[t][0][r] - pc[t][1][r], cim = pc[t][2][r] - pc[t][0][r] - pc[t][1][r];
-      const cd Pp = mk(cre, cim), Pm = mk(part[dl][t][8 + r][lane], part[dl][t][12 + r][lane]);
-      const cd Qd = add(mk(mre + part[dl][t][r][lane], mim + part[dl][t][4 + r][lane]),
-                        add(mul(mk(pscal[t][0][e], pscal[t][1][e]), Pp), mul(mk(pscal[t][2][e], pscal[t][3][e]), Pm)));
       const int ek = kr * 16 + mr + 64 * r;   // kay_tile's element of this pair
-      const cd Qf = add(Qd, mk(ks[(2 * d) * 256 + ek], ks[(2 * d + 1) * 256 + ek]));
+      const cd Qf = qtf_pair_sum(mre, mim, part[dl][t][r][lane], part[dl][t][4 + r][lane], cre, cim,
+                                 part[dl][t][8 + r][lane], part[dl][t][12 + r][lane], pscal[t][0][e], pscal[t][1][e],
+                                 pscal[t][2][e], pscal[t][3][e], ks[(2 * d) * 256 + ek], ks[(2 * d + 1) * 256 + ek]);
       rh_c128* up = qtf + ((size_t)i1 * n2 + i2) * 6 + d;
       if (i1 == i2) {
         st(up, sub(add(Qf, cconj(Qf)), cconj(Qf)));
