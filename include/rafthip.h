@@ -189,10 +189,10 @@ int rh_group_cases(void);
  * Used by the tests and the kernel-tuning scripts. */
 int rh_set_qtf_waves(rh_ctx* ctx, int waves);
 
-/* QTF pair-sum path of this context: 0 (default) = FP64 MFMA GEMMs when the grid is sorted
- * (rh_qtf_design.order == 1; 32 x 32 pair tiles for a whole QTF, 16 x 16 for a row-sharded
- * one), 1 = the per-pair kernel k_qtf_pairs (parity cross-checks), 2 = the GEMMs on 16 x 16
- * tiles only (A/B and cross-checks). */
+/* QTF pair-sum path of this context: 0 (default) = FP64 MFMA GEMMs on 16 x 16 pair tiles when
+ * the grid is sorted (rh_qtf_design.order == 1), 1 = the per-pair kernel k_qtf_pairs (parity
+ * cross-checks), 2 = the GEMMs with 32 x 32 tiles for a whole QTF (measured slower; the same
+ * bits as 0). */
 int rh_set_qtf_path(rh_ctx* ctx, int path);
 
 /* Unit-amplitude wave kinematics and strip-theory inertial excitation per heading.
