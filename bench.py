@@ -379,26 +379,20 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
                       "parallelism": f"tile-sharded x{world} + all-gather of packed pairs"},
            "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                         "frac": achieved / PEAK_FP64,
-                        "traffic": pmc_traffic("qtf", "k_qtf_tables", "k_qtf_lcoef", "k_qtf_kay", "k_qtf_gemm"),
-                        "kernel": "rh_qtf_slender%s: k_qtf_tables, k_qtf_lcoef, k_qtf_kay, k_qtf_gemm (every launch of a "
+                        "traffic": pmc_traffic("qtf", "k_qtf_tables", "k_qtf_lk", "k_qtf_gemm"),
+                        "kernel": "rh_qtf_slender%s: k_qtf_tables, k_qtf_lk, k_qtf_gemm (every launch of a "
                                   "QTF on this rank)" % ("_rows" if world > 1 else ""),
                         "kernel_ms": ms, "flops_per_pair": fpp, "pairs_this_rank": mine,
                         "note": "FP64: the pair sum as MFMA GEMMs (k_qtf_gemm) + VALU Kim & Yue epilogue (DESIGN.md "
                                 "§4); peak = MI355X FP64 dense (matrix = vector rate); algorithmic FLOPs from SURVEY.md "
-                                "§8(d) over this rank's pairs; traffic = HBM bytes of all four launches of a QTF (PMC)"}}
+                                "§8(d) over this rank's pairs; traffic = HBM bytes of all three launches of a QTF (PMC)"}}
     return out
 
 
-def bench_c4(device, steps, world, rank, dist, ncase=512):
-    """C4 (BASELINE.json configs[3]): tests/test_data/VolturnUS-S_farm.yaml, 2 coupled FOWTs,
-    12-DOF system per bin, nw = 240; a step = `ncase` JONSWAP sea states per GPU through
-    Model.analyzeArrayBatch: every (case, FOWT) drag fixed point in one launch, the wave
-    excitation, the 12x12 system solves of every (case, bin) and the per-FOWT statistics; the
-    case table is prepared once (Model.prepareArrayBatch), as C2's prepare_batch.
-    Mooring: the reference-run fixture (FOWT C_moor + shared-line array stiffness), the
-    configuration tests/golden/c4_farm.npz pins.  Weak scaling (cases per GPU fixed)."""
+def build_c4(device, ncase=512, rank=0):
+    """The C4 model (farm of 2 FOWTs, fixture mooring) and its prepared batch of `ncase` sea
+    states (Model.prepareArrayBatch: case table + wave tables resident in HBM)."""
     import raft
-    import torch
     G = dict(np.load(os.path.join(ROOT, "tests", "golden", "c4_farm.npz")))
     with open(os.path.join(ROOT, "tests", "golden", "designs", "VolturnUS-S_farm.json")) as fh:
         design = json.load(fh)
@@ -416,7 +410,19 @@ def bench_c4(device, steps, world, rank, dist, ncase=512):
         f.calcStatics()
         f.calcHydroConstants()
     cases = sea_states(ncase, 20241020 + rank)
-    P = m.prepareArrayBatch(cases)               # case table + wave tables resident in HBM (as C2's prepare_batch)
+    return m, m.prepareArrayBatch(cases)
+
+
+def bench_c4(device, steps, world, rank, dist, ncase=512):
+    """C4 (BASELINE.json configs[3]): tests/test_data/VolturnUS-S_farm.yaml, 2 coupled FOWTs,
+    12-DOF system per bin, nw = 240; a step = `ncase` JONSWAP sea states per GPU through
+    Model.analyzeArrayBatch: every (case, FOWT) drag fixed point in one launch, the wave
+    excitation, the 12x12 system solves of every (case, bin) and the per-FOWT statistics; the
+    case table is prepared once (Model.prepareArrayBatch), as C2's prepare_batch.
+    Mooring: the reference-run fixture (FOWT C_moor + shared-line array stiffness), the
+    configuration tests/golden/c4_farm.npz pins.  Weak scaling (cases per GPU fixed)."""
+    import torch
+    m, P = build_c4(device, ncase, rank)
     for _ in range(2):
         r = m.analyzeArrayBatch(prepared=P, host=False)
     torch.cuda.synchronize()
@@ -455,11 +461,11 @@ def bench_c4(device, steps, world, rank, dist, ncase=512):
                          "frac": achieved / PEAK_FP64, "traffic": pmc_traffic("c4", *solve_kernels(dd.nw)),
                          "kernel": solve_kernel_name(dd.nw), "kernels_timed": list(solve_kernels(dd.nw)),
                          "chain_traffic": pmc_traffic("c4", *solve_kernels(dd.nw), "rh::k_array_exc<2>",
-                                                      "rh::k_array_resp<2>", "rh::k_motion_stats"),
+                                                      f"rh::k_array_resp<2, {str(dd.nw > 256).lower()}>"),
                          "kernel_ms": kern_ms, "flops_per_launch": flops,
                          "note": "the (case, FOWT) drag fixed point (kernels_timed); SURVEY.md §8(d) formula per "
                                  "(case, FOWT); traffic = HBM bytes of those launches, chain_traffic = of the whole "
-                                 "step (fixed point, excitation, block solve, motion statistics) from "
+                                 "step (fixed point, excitation, block solve with the motion statistics) from "
                                  + os.path.relpath(PMC_SUMMARY, ROOT)}}
 
 

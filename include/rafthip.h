@@ -192,7 +192,8 @@ int rh_set_qtf_waves(rh_ctx* ctx, int waves);
 /* QTF pair-sum path of this context: 0 (default) = FP64 MFMA GEMMs on 16 x 16 pair tiles when
  * the grid is sorted (rh_qtf_design.order == 1), 1 = the per-pair kernel k_qtf_pairs (parity
  * cross-checks), 2 = the GEMMs with 32 x 32 tiles for a whole QTF (measured slower; the same
- * bits as 0). */
+ * bits as 0), 3 = as 0 with the GEMM coefficients (k_qtf_lcoef) and the Kim & Yue sums
+ * (k_qtf_kay) as two launches instead of one (the same bits as 0). */
 int rh_set_qtf_path(rh_ctx* ctx, int path);
 
 /* Unit-amplitude wave kinematics and strip-theory inertial excitation per heading.
@@ -309,6 +310,17 @@ int rh_system_solve_batch(rh_ctx* ctx, int ncase, int nf, int nw, const rh_c128*
 int rh_array_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf, int ncase, const int* design_idx,
                       const int* head, const double* zeta, const double* B_drag, const double* Bmat, const double* K,
                       rh_c128* Xi, rh_stream stream);
+
+/* rh_array_response plus the motion statistics of every (case, FOWT) from the solution while
+ * it is in registers (no read-back of Xi): psd [ncase * nf][6][nw] = 0.5 |Xi|^2 / dw and
+ * std [ncase * nf][6] = sqrt(0.5 sum_w |Xi|^2), rotations in degrees -- the values, bit for bit,
+ * of rh_motion_stats(ctx, ncase * nf, 1, nw, dw, Xi, psd, std, stream) on the result
+ * (FOWT.getPSD / getRMS, raft/helpers.py:581-603).  Either output may be NULL; dw > 0 when one
+ * is requested. */
+int rh_array_response_stats(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf, int ncase,
+                            const int* design_idx, const int* head, const double* zeta, const double* B_drag,
+                            const double* Bmat, const double* K, rh_c128* Xi, double dw, double* psd, double* std_,
+                            rh_stream stream);
 
 /* ------------------------------------------------------------------------------------
  * Slender-body second-order QTF (FOWT.calcQTF_slenderBody, raft/raft_fowt.py:1385-1648)

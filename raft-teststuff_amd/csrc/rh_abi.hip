@@ -64,6 +64,7 @@ struct rh_ctx {
   int ncu = 0;                  // compute units of the device (rh_ctx_create)
   int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
   bool qtf_direct = false;      // rh_set_qtf_path(ctx, 1): the per-pair kernel even on a sorted grid
+  bool qtf_sep = false;         // rh_set_qtf_path(ctx, 3): k_qtf_lcoef and k_qtf_kay as two launches
   bool qtf_t32 = false;         // rh_set_qtf_path(ctx, 2): 32 x 32 GEMM tiles for a whole QTF (opt-in:
                                 // 68.7 vs 57.0 us per C3 QTF)
   // per-stream scratch of rh_wave_tables (per-node forces, k_wave_tables_nodes ->
@@ -254,11 +255,13 @@ int rh_set_qtf_waves(rh_ctx* ctx, int waves) {
 
 int rh_set_qtf_path(rh_ctx* ctx, int path) {
   if (!ctx) return fail(RH_EINVAL, "rh_set_qtf_path: null context");
-  if (path < 0 || path > 2)
+  if (path < 0 || path > 3)
     return fail(RH_EINVAL, "rh_set_qtf_path: path=%d (0 = MFMA GEMMs when order == 1, 1 = per-pair kernel, "
-                           "2 = MFMA GEMMs with 32 x 32 tiles for a whole QTF)", path);
+                           "2 = MFMA GEMMs with 32 x 32 tiles for a whole QTF, 3 = the GEMM coefficients and "
+                           "Kim & Yue as two launches)", path);
   ctx->qtf_direct = path == 1;
   ctx->qtf_t32 = path == 2;
+  ctx->qtf_sep = path == 3;
   return RH_OK;
 }
 
@@ -704,8 +707,17 @@ int rh_system_solve_batch(rh_ctx* ctx, int ncase, int nf, int nw, const rh_c128*
 int rh_array_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf, int ncase, const int* design_idx,
                       const int* head, const double* zeta, const double* B_drag, const double* Bmat, const double* K,
                       rh_c128* Xi, rh_stream stream) {
+  return rh_array_response_stats(ctx, designs, ndesign, nf, ncase, design_idx, head, zeta, B_drag, Bmat, K, Xi, 0.0,
+                                 nullptr, nullptr, stream);
+}
+
+int rh_array_response_stats(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf, int ncase,
+                            const int* design_idx, const int* head, const double* zeta, const double* B_drag,
+                            const double* Bmat, const double* K, rh_c128* Xi, double dw, double* psd, double* std_,
+                            rh_stream stream) {
   if (!ctx || !designs || !design_idx || !head || !zeta || !B_drag || !Bmat || !Xi)
     return fail(RH_EINVAL, "rh_array_response: null argument");
+  if ((psd || std_) && !(dw > 0)) return fail(RH_EINVAL, "rh_array_response_stats: dw=%g", dw);
   if (nf < 1 || nf > 2) return fail(RH_EINVAL, "rh_array_response: nf=%d (supported: 1, 2)", nf);
   if (ncase <= 0) return ncase == 0 ? RH_OK : fail(RH_EINVAL, "rh_array_response: ncase=%d", ncase);
   if (ndesign < 1) return fail(RH_EINVAL, "rh_array_response: ndesign=%d", ndesign);
@@ -723,15 +735,22 @@ int rh_array_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
-  rh::ArrayArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, B_drag, Bmat, K, Xi, nn, nmmax};
-  const dim3 ge(ncase * nf), g((nw + 63) / 64, ncase);   // excitation per (case, FOWT), then the solve
+  rh::ArrayArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, B_drag, Bmat, K, Xi, nn, nmmax, dw, psd, std_};
+  const dim3 ge(ncase * nf), g(ncase);   // excitation per (case, FOWT), then the solve (+ statistics) per case
+  const bool multi = nw > rh::kArrRespThreads;
+  const dim3 gr(rh::kArrRespThreads);
   if (nf == 1) {
     hipLaunchKernelGGL(rh::k_array_exc<1>, ge, dim3(rh::kArrExcThreads), lsm, s, a);
-    hipLaunchKernelGGL(rh::k_array_resp<1>, g, dim3(64), 0, s, a);
+    RH_HIP(hipGetLastError());
+    if (multi) hipLaunchKernelGGL((rh::k_array_resp<1, true>), g, gr, 0, s, a);
+    else hipLaunchKernelGGL((rh::k_array_resp<1, false>), g, gr, 0, s, a);
   } else {
     hipLaunchKernelGGL(rh::k_array_exc<2>, ge, dim3(rh::kArrExcThreads), lsm, s, a);
-    hipLaunchKernelGGL(rh::k_array_resp<2>, g, dim3(64), 0, s, a);
+    RH_HIP(hipGetLastError());
+    if (multi) hipLaunchKernelGGL((rh::k_array_resp<2, true>), g, gr, 0, s, a);
+    else hipLaunchKernelGGL((rh::k_array_resp<2, false>), g, gr, 0, s, a);
   }
+  RH_HIP(hipGetLastError());
   return designs_used(ctx, s);
 }
 
@@ -769,11 +788,21 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
     // (rh_qtf_mfma.hip)
     const int nt = n2p / 16, ntile = nt * (nt + 1) / 2;
     const int blocks = (ntile - rank + nrank - 1) / nrank;
-    hipLaunchKernelGGL(rh::k_qtf_lcoef, dim3(nb, 18 + q->nq + q->nmq), dim3(512), 0, s, *q, wk, M66);
-    RH_HIP(hipGetLastError());
-    if (blocks > 0) {
-      hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, s, *q, wk, rank, nrank);
+    if (blocks > 0 && !ctx->qtf_sep) {
+      // the Kim & Yue tiles (two per workgroup) and the GEMM coefficient blocks in one launch
+      const int nkb = (blocks + 1) / 2, nly = 18 + q->nq + q->nmq;
+      hipLaunchKernelGGL(rh::k_qtf_lk, dim3(nkb + nb * nly), dim3(rh::kLkThreads), 0, s, *q, wk, M66, rank, nrank,
+                         blocks, nkb, nb);
       RH_HIP(hipGetLastError());
+    } else {
+      hipLaunchKernelGGL(rh::k_qtf_lcoef, dim3(nb, 18 + q->nq + q->nmq), dim3(512), 0, s, *q, wk, M66);
+      RH_HIP(hipGetLastError());
+      if (blocks > 0) {
+        hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, s, *q, wk, rank, nrank);
+        RH_HIP(hipGetLastError());
+      }
+    }
+    if (blocks > 0) {
       if (nrank == 1 && mirror && ctx->qtf_t32) {   // opt-in for a whole QTF: 32 x 32 pair tiles
         const int nt32 = (nt + 1) / 2;
         hipLaunchKernelGGL(rh::k_qtf_gemm32, dim3(nt32 * (nt32 + 1)), dim3(384), 0, s, *q, wk, qtf);

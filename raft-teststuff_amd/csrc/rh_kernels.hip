@@ -1196,7 +1196,9 @@ __global__ __launch_bounds__(64) void k_system_solve_reg(int nw, const rh_c128* 
 //                 M / B_lin / C and the case's B_drag (the expression of fowt.Z,
 //                 raft/raft_model.py:944, 1013), Z_sys = blockdiag(Z_f) + K_array, and
 //                 Xi = Z_sys^-1 F solved by the 6x6 blocks as in k_system_solve_reg, reading
-//                 the lane's F from Xi and overwriting it with the solution.
+//                 the lane's F from Xi and overwriting it with the solution; optionally the
+//                 motion PSD / RMS of every FOWT from the solution in registers (k_motion_stats
+//                 with one row, the same arithmetic in the same order: no read-back of Xi).
 // The excitation is its own launch because the block solve's register peak and its LDS slab
 // hold k_array_resp at one wave per SIMD, where the node loop of the excitation could not hide
 // its wave-table loads (one fused kernel: 190 us per C4 step against 58 us for the excitation
@@ -1216,7 +1218,11 @@ struct ArrayArgs {
   const double* K;             // [6 NF][6 NF] array stiffness, or NULL
   rh_c128* Xi;                 // [ncase][6 NF][nw]: F from k_array_exc, then the response
   int nn_max, nm_max;          // largest node / member counts of the designs (dynamic LDS layout)
+  double dw = 0;               // motion statistics (k_array_resp): frequency step,
+  double* psd = nullptr;       // [ncase * NF][6][nw] or NULL,
+  double* stdv = nullptr;      // [ncase * NF][6] or NULL
 };
+constexpr int kArrRespThreads = 256;   // k_array_resp: one case per workgroup, bins in chunks of 256
 constexpr int kArrExcThreads = 256;
 __host__ __device__ inline size_t array_exc_smem(int nn_max, int nm_max) {
   return sizeof(double) * (size_t)(5 * nn_max + 18 * nm_max) + sizeof(int) * (size_t)(nm_max + 1);
@@ -1325,14 +1331,19 @@ __global__ __launch_bounds__(kArrExcThreads) void k_array_exc(ArrayArgs a) {
   }
 }
 
-template <int NF>
-__global__ __launch_bounds__(64) void k_array_resp(ArrayArgs a) {
+// MULTI: nw > kArrRespThreads, the bins in several chunks (the RMS sums are carried across them);
+// otherwise one chunk and nothing is live across the block solve but the solution.
+template <int NF, bool MULTI>
+__global__ __launch_bounds__(kArrRespThreads) void k_array_resp(ArrayArgs a) {
   constexpr int N = 6 * NF;
+  constexpr int W = kArrRespThreads / 64;
+  __shared__ double xs[NF == 2 ? 36 * 2 * kArrRespThreads : 1];   // NF == 2: the lane-private X slab [36][re, im][lanes]
   __shared__ double ks[N * N];        // K_array (uniform reads)
   __shared__ double mz[NF][4][36];    // per FOWT: M, B_lin (frequency-independent designs), C, B_drag
-  const int tid = (int)threadIdx.x;
-  const int ic = blockIdx.y;
-  for (int e = tid; e < N * N; e += 64) ks[e] = a.K ? a.K[e] : 0.0;
+  __shared__ double sred[W][N];       // motion RMS: the waves' sums
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ic = blockIdx.x;
+  for (int e = tid; e < N * N; e += kArrRespThreads) ks[e] = a.K ? a.K[e] : 0.0;
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
     const rh_design& d = a.designs[a.design_idx[ic * NF + f]].d;
@@ -1346,113 +1357,151 @@ __global__ __launch_bounds__(64) void k_array_resp(ArrayArgs a) {
   __syncthreads();
   const rh_design& d0 = a.designs[a.design_idx[ic * NF]].d;
   const int nw = d0.nw;
-  const int b0 = blockIdx.x * 64 + tid;
-  const bool live = b0 < nw;
-  const int b = live ? b0 : nw - 1;          // pad lanes solve the last bin and store nothing
   rh_c128* Xo = a.Xi + (size_t)ic * N * nw;
-  int zo;                        // a zero the compiler cannot see through: the LDS reads stay where
-  asm volatile("s_mov_b32 %0, 0" : "=s"(zo));   // they are used instead of being hoisted into registers
-  const double* ksz = ks + zo;
-  auto kk = [&](int i, int j) { return ksz[i * N + j]; };
-  // (0 + Z_f) + K_ff, Z_f = (-w^2 M + C) + i w (B + B_drag): the additions in the reference's order
-  auto zload = [&](int f, cd (&A)[6][6]) {
-    const rh_design& d = a.designs[a.design_idx[ic * NF + f]].d;
-    const double w = d.w[b], w2 = -(w * w);
-    const double* m = &mz[f][0][0] + zo;
-    if (d.mb_per_bin) {    // uniform: per-bin M and B (aero / BEM) from the design's arrays
-      const double* M = d.M + (size_t)b * 36;
-      const double* B = d.B + (size_t)b * 36;
+  const bool stats = a.psd || a.stdv;   // uniform
+  double ss[N];                         // per DOF row: this lane's sum of |x|^2 over its bins
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-          const int e = 6 * i + j;
-          A[i][j] = mk((w2 * M[e] + m[72 + e]) + kk(6 * f + i, 6 * f + j), w * (B[e] + m[108 + e]));
+  for (int k = 0; k < N; ++k) ss[k] = 0.0;
+  // |x|^2 of a solution row (rotations in degrees) into the PSD and the lane's RMS sums
+  // (k_motion_stats with nrow = 1: psd = 0 + 0.5 m2 / dw, the same bits)
+  auto add_stats = [&](int k, int b, cd x) {
+    const double m2 = abs2(k % 6 >= 3 ? scl(x, kRad2Deg) : x);
+    if (a.psd) a.psd[((size_t)ic * N + k) * nw + b] = 0.5 * m2 / a.dw;
+    ss[k] += m2;
+  };
+#pragma unroll 1
+  for (int c0 = 0; c0 < (MULTI ? nw : 1); c0 += kArrRespThreads) {
+    if (MULTI && !__builtin_amdgcn_ballot_w64(c0 + tid < nw)) continue;   // the whole wave past the grid (uniform)
+    const int b0 = c0 + tid;
+    const bool live = b0 < nw;
+    const int b = live ? b0 : nw - 1;          // pad lanes solve the last bin and store nothing
+    int zo;                        // a zero the compiler cannot see through: the LDS reads stay where
+    asm volatile("s_mov_b32 %0, 0" : "=s"(zo));   // they are used instead of being hoisted into registers
+    const double* ksz = ks + zo;
+    auto kk = [&](int i, int j) { return ksz[i * N + j]; };
+    // (0 + Z_f) + K_ff, Z_f = (-w^2 M + C) + i w (B + B_drag): the additions in the reference's order
+    auto zload = [&](int f, cd (&A)[6][6]) {
+      const rh_design& d = a.designs[a.design_idx[ic * NF + f]].d;
+      const double w = d.w[b], w2 = -(w * w);
+      const double* m = &mz[f][0][0] + zo;
+      if (d.mb_per_bin) {    // uniform: per-bin M and B (aero / BEM) from the design's arrays
+        const double* M = d.M + (size_t)b * 36;
+        const double* B = d.B + (size_t)b * 36;
+  #pragma unroll
+        for (int i = 0; i < 6; ++i)
+  #pragma unroll
+          for (int j = 0; j < 6; ++j) {
+            const int e = 6 * i + j;
+            A[i][j] = mk((w2 * M[e] + m[72 + e]) + kk(6 * f + i, 6 * f + j), w * (B[e] + m[108 + e]));
+          }
+      } else {
+  #pragma unroll
+        for (int i = 0; i < 6; ++i)
+  #pragma unroll
+          for (int j = 0; j < 6; ++j) {
+            const int e = 6 * i + j;
+            A[i][j] = mk((w2 * m[e] + m[72 + e]) + kk(6 * f + i, 6 * f + j), w * (m[36 + e] + m[108 + e]));
+          }
+      }
+    };
+    auto excite = [&](int f, cd (&F)[6]) {   // F_f of this lane's bin, from k_array_exc
+  #pragma unroll
+      for (int c = 0; c < 6; ++c) F[c] = ld(Xo + (size_t)(6 * f + c) * nw + b);
+    };
+    if constexpr (NF == 1) {
+      cd A[6][6], x[6];
+      excite(0, x);
+      zload(0, A);
+      lu_solve<6>(A, x);
+      if (live)
+  #pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          st(Xo + (size_t)i * nw + b, x[i]);
+          if (stats) add_stats(i, b, x[i]);
         }
     } else {
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
+      static_assert(NF == 2, "k_array_resp: one or two FOWTs");
+      // X = A^-1 K12 column by column to a lane-private LDS slab [36][re, im][lanes]
+      constexpr int T = kArrRespThreads;
+      cd y[6];
+      {
+        cd A[6][6];
+        int pa[6];
+        excite(0, y);                           // f1
+        zload(0, A);
+        lu_factor<6>(A, pa);
+        lu_apply<6>(A, pa, y);                  // y = A^-1 f1
+  #pragma unroll 1
         for (int j = 0; j < 6; ++j) {
-          const int e = 6 * i + j;
-          A[i][j] = mk((w2 * m[e] + m[72 + e]) + kk(6 * f + i, 6 * f + j), w * (m[36 + e] + m[108 + e]));
-        }
-    }
-  };
-  auto excite = [&](int f, cd (&F)[6]) {   // F_f of this lane's bin, from k_array_exc
-#pragma unroll
-    for (int c = 0; c < 6; ++c) F[c] = ld(Xo + (size_t)(6 * f + c) * nw + b);
-  };
-  if constexpr (NF == 1) {
-    cd A[6][6], x[6];
-    excite(0, x);
-    zload(0, A);
-    lu_solve<6>(A, x);
-    if (live)
-#pragma unroll
-      for (int i = 0; i < 6; ++i) st(Xo + (size_t)i * nw + b, x[i]);
-  } else {
-    static_assert(NF == 2, "k_array_resp: one or two FOWTs");
-    // X = A^-1 K12 column by column to a lane-private LDS slab [36][re, im][64 lanes]
-    __shared__ double xs[36 * 2 * 64];
-    cd y[6];
-    {
-      cd A[6][6];
-      int pa[6];
-      excite(0, y);                           // f1
-      zload(0, A);
-      lu_factor<6>(A, pa);
-      lu_apply<6>(A, pa, y);                  // y = A^-1 f1
-#pragma unroll 1
-      for (int j = 0; j < 6; ++j) {
-        cd c[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) c[i] = mk(kk(i, 6 + j), 0.0);
-        lu_apply<6>(A, pa, c);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          xs[((6 * i + j) * 2) * 64 + tid] = c[i].r;
-          xs[((6 * i + j) * 2 + 1) * 64 + tid] = c[i].i;
+          cd c[6];
+  #pragma unroll
+          for (int i = 0; i < 6; ++i) c[i] = mk(kk(i, 6 + j), 0.0);
+          lu_apply<6>(A, pa, c);
+  #pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            xs[((6 * i + j) * 2) * T + tid] = c[i].r;
+            xs[((6 * i + j) * 2 + 1) * T + tid] = c[i].i;
+          }
         }
       }
-    }
-    auto X = [&](int i, int j) { return mk(xs[((6 * i + j) * 2) * 64 + tid], xs[((6 * i + j) * 2 + 1) * 64 + tid]); };
-    cd g[6];
-    excite(1, g);                             // f2, loaded once A is dead
-    cd S[6][6];
-    int ps[6];
-    zload(1, S);                              // S = D - K21 X
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
+      auto X = [&](int i, int j) { return mk(xs[((6 * i + j) * 2) * T + tid], xs[((6 * i + j) * 2 + 1) * T + tid]); };
+      cd g[6];
+      excite(1, g);                             // f2, loaded once A is dead
+      cd S[6][6];
+      int ps[6];
+      zload(1, S);                              // S = D - K21 X
+  #pragma unroll
+      for (int i = 0; i < 6; ++i)
+  #pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          cd t = mk(0, 0);
+  #pragma unroll
+          for (int m = 0; m < 6; ++m) t = add(t, scl(X(m, j), kk(6 + i, m)));
+          S[i][j] = sub(S[i][j], t);
+        }
+  #pragma unroll
+      for (int i = 0; i < 6; ++i) {             // g = f2 - K21 A^-1 f1
         cd t = mk(0, 0);
-#pragma unroll
-        for (int m = 0; m < 6; ++m) t = add(t, scl(X(m, j), kk(6 + i, m)));
-        S[i][j] = sub(S[i][j], t);
+  #pragma unroll
+        for (int m = 0; m < 6; ++m) t = add(t, scl(y[m], kk(6 + i, m)));
+        g[i] = sub(g[i], t);
       }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {             // g = f2 - K21 A^-1 f1
-      cd t = mk(0, 0);
-#pragma unroll
-      for (int m = 0; m < 6; ++m) t = add(t, scl(y[m], kk(6 + i, m)));
-      g[i] = sub(g[i], t);
-    }
-    lu_factor<6>(S, ps);
-    lu_apply<6>(S, ps, g);                    // x2
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {             // x1 = A^-1 f1 - X x2
-      cd t = y[i];
-#pragma unroll
-      for (int m = 0; m < 6; ++m) t = sub(t, mul(X(i, m), g[m]));
-      y[i] = t;
-    }
-    if (live) {
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        st(Xo + (size_t)i * nw + b, y[i]);
-        st(Xo + (size_t)(6 + i) * nw + b, g[i]);
+      lu_factor<6>(S, ps);
+      lu_apply<6>(S, ps, g);                    // x2
+  #pragma unroll
+      for (int i = 0; i < 6; ++i) {             // x1 = A^-1 f1 - X x2
+        cd t = y[i];
+  #pragma unroll
+        for (int m = 0; m < 6; ++m) t = sub(t, mul(X(i, m), g[m]));
+        y[i] = t;
       }
+      if (live) {
+  #pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          st(Xo + (size_t)i * nw + b, y[i]);
+          st(Xo + (size_t)(6 + i) * nw + b, g[i]);
+        }
+        if (stats) {
+  #pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            add_stats(i, b, y[i]);
+            add_stats(6 + i, b, g[i]);
+          }
+        }
+      }
+    }
+  }
+  if (a.stdv) {   // uniform: wave sums, then the waves in order (k_motion_stats' reduction)
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const double s = wave_sum(ss[k]);
+      if (lane == 0) sred[wv][k] = s;
+    }
+    __syncthreads();
+    if (tid < N) {
+      double s = 0;
+      for (int w = 0; w < W; ++w) s += sred[w][tid];
+      a.stdv[(size_t)ic * N + tid] = sqrt(0.5 * s);
     }
   }
 }

@@ -1148,16 +1148,24 @@ __global__ __launch_bounds__(384) void k_qtf_gemm32(rh_qtf_design q, QtfWork wk,
 // phase x [s0 pf; s x pf] (the rows' translateForce3to6DOF) to the tile's LDS sum in member
 // order.  The next row's operands are loaded while the current row is reduced.
 
-constexpr int kKayW = 4;
+#ifndef RH_KAY_SPLIT
+#define RH_KAY_SPLIT 1   // 2 and 4 measured slower
+#endif
+constexpr int kKayM = 4;                   // Kim & Yue members per round
+constexpr int kKayS = RH_KAY_SPLIT;        // waves per member: each takes a contiguous part of its rows
+constexpr int kKayW = kKayM * kKayS;
 constexpr int kKayThreads = 64 * kKayW;
 // One pair tile's Kim & Yue sums by a group of kKayW waves (tid 0 .. kKayThreads - 1 of the
 // group) into acc[12][256]; live = false: the group has no tile and only joins the block's
 // barriers (every group of a block runs the same member rounds).  Every __syncthreads here is
-// a whole-block barrier: the caller's block is made of such groups only.
+// a whole-block barrier: the caller's block is made of such groups only.  A member's rows are
+// split into kKayS contiguous parts, one per wave; the parts' row sums meet in part order
+// (psg, LDS) before the member's phase is applied.
 __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& wk, int T1, int T2, bool live, int tid,
-                                         double (*acc)[256]) {
+                                         double (*acc)[256], double* psg) {
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int slot = wv / kKayS, part = wv % kKayS;
   const int n2 = q.n2, n2p = qtf_n2p(q), nt = n2p / 16, nkr = q.nkr;
   const int mr = lane & 15, kr = lane >> 4;
   const int i1b = 16 * T1, i2b = 16 * T2;
@@ -1170,27 +1178,28 @@ __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& 
   __syncthreads();
   int m = 0, j = 0;                 // scan state: member m is the j-th Kim & Yue member
   for (int round = 0;; ++round) {
-    // this wave's member of the round: the (round * kKayW + wv)-th member with rows
+    // this wave's member of the round: the (round * kKayM + slot)-th member with rows
     int mine = -1;
     while (m < q.nmq) {
       const bool has = ldsi(q.kstart + m + 1) > ldsi(q.kstart + m) && ldsi(q.kstart + m) < nkr;
       if (has) {
-        if (j == round * kKayW + wv) mine = m;
+        if (j == round * kKayM + slot) mine = m;
         ++j;
       }
       ++m;
-      if (j == (round + 1) * kKayW) break;
+      if (j == (round + 1) * kKayM) break;
     }
-    const bool any_left = j > round * kKayW;   // block-uniform: this round has at least one member
+    const bool any_left = j > round * kKayM;   // block-uniform: this round has at least one member
     if (!any_left) break;
     if (!live) mine = -1;                      // no tile: the rounds' barriers only
-    double sg[4][4];   // [s0, sx, sy, sz][element] of this wave's member
+    double sg[4][4];   // [s0, sx, sy, sz][element] of this wave's part of its member
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sg[c][r] = 0.0;
     if (mine >= 0) {
-      const int r0 = ldsi(q.kstart + mine), r1 = min(ldsi(q.kstart + mine + 1), nkr);
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sg[c][r] = 0.0;
+      const int r0 = ldsi(q.kstart + mine), r1m = min(ldsi(q.kstart + mine + 1), nkr);
+      const int ra = r0 + (r1m - r0) * part / kKayS, r1 = r0 + (r1m - r0) * (part + 1) / kKayS;
       double va[6], vb[6], vr[6];
       auto load_row = [&](int ir, double* A, double* B, double* Rr) {
         const size_t o1 = ((size_t)ir * kKayK + kr) * n2p + i1b + mr, o2 = ((size_t)ir * kKayK + kr) * n2p + i2b + mr;
@@ -1215,7 +1224,7 @@ __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& 
         w1v[r] = q.w2[i1];
       }
 #pragma unroll 1
-      for (int ir = r0; ir < r1; ++ir) {
+      for (int ir = ra; ir < r1; ++ir) {
         load_row(ir, va, vb, vr);
         double t1[4][6], t2[6];
         {
@@ -1278,12 +1287,28 @@ __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& 
         }
       }
     }
+    if (kKayS > 1) {   // the later parts' row sums to the first part's wave, added in part order
+      if (part > 0 && mine >= 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) psg[((slot * (kKayS - 1) + part - 1) * 16 + 4 * c + r) * 64 + lane] = sg[c][r];
+      }
+      __syncthreads();
+      if (part == 0 && mine >= 0) {
+        for (int pp = 1; pp < kKayS; ++pp)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sg[c][r] += psg[((slot * (kKayS - 1) + pp - 1) * 16 + 4 * c + r) * 64 + lane];
+      }
+    }
     // this round's members reach the tile sum in member order (deterministic): at its turn a
     // wave adds phase x [s0 pf; s x pf], the phase of its member's waterline point with
     // conj(F) when k1 < k2
 #pragma unroll 1
-    for (int v = 0; v < kKayW; ++v) {
-      if (wv == v && mine >= 0) {
+    for (int v = 0; v < kKayM; ++v) {
+      if (slot == v && part == 0 && mine >= 0) {
         const double wx = qm(q, RH_QM_WLX, mine), wy = qm(q, RH_QM_WLY, mine), wz = qm(q, RH_QM_WLZ, mine);
         const double pf0 = qm(q, RH_QM_PFX, mine), pf1 = qm(q, RH_QM_PFY, mine), pf2 = qm(q, RH_QM_PFZ, mine);
 #pragma unroll
@@ -1329,9 +1354,39 @@ __global__ __launch_bounds__(512) void k_qtf_lcoef(rh_qtf_design q, QtfWork wk, 
 __global__ __launch_bounds__(kKayThreads) __attribute__((amdgpu_waves_per_eu(RH_KAY_WPE))) void k_qtf_kay(
     rh_qtf_design q, QtfWork wk, int rank, int nrank) {
   __shared__ double acc[12][256];
+  __shared__ double psg[kKayS > 1 ? kKayM * (kKayS - 1) * 16 * 64 : 1];   // the parts' row sums
   int T1, T2;
   qtf_tile_of(rank + nrank * xcd_remap((int)blockIdx.x, (int)gridDim.x), qtf_n2p(q) / 16, T1, T2);
-  kay_tile(q, wk, T1, T2, true, (int)threadIdx.x, acc);
+  kay_tile(q, wk, T1, T2, true, (int)threadIdx.x, acc, psg);
+}
+
+// k_qtf_lcoef and k_qtf_kay in ONE launch (both read only the tables of k_qtf_tables): the
+// first nkb workgroups take two Kim & Yue pair tiles each (two kay_tile groups of kKayThreads),
+// the rest are k_qtf_lcoef's (x, y) blocks, so the coefficient blocks fill the CUs the Kim & Yue
+// tiles leave idle instead of running before them.  Per tile and per block the arithmetic is
+// that of the two kernels: the same bits.
+constexpr int kLkThreads = 2 * kKayThreads;
+
+static_assert(kLkThreads == 512, "k_qtf_lk: lcoef_block is a 512-thread block");
+__global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(RH_KAY_WPE))) void k_qtf_lk(
+    rh_qtf_design q, QtfWork wk, const double* __restrict__ M66, int rank, int nrank, int ntile, int nkb, int nbx) {
+  constexpr int kAcc = 12 * 256, kRed = 8 * 12 * 64;
+  constexpr int kSm = 2 * kAcc > kRed ? 2 * kAcc : kRed;
+  __shared__ double sm[kSm];                 // two Kim & Yue tile sums, or lcoef_block's wave sums
+  __shared__ double psg[kKayS > 1 ? 2 * kKayM * (kKayS - 1) * 16 * 64 : 1];
+  const int tid = (int)threadIdx.x;
+  if ((int)blockIdx.x < nkb) {               // block-uniform
+    const int grp = __builtin_amdgcn_readfirstlane(tid / kKayThreads);   // wave-uniform: the tile indices stay scalar
+    const int t = 2 * xcd_remap((int)blockIdx.x, nkb) + grp;   // this group's tile of the rank's order
+    const bool live = t < ntile;
+    int T1 = 0, T2 = 0;
+    if (live) qtf_tile_of(rank + nrank * t, qtf_n2p(q) / 16, T1, T2);
+    kay_tile(q, wk, T1, T2, live, tid - grp * kKayThreads, reinterpret_cast<double(*)[256]>(sm + grp * kAcc),
+             psg + (kKayS > 1 ? grp * kKayM * (kKayS - 1) * 16 * 64 : 0));
+  } else {
+    const int bl = (int)blockIdx.x - nkb;
+    lcoef_block(q, wk, M66, bl % nbx, bl / nbx, reinterpret_cast<double(*)[12][64]>(sm));
+  }
 }
 
 }  // namespace rh

@@ -565,14 +565,15 @@ class Model:
 
     def analyzeArrayBatch(self, cases=None, tol=0.01, host=True, marks=None, prepared=None):
         """The coupled-array response of many single-sea-state cases (raft/raft_model.py:852-1065
-        for nFOWT > 1) in three device calls instead of per-case, per-FOWT host round trips:
+        for nFOWT > 1) in two device calls instead of per-case, per-FOWT host round trips:
           1. every (case, FOWT) drag fixed point in one rh_solve_cases launch (outputs: zeta,
              the node drag matrices and B_drag);
           2. rh_array_response: per (case, bin) the wave excitation of each FOWT with its final
              linearisation, its impedance rebuilt from the design's matrices and B_drag,
              Z_sys = blockdiag(Z_i) + array mooring stiffness and Xi = Z_sys^-1 F_wave, in one
              launch with no per-bin Z or F array in HBM;
-          3. per-FOWT motion PSD / RMS (rh_motion_stats).
+             and the per-FOWT motion PSD / RMS from the solution in registers
+             (rh_array_response_stats: rh_motion_stats' values, bit for bit).
         Returns Xi [n, 6N, nw], iters / status [n, N], psd [n, N, 6, nw], std [n, N, 6], zeta.
         prepared: prepareArrayBatch(cases) of an earlier call (then `cases` is not needed).
         marks: optional two timing events recorded around the fixed-point launch (bench)."""
@@ -590,13 +591,12 @@ class Model:
         ctx = N.context(self.device)
         K = P["K"]
         X = torch.empty([n, 6 * nf, nw], dtype=torch.complex128, device=dev)
-        N.check(N.lib().rh_array_response(ctx, arr, nf, nf, n, N.ptr(prep["design"]), N.ptr(prep["head"]),
-                                          N.ptr(res["zeta"]), N.ptr(res["B_drag"]), N.ptr(res["Bmat"]), N.ptr(K),
-                                          N.ptr(X), s), "rh_array_response")
         psd = torch.empty([n * nf, 6, nw], dtype=torch.float64, device=dev)
         std = torch.empty([n * nf, 6], dtype=torch.float64, device=dev)
-        N.check(N.lib().rh_motion_stats(ctx, n * nf, 1, nw, float(self.fowtList[0].dw), N.ptr(X), N.ptr(psd),
-                                        N.ptr(std), s), "rh_motion_stats")
+        N.check(N.lib().rh_array_response_stats(ctx, arr, nf, nf, n, N.ptr(prep["design"]), N.ptr(prep["head"]),
+                                                N.ptr(res["zeta"]), N.ptr(res["B_drag"]), N.ptr(res["Bmat"]),
+                                                N.ptr(K), N.ptr(X), float(self.fowtList[0].dw), N.ptr(psd),
+                                                N.ptr(std), s), "rh_array_response_stats")
         out = {"Xi": X, "iters": res["iters"].view(n, nf), "status": res["status"].view(n, nf),
                "psd": psd.view(n, nf, 6, nw), "std": std.view(n, nf, 6), "zeta": res["zeta"].view(n, nf, nw)[:, 0]}
         out["_keep"] = (res, arr, K)

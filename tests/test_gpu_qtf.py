@@ -105,7 +105,9 @@ def test_mfma_path_matches_per_pair_kernel(T, beta_deg, grid):
     against the per-pair kernel k_qtf_pairs (rh_set_qtf_path(ctx, 1)): the same arithmetic
     reassociated, so they agree far inside the 1e-9 parity bar (1e-12 normwise, elementwise
     to 1e-12 of the largest entry), with the moving body and fixed, at 0 and 30 degrees (Q1).
-    The opt-in 32 x 32 GEMM tiles (rh_set_qtf_path(ctx, 2)) give the default's bits."""
+    The opt-in 32 x 32 GEMM tiles (rh_set_qtf_path(ctx, 2)) and the GEMM coefficients and Kim &
+    Yue sums as two launches (rh_set_qtf_path(ctx, 3), one merged launch by default) give the
+    default's bits."""
     import torch
     from raft import _native as N
     from raft.hydro_math import wave_numbers
@@ -125,13 +127,14 @@ def test_mfma_path_matches_per_pair_kernel(T, beta_deg, grid):
         X = torch.tensor(X0, dtype=torch.complex128, device=dd.device)
         out = []
         try:
-            for path in (0, 1, 2):
+            for path in (0, 1, 2, 3):
                 N.check(N.lib().rh_set_qtf_path(ctx, path), "rh_set_qtf_path")
                 out.append(qd.qtf(dd.w, X, M66).cpu().numpy())
         finally:
             N.check(N.lib().rh_set_qtf_path(ctx, 0), "rh_set_qtf_path")
-        a, b, c = out
+        a, b, c, d = out
         np.testing.assert_array_equal(c, a)      # 32 x 32 tiles (opt-in): the same bits as 16 x 16
+        np.testing.assert_array_equal(d, a)      # two launches: the same arithmetic, the same bits
         assert rel(a, b) < 1e-12, rel(a, b)
         np.testing.assert_allclose(a, b, rtol=0, atol=1e-12 * np.abs(b).max())
         i, j = np.tril_indices(len(w2), -1)

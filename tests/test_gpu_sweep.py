@@ -307,3 +307,40 @@ def test_array_response_equals_two_step_path(farm):
     ref = _two_step_array_response(m, P, res)
     for ic in range(len(cases)):
         assert np.linalg.norm(fused[ic] - ref[ic]) <= 1e-12 * np.linalg.norm(ref[ic]), ic
+
+
+@pytest.mark.parametrize("farm", [True, False], ids=["two_fowts", "one_fowt"])
+def test_array_statistics_equal_motion_stats(farm):
+    """analyzeArrayBatch's PSD / RMS, formed by k_array_resp from the solution in registers
+    (rh_array_response_stats), equal rh_motion_stats run on its Xi bit for bit, for two coupled
+    FOWTs and for one; plain rh_array_response gives the same Xi.  The one-FOWT grid of
+    c2_nw1000 (1000 bins) runs four bin chunks per workgroup."""
+    import torch
+    from raft import _native as N
+    from test_gpu_parity import make_model
+    if farm:
+        m, _ = _farm_model(load_golden("c4_farm"))
+    else:
+        m, _ = make_model("VolturnUS-S_example", load_golden("c2_nw1000"), {"min_freq": 0.0002})
+        assert m.nFOWT == 1 and m.nw > 3 * 256
+    rng = np.random.default_rng(47)
+    cases = [dict(wave_spectrum="JONSWAP", wave_period=float(rng.uniform(6, 18)), wave_height=float(rng.uniform(1, 10)),
+                  wave_heading=float(rng.choice([0, 45, 135, 270])), wave_gamma=0.0) for _ in range(12)]
+    P = m.prepareArrayBatch(cases)
+    out = m.analyzeArrayBatch(prepared=P, host=False)
+    nf, n, nw = m.nFOWT, len(cases), m.nw
+    X = out["Xi"]
+    psd = torch.empty([n * nf, 6, nw], dtype=torch.float64, device=X.device)
+    std = torch.empty([n * nf, 6], dtype=torch.float64, device=X.device)
+    ctx, s = N.context(m.device), N.stream_handle(torch, X.device)
+    N.check(N.lib().rh_motion_stats(ctx, n * nf, 1, nw, float(m.fowtList[0].dw), N.ptr(X), N.ptr(psd), N.ptr(std), s),
+            "rh_motion_stats")
+    np.testing.assert_array_equal(out["psd"].reshape(n * nf, 6, nw).cpu().numpy(), psd.cpu().numpy())
+    np.testing.assert_array_equal(out["std"].reshape(n * nf, 6).cpu().numpy(), std.cpu().numpy())
+    res, arr, K = out["_keep"]
+    prep = P["prep"]
+    X2 = torch.empty_like(X)
+    N.check(N.lib().rh_array_response(ctx, arr, nf, nf, n, N.ptr(prep["design"]), N.ptr(prep["head"]),
+                                      N.ptr(res["zeta"]), N.ptr(res["B_drag"]), N.ptr(res["Bmat"]), N.ptr(K),
+                                      N.ptr(X2), s), "rh_array_response")
+    np.testing.assert_array_equal(X2.cpu().numpy(), X.cpu().numpy())

@@ -24,6 +24,6 @@ def test_isa_gate():
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
     assert all(f"k_solve_lds<{k}>" in p.stdout for k in ("2, 512, false, 1", "2, 128, true, 1", "2, 512, false, 2"))
     assert "FAIL" not in p.stdout
-    assert "k_qtf_lcoef" in p.stdout and "k_array_resp<2>" in p.stdout
+    assert all(k in p.stdout for k in ("k_qtf_lk", "k_qtf_lcoef", "k_array_resp<2, false>", "k_array_resp<2, true>"))
     ratchets = [ln for ln in p.stdout.splitlines() if "ratchet" in ln]
     assert ratchets and all("k_solve_cases<" in ln for ln in ratchets), ratchets

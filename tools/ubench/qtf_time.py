@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--save")
     ap.add_argument("--check")
     ap.add_argument("--n", type=int, default=50)
-    ap.add_argument("--path", type=int, default=0, help="rh_set_qtf_path (0 default, 2 = 16 x 16 GEMM tiles)")
+    ap.add_argument("--path", type=int, default=0, help="rh_set_qtf_path (0 default, 2 = 32 x 32 GEMM tiles, 3 = coefficients and Kim & Yue as two launches)")
     a = ap.parse_args()
     import torch
     import bench
