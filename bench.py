@@ -423,19 +423,22 @@ def bench_c4(device, steps, world, rank, dist, ncase=512):
     configuration tests/golden/c4_farm.npz pins.  Weak scaling (cases per GPU fixed)."""
     import torch
     m, P = build_c4(device, ncase, rank)
-    for _ in range(2):
+    for _ in range(20):
         r = m.analyzeArrayBatch(prepared=P, host=False)
     torch.cuda.synchronize()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+    # two events per step, around the fixed-point launch; the step's device time runs from one
+    # step's first mark to the next one's (`end` closes the last step).  Every timing event is a
+    # barrier packet: 4 per step cost 19 us of a 0.55 ms step (tools/ubench/event_cost.py)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+    end = torch.cuda.Event(enable_timing=True)
     stream = torch.cuda.current_stream()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
-        ev[i][0].record(stream)
-        r = m.analyzeArrayBatch(prepared=P, host=False, marks=(ev[i][1], ev[i][2]))
-        ev[i][3].record(stream)
+        r = m.analyzeArrayBatch(prepared=P, host=False, marks=(ev[i][0], ev[i][1]))
+    end.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -443,8 +446,8 @@ def bench_c4(device, steps, world, rank, dist, ncase=512):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
-    kern_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
-    step_ms = float(np.mean([e[0].elapsed_time(e[3]) for e in ev]))
+    kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    step_ms = ev[0][0].elapsed_time(end) / steps   # from the first step's launch mark: host-side prep excluded
     iters = r["iters"].cpu().numpy()
     dd = m.fowtList[0].device_design()
     circ = dd.node[N_CIRC()].cpu().numpy()
@@ -688,9 +691,11 @@ def main():
     def step(e=None):
         """One C2 step: the per-heading wave tables of the design (k_wave_tables, all headings
         of the batch in one launch) and the batched drag fixed point (k_solve_lds)."""
+        if e is not None:
+            e[0].record(stream)
         dd.retabulate()
         if e is not None:
-            e.record(stream)
+            e[1].record(stream)
         return solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=want, prepared=prep)
 
     comm = torch.cuda.Stream(device) if world > 1 else None
@@ -716,7 +721,7 @@ def main():
     if not args.no_qtf:
         legs["qtf"] = bench_qtf(device, max(20, args.steps // 4), 10, world, rank, dist)
     if not args.no_c4:
-        legs["c4"] = bench_c4(device, max(3, args.steps // 4), world, rank, dist)
+        legs["c4"] = bench_c4(device, max(3, args.steps // 2), world, rank, dist)
     if not args.no_c5:
         legs["c5"] = bench_c5(device, max(3, args.steps // 4), world, rank, dist, pool, nproc)
     for _ in range(args.warmup):
@@ -729,18 +734,24 @@ def main():
     torch.cuda.synchronize()
 
     def timed(gather):
-        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        # two events per step: before the wave tables and before the solve; the solve of step i
+        # ends where step i + 1 begins (ev[i + 1][0], or `end` after the last step), nothing runs
+        # between them on the stream.  (Each timing event is a barrier packet: a third one per
+        # step cost 4 us of the 0.87 ms step, tools/ubench/event_cost.py.)
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+        end = torch.cuda.Event(enable_timing=True)
         pend = []
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            ev[i][0].record(stream)
-            r = step(ev[i][1])
-            ev[i][2].record(stream)
+            r = step(ev[i])
             if gather:
-                pend.append(gather_async(r, ev[i][2]))
+                e_done = torch.cuda.Event()
+                e_done.record(stream)
+                pend.append(gather_async(r, e_done))
+        end.record(stream)
         for work, _, _ in pend:
             work.wait()
         torch.cuda.synchronize()
@@ -758,14 +769,15 @@ def main():
             gms = pend[-1][2].elapsed_time(g1)   # the last step's gather (nothing overlaps it)
             out = pend[-1][1]
             assert out.shape[0] == world * args.ncase and torch.all(out[:, -1] >= 1)
-        return float(t.item()), ev, r, gms
+        return float(t.item()), (ev, end), r, gms
 
-    dt_ng, ev, res, _ = timed(False)
+    dt_ng, (ev, end), res, _ = timed(False)
     dt_max, gather_ms = dt_ng, None
     if world > 1:
         dt_max, _, _, gather_ms = timed(True)
     tab_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    kern_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    nxt = [e[0] for e in ev[1:]] + [end]
+    kern_ms = float(np.mean([e[1].elapsed_time(n) for e, n in zip(ev, nxt)]))
 
     iters = res["iters"].cpu().numpy()
     status = res["status"].cpu().numpy()
