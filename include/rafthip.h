@@ -316,11 +316,13 @@ int rh_array_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf
  * std [ncase * nf][6] = sqrt(0.5 sum_w |Xi|^2), rotations in degrees -- the values, bit for bit,
  * of rh_motion_stats(ctx, ncase * nf, 1, nw, dw, Xi, psd, std, stream) on the result
  * (FOWT.getPSD / getRMS, raft/helpers.py:581-603).  Either output may be NULL; dw > 0 when one
- * is requested. */
+ * is requested.  order: optional device permutation of the ncase * nf (case, FOWT) entries,
+ * sorted by design and heading (e.g. the rh_cases.order of the fixed point): each XCD then
+ * excites a contiguous slice of it and streams few wave tables (placement only, never results). */
 int rh_array_response_stats(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf, int ncase,
                             const int* design_idx, const int* head, const double* zeta, const double* B_drag,
                             const double* Bmat, const double* K, rh_c128* Xi, double dw, double* psd, double* std_,
-                            rh_stream stream);
+                            const int* order, rh_stream stream);
 
 /* ------------------------------------------------------------------------------------
  * Slender-body second-order QTF (FOWT.calcQTF_slenderBody, raft/raft_fowt.py:1385-1648)

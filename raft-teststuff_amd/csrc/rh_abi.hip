@@ -708,13 +708,13 @@ int rh_array_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf
                       const int* head, const double* zeta, const double* B_drag, const double* Bmat, const double* K,
                       rh_c128* Xi, rh_stream stream) {
   return rh_array_response_stats(ctx, designs, ndesign, nf, ncase, design_idx, head, zeta, B_drag, Bmat, K, Xi, 0.0,
-                                 nullptr, nullptr, stream);
+                                 nullptr, nullptr, nullptr, stream);
 }
 
 int rh_array_response_stats(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf, int ncase,
                             const int* design_idx, const int* head, const double* zeta, const double* B_drag,
                             const double* Bmat, const double* K, rh_c128* Xi, double dw, double* psd, double* std_,
-                            rh_stream stream) {
+                            const int* order, rh_stream stream) {
   if (!ctx || !designs || !design_idx || !head || !zeta || !B_drag || !Bmat || !Xi)
     return fail(RH_EINVAL, "rh_array_response: null argument");
   if ((psd || std_) && !(dw > 0)) return fail(RH_EINVAL, "rh_array_response_stats: dw=%g", dw);
@@ -735,7 +735,8 @@ int rh_array_response_stats(rh_ctx* ctx, const rh_design* designs, int ndesign, 
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
-  rh::ArrayArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, B_drag, Bmat, K, Xi, nn, nmmax, dw, psd, std_};
+  rh::ArrayArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, B_drag, Bmat, K, Xi, nn, nmmax, dw, psd, std_,
+                  order};
   const dim3 ge(ncase * nf), g(ncase);   // excitation per (case, FOWT), then the solve (+ statistics) per case
   const bool multi = nw > rh::kArrRespThreads;
   const dim3 gr(rh::kArrRespThreads);

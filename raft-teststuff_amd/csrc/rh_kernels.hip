@@ -1221,6 +1221,7 @@ struct ArrayArgs {
   double dw = 0;               // motion statistics (k_array_resp): frequency step,
   double* psd = nullptr;       // [ncase * NF][6][nw] or NULL,
   double* stdv = nullptr;      // [ncase * NF][6] or NULL
+  const int* order = nullptr;  // k_array_exc: entries in launch order (design, then heading), or NULL
 };
 constexpr int kArrRespThreads = 256;   // k_array_resp: one case per workgroup, bins in chunks of 256
 constexpr int kArrExcThreads = 256;
@@ -1228,7 +1229,9 @@ __host__ __device__ inline size_t array_exc_smem(int nn_max, int nm_max) {
   return sizeof(double) * (size_t)(5 * nn_max + 18 * nm_max) + sizeof(int) * (size_t)(nm_max + 1);
 }
 
-// one (case, FOWT) entry per workgroup: blockIdx.x = ic * NF + f, every bin of the grid
+// one (case, FOWT) entry per workgroup, every bin of the grid.  With an order, an XCD's
+// workgroups take a contiguous slice of it (xcd_remap): the entries of few (design, heading)
+// tables, which then stay in that XCD's L2 instead of every XCD streaming every table.
 template <int NF>
 __global__ __launch_bounds__(kArrExcThreads) void k_array_exc(ArrayArgs a) {
   extern __shared__ __attribute__((aligned(16))) double dyn[];
@@ -1237,7 +1240,7 @@ __global__ __launch_bounds__(kArrExcThreads) void k_array_exc(ArrayArgs a) {
   double* mbf = alf + (size_t)nnA * 5;                        // [18][nmA] member factors cq, c1, c2
   int* ms = reinterpret_cast<int*>(mbf + (size_t)18 * nmA);   // [nmA + 1] member node ranges
   const int tid = (int)threadIdx.x;
-  const size_t e = blockIdx.x;
+  const size_t e = a.order ? (size_t)a.order[xcd_remap((int)blockIdx.x, (int)gridDim.x)] : blockIdx.x;
   const int ic = (int)(e / NF), f = (int)(e % NF);
   const rh_design& d = a.designs[a.design_idx[e]].d;
   const int nn = d.nn, nm = d.nm, nw = d.nw, head = a.head[e];

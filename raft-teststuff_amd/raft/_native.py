@@ -102,7 +102,7 @@ def lib():
                 "rh_array_response": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.c_int, ctypes.c_int, _p, _p,
                                       _p, _p, _p, _p, _p, _p],
                 "rh_array_response_stats": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                            _p, _p, _p, _p, _p, _p, _p, ctypes.c_double, _p, _p, _p],
+                                            _p, _p, _p, _p, _p, _p, _p, ctypes.c_double, _p, _p, _p, _p],
                 "rh_wave_excitation": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.c_int, _p, _p, _p, _p, _p,
                                        _p],
                 "rh_channel_stats": [_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, _p,

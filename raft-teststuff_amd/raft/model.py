@@ -596,7 +596,7 @@ class Model:
         N.check(N.lib().rh_array_response_stats(ctx, arr, nf, nf, n, N.ptr(prep["design"]), N.ptr(prep["head"]),
                                                 N.ptr(res["zeta"]), N.ptr(res["B_drag"]), N.ptr(res["Bmat"]),
                                                 N.ptr(K), N.ptr(X), float(self.fowtList[0].dw), N.ptr(psd),
-                                                N.ptr(std), s), "rh_array_response_stats")
+                                                N.ptr(std), N.ptr(prep["order"]), s), "rh_array_response_stats")
         out = {"Xi": X, "iters": res["iters"].view(n, nf), "status": res["status"].view(n, nf),
                "psd": psd.view(n, nf, 6, nw), "std": std.view(n, nf, 6), "zeta": res["zeta"].view(n, nf, nw)[:, 0]}
         out["_keep"] = (res, arr, K)
