@@ -1384,12 +1384,10 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(RH_K
     kay_tile(q, wk, T1, T2, live, tid - grp * kKayThreads, reinterpret_cast<double(*)[256]>(sm + grp * kAcc),
              psg + (kKayS > 1 ? grp * kKayM * (kKayS - 1) * 16 * 64 : 0));
   } else {
-    // coefficient blocks frequency-block-major, an XCD's workgroups on a contiguous run of them
-    // (the XCD of block b is b % 8, a rotation of (b - nkb) % 8): the 18 global columns of a
-    // frequency block, which read every node's tables of that block, share one L2
-    const int nly = 18 + q.nq + q.nmq;
-    const int id = xcd_remap((int)blockIdx.x - nkb, (int)gridDim.x - nkb);
-    lcoef_block(q, wk, M66, id / nly, id % nly, reinterpret_cast<double(*)[12][64]>(sm));
+    // (k_qtf_lcoef's block order; frequency-block-major runs per XCD cut the launch's HBM reads
+    // from 52 to 31 MB but cost 3.5 us per QTF)
+    const int bl = (int)blockIdx.x - nkb;
+    lcoef_block(q, wk, M66, bl % nbx, bl / nbx, reinterpret_cast<double(*)[12][64]>(sm));
   }
 }
 
