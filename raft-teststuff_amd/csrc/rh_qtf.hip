@@ -166,11 +166,13 @@ __device__ __forceinline__ void qtf_resample(const rh_qtf_design& q, int nw, con
 #pragma unroll
     for (int d = 0; d < 6; ++d) X[d] = ld(Xi0 + (size_t)d * nw + nw - 1);
   } else {
-    int lo = 0, hi = nw - 1;              // invariant: w[lo] <= x < w[hi]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (w[mid] <= x) lo = mid; else hi = mid;
-    }
+    // lo with w[lo] <= x < w[lo + 1]: guessed from the first step (RAFT's grids are uniform,
+    // raft/raft_model.py:66-67) and moved until the invariant holds, so any sorted grid gives
+    // the interval a bisection would (two dependent loads instead of ten on a uniform grid)
+    const double g = (x - w[0]) / (w[1] - w[0]);      // clamped before the conversion (NaN -> 0)
+    int lo = g >= 0.0 && g < nw - 2 ? (int)g : g >= nw - 2 ? nw - 2 : 0;
+    while (lo > 0 && w[lo] > x) --lo;
+    while (lo < nw - 2 && w[lo + 1] <= x) ++lo;
     const double dx = w[lo + 1] - w[lo];
 #pragma unroll
     for (int d = 0; d < 6; ++d) {
