@@ -8,7 +8,7 @@ mkdir -p $R/raft-teststuff_amd/variants
 pids=()
 while [ $# -gt 1 ]; do
   name=$1; flags=$2; shift 2
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -Wno-unused-result -mllvm -amdgpu-disable-clustered-low-occupancy-reschedule -DRH_VARIANTS $flags \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -Wno-unused-result -DRH_VARIANTS $flags \
     -o $R/raft-teststuff_amd/variants/lib_$name.so $R/raft-teststuff_amd/csrc/rh_abi.hip &
   pids+=($!)
 done
