@@ -62,6 +62,39 @@ def pmc_traffic(workload, *kernels):
     return total
 
 
+# FP64 FLOPs per wave-instruction counter (64 lanes): an FMA is 2 FLOPs per lane, MUL / ADD /
+# transcendental 1; one SQ_INSTS_VALU_MFMA_MOPS_F64 unit is 512 FLOPs (the rocprof FLOP metric).
+HW_FLOP_WEIGHTS = {"SQ_INSTS_VALU_FMA_F64": 128.0, "SQ_INSTS_VALU_MUL_F64": 64.0, "SQ_INSTS_VALU_ADD_F64": 64.0,
+                   "SQ_INSTS_VALU_TRANS_F64": 64.0, "SQ_INSTS_VALU_MFMA_MOPS_F64": 512.0}
+
+
+def pmc_hw_flops(workload, *kernels):
+    """FP64 FLOPs the hardware executed per call (every lane of every issued FP64 VALU and MFMA
+    wave-instruction, HW_FLOP_WEIGHTS), summed over `kernels` from the `workload` section of
+    PMC_SUMMARY; None if a kernel or counter is missing.  Beside the formula credit of SURVEY
+    §8(d): work the kernel really does, padding and recomputation included."""
+    d = pmc_section(workload)
+    if d is None:
+        return None
+    total = 0.0
+    for kernel in kernels:
+        hit = [v.get("counters", {}) for name, v in d.items() if kernel_name_is(name, kernel)]
+        if len(hit) != 1 or not all(c in hit[0] for c in HW_FLOP_WEIGHTS):
+            return None
+        total += sum(w * hit[0][c] for c, w in HW_FLOP_WEIGHTS.items())
+    return total
+
+
+def hw_util(workload, kernels, kernel_ms):
+    """{"hw_flops": per call, "hw_achieved": TFLOP/s over the measured launch time, "hw_frac"} or
+    Nones when PMC_SUMMARY lacks the FP64 instruction counters."""
+    f = pmc_hw_flops(workload, *kernels)
+    if f is None or not kernel_ms:
+        return {"hw_flops": None, "hw_achieved": None, "hw_frac": None}
+    a = f / (kernel_ms * 1e-3)
+    return {"hw_flops": f, "hw_achieved": a / 1e12, "hw_frac": a / PEAK_FP64}
+
+
 def kernel_name_is(name, kernel):
     """Whether the demangled rocprof kernel `name` ("rh::k_qtf_kay(rh_qtf_design, ...)" or
     "void rh::k_solve_lds<2, 512, false, 1>(rh::CaseArgs)") is `kernel` exactly (a namespace-
@@ -98,11 +131,10 @@ def pmc_l2(kernel, kernel_ms):
     return None
 
 
-def solve_kernels(nw, a0=False):
-    """Every kernel one rh_solve_cases call launches for this grid: with the opt-in iteration-0
-    GEMM (rh_set_a0, rh_a0.hip; off by default) k_a0_sums runs before the fast-path solve."""
-    name = solve_kernel_name(nw)
-    return ("rh::k_a0_sums", name) if a0 and "k_solve_lds" in name else (name,)
+def solve_kernels(nw):
+    """Every kernel one rh_solve_cases call launches for this grid (one: the iteration-0 GEMM
+    k_a0_sums of round 4 is a variant-library kernel now)."""
+    return (solve_kernel_name(nw),)
 
 
 def solve_kernel_name(nw):
@@ -380,6 +412,7 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
            "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                         "frac": achieved / PEAK_FP64,
                         "traffic": pmc_traffic("qtf", "k_qtf_tables", "k_qtf_lk", "k_qtf_gemm"),
+                        **hw_util("qtf", ("k_qtf_tables", "k_qtf_lk", "k_qtf_gemm"), ms),
                         "kernel": "rh_qtf_slender%s: k_qtf_tables, k_qtf_lk, k_qtf_gemm (every launch of a "
                                   "QTF on this rank)" % ("_rows" if world > 1 else ""),
                         "kernel_ms": ms, "flops_per_pair": fpp, "pairs_this_rank": mine,
@@ -462,6 +495,7 @@ def bench_c4(device, steps, world, rank, dist, ncase=512):
                        "parallelism": f"case-sharded x{world}"},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP64, "traffic": pmc_traffic("c4", *solve_kernels(dd.nw)),
+                         **hw_util("c4", solve_kernels(dd.nw), kern_ms),
                          "kernel": solve_kernel_name(dd.nw), "kernels_timed": list(solve_kernels(dd.nw)),
                          "chain_traffic": pmc_traffic("c4", *solve_kernels(dd.nw), "rh::k_array_exc<2>",
                                                       f"rh::k_array_resp<2, {str(dd.nw > 256).lower()}>"),
@@ -807,6 +841,7 @@ def main():
                    "parallelism": f"case-sharded x{world}"},
         "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP64, "traffic": pmc_traffic("solve", *solve_kernels(dd.nw)),
+                     **hw_util("solve", solve_kernels(dd.nw), kern_ms),
                      "l2": pmc_l2(solve_kernel_name(dd.nw), kern_ms),
                      "kernel": solve_kernel_name(dd.nw), "kernels_timed": list(solve_kernels(dd.nw)),
                      "kernel_ms": kern_ms,

@@ -169,13 +169,16 @@ int rh_version(void);
  * kernel, the lane-pair kernel and the two-pass launch, all measured slower) */
 int rh_set_solver(rh_ctx* ctx, int which);
 
-/* Iteration-0 sums as a batch GEMM on this context (not part of the reference API; default 0):
- * 1 = when the fast path solves cases that start from XiStart (no Xi_init, first_iter 0), phase
- * A of their first iteration is formed for the whole batch by one MFMA launch (k_a0_sums) before
- * the solve, in each case's Xi_last block; 0 = every case forms it in its own workgroup.  The
- * two agree to rounding (the bin sums are grouped differently), with the same iteration counts
- * on the parity cases.  Opt-in: measured slower on C2 and C4. */
+/* Iteration-0 sums as a batch GEMM on this context (not part of the reference API; default 0).
+ * The shipped library accepts only 0 (every case forms them in its own workgroup) and refuses 1
+ * with RH_EINVAL: k_a0_sums, which forms phase A of the first iteration of every case that starts
+ * from XiStart as one MFMA launch, was measured slower on C2 and C4 and is built
+ * only into variant libraries (tools/build_variants.sh, -DRH_VARIANTS), where 1 enables it. */
 int rh_set_a0(rh_ctx* ctx, int on);
+
+/* Largest grid (bins) rh_solve_cases can solve with rh_solve_out.Xi = NULL (the linearisation
+ * only); larger grids keep their iterate in the Xi output and need it (RH_EINVAL otherwise). */
+int rh_solve_noxi_max_bins(void);
 
 /* Maximum cases per group of rh_cases.group_start: 1 in the shipped library (no grouped
  * kernel; group_start is then ignored). */
@@ -191,9 +194,10 @@ int rh_set_qtf_waves(rh_ctx* ctx, int waves);
 
 /* QTF pair-sum path of this context: 0 (default) = FP64 MFMA GEMMs on 16 x 16 pair tiles when
  * the grid is sorted (rh_qtf_design.order == 1), 1 = the per-pair kernel k_qtf_pairs (parity
- * cross-checks), 2 = the GEMMs with 32 x 32 tiles for a whole QTF (measured slower; the same
- * bits as 0), 3 = as 0 with the GEMM coefficients (k_qtf_lcoef) and the Kim & Yue sums
- * (k_qtf_kay) as two launches instead of one (the same bits as 0). */
+ * cross-checks).  Variant libraries (tools/build_variants.sh) also take 2 = the GEMMs with
+ * 32 x 32 tiles for a whole QTF and 3 = the GEMM coefficients (k_qtf_lcoef) and the Kim & Yue
+ * sums (k_qtf_kay) as two launches (both measured slower, the same bits as 0); the shipped
+ * library refuses them with RH_EINVAL. */
 int rh_set_qtf_path(rh_ctx* ctx, int path);
 
 /* Unit-amplitude wave kinematics and strip-theory inertial excitation per heading.

@@ -11,17 +11,19 @@
 
 #include "rh_device.h"
 
-#include "rh_kernels.hip"   // single translation unit: kernels + their host launchers
+#include "rh_kernels.hip"   // kernels + their host launchers (this translation unit: default scheduler)
 #include "rh_qtf.hip"
 #include "rh_qtf_mfma.hip"
-#include "rh_a0.hip"
-#include "rh_solve.hip"
+#include "rh_solve.hip"        // k_solve_lds: only the two-pass <2, 512, false, 2> is instantiated here
+#include "rh_solve_launch.h"   // ... the single-pass ones live in rh_solve_fast.hip (max-ilp scheduler)
 #ifdef RH_VARIANTS
 // Opt-in solve kernels that were measured slower than k_solve_lds on C2: the
 // lock-step grouped kernel, the lane-pair kernel and the two-pass launch.  They are not part
 // of the shipped library; tools/build_variants.sh builds them for on-box A/B timing.
 #include "../../tools/ubench/variants_src/rh_solve_grp.hip"
 #include "../../tools/ubench/variants_src/rh_solve_pair.hip"
+#include "../../tools/ubench/variants_src/rh_a0.hip"            // k_a0_sums (rh_set_a0)
+#include "../../tools/ubench/variants_src/rh_qtf_variants.hip"  // k_qtf_gemm32, k_qtf_lcoef + k_qtf_kay (rh_set_qtf_path 2, 3)
 #endif
 #include "rh_prep.h"       // host-only: native per-design preparation (rh_prep_designs)
 
@@ -47,9 +49,9 @@ struct rh_ctx {
   int cur = 0;                          // slot of the last staging
   // tuning / cross-check knobs (per context: the ABI has no mutable process globals)
   bool force_general = false;   // rh_set_solver(ctx, 1): always use k_solve_cases (parity cross-checks)
-  bool a0 = false;              // rh_set_a0: iteration-0 phase A of the fast path as a batch GEMM (rh_a0.hip;
-                                // opt-in: measured slower than the per-case phase A)
 #ifdef RH_VARIANTS
+  bool a0 = false;              // rh_set_a0: iteration-0 phase A of the fast path as a batch GEMM (rh_a0.hip;
+                                // measured slower than the per-case phase A)
   bool no_group = false;        // rh_set_solver(ctx, 2): ignore group_start (one case per workgroup)
 #ifndef RH_PAIR_ON
 #define RH_PAIR_ON 0
@@ -64,9 +66,11 @@ struct rh_ctx {
   int ncu = 0;                  // compute units of the device (rh_ctx_create)
   int qtf_waves = 0;            // rh_set_qtf_waves: waves per 64 QTF pairs in k_qtf_pairs (0 = auto)
   bool qtf_direct = false;      // rh_set_qtf_path(ctx, 1): the per-pair kernel even on a sorted grid
+#ifdef RH_VARIANTS
   bool qtf_sep = false;         // rh_set_qtf_path(ctx, 3): k_qtf_lcoef and k_qtf_kay as two launches
-  bool qtf_t32 = false;         // rh_set_qtf_path(ctx, 2): 32 x 32 GEMM tiles for a whole QTF (opt-in:
-                                // 68.7 vs 57.0 us per C3 QTF)
+  bool qtf_t32 = false;         // rh_set_qtf_path(ctx, 2): 32 x 32 GEMM tiles for a whole QTF
+                                // (68.7 vs 57.0 us per C3 QTF)
+#endif
   // per-stream scratch of rh_wave_tables (per-node forces, k_wave_tables_nodes ->
   // k_wave_force_sum): one buffer per stream, so stream order alone protects its reuse
   struct Scratch {
@@ -199,23 +203,7 @@ const char* rh_last_error(void) { return g_err.c_str(); }
 
 int rh_version(void) { return 3; }
 
-#ifdef RH_PROF
-extern "C" int rh_prof_read(unsigned long long* out, int reset) {
-  RH_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(rh::rh_prof), sizeof(unsigned long long) * 8));
-  if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    RH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(rh::rh_prof), z, sizeof z));
-  }
-  return RH_OK;
-}
-#endif
-
-#ifdef RH_WGTIME
-extern "C" int rh_wgt_read(unsigned long long* out, int n) {
-  RH_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(rh::rh_wgt), sizeof(unsigned long long) * 2 * (n < 8192 ? n : 8192)));
-  return RH_OK;
-}
-#endif
+// (rh_prof_read / rh_wgt_read of instrumented builds live in rh_solve_fast.hip, beside the counters)
 
 int rh_set_solver(rh_ctx* ctx, int which) {
   if (!ctx) return fail(RH_EINVAL, "rh_set_solver: null context");
@@ -238,10 +226,17 @@ int rh_set_solver(rh_ctx* ctx, int which) {
 
 int rh_group_cases(void) { return kGroupCases; }
 
+int rh_solve_noxi_max_bins(void) { return 2 * rh::kLT; }
+
 int rh_set_a0(rh_ctx* ctx, int on) {
   if (!ctx) return fail(RH_EINVAL, "rh_set_a0: null context");
   if (on != 0 && on != 1) return fail(RH_EINVAL, "rh_set_a0: on=%d (0 or 1)", on);
+#ifdef RH_VARIANTS
   ctx->a0 = on != 0;
+#else
+  if (on) return fail(RH_EINVAL, "rh_set_a0: k_a0_sums is not in the shipped library (measured slower, DESIGN.md §5; "
+                                 "tools/build_variants.sh builds it)");
+#endif
   return RH_OK;
 }
 
@@ -259,9 +254,15 @@ int rh_set_qtf_path(rh_ctx* ctx, int path) {
     return fail(RH_EINVAL, "rh_set_qtf_path: path=%d (0 = MFMA GEMMs when order == 1, 1 = per-pair kernel, "
                            "2 = MFMA GEMMs with 32 x 32 tiles for a whole QTF, 3 = the GEMM coefficients and "
                            "Kim & Yue as two launches)", path);
-  ctx->qtf_direct = path == 1;
+#ifdef RH_VARIANTS
   ctx->qtf_t32 = path == 2;
   ctx->qtf_sep = path == 3;
+#else
+  if (path >= 2)
+    return fail(RH_EINVAL, "rh_set_qtf_path: path %d is not in the shipped library (measured slower, DESIGN.md §5; "
+                           "tools/build_variants.sh builds it)", path);
+#endif
+  ctx->qtf_direct = path == 1;
   return RH_OK;
 }
 
@@ -392,8 +393,8 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
     return fail(RH_EINVAL, "rh_solve_cases: Xi_last, iters and status outputs are required");
   if (!out->Xi && (out->psd || out->std || out->rao))
     return fail(RH_EINVAL, "rh_solve_cases: psd, std and rao need the Xi output");
-  if (!out->Xi && designs[0].nw > 2 * rh::kLT)
-    return fail(RH_EINVAL, "rh_solve_cases: grids beyond %d bins need the Xi output", 2 * rh::kLT);
+  if (!out->Xi && designs[0].nw > rh_solve_noxi_max_bins())
+    return fail(RH_EINVAL, "rh_solve_cases: grids beyond %d bins need the Xi output", rh_solve_noxi_max_bins());
   if (cases->nIter < 0) return fail(RH_EINVAL, "rh_solve_cases: nIter=%d", cases->nIter);
   if (cases->first_iter < 0 || cases->first_iter > cases->nIter)
     return fail(RH_EINVAL, "rh_solve_cases: first_iter=%d outside [0, nIter=%d]", cases->first_iter, cases->nIter);
@@ -448,6 +449,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   // Cases that start from XiStart: phase A of iteration 0 for the whole batch as one GEMM
   // launch (rh_a0.hip), its sums in each case's Xi_last block (k_solve_lds reads them first).
   auto prep_a0 = [&]() -> int {
+#ifdef RH_VARIANTS
     if (!ctx->a0 || cases->first_iter != 0 || cases->Xi_init || !rh::a0_fits(nw, nnmax) ||
         rh::kA0StaticLds + rh::a0_smem(nnmax, nmmax) > kMaxLds)
       return RH_OK;
@@ -455,6 +457,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
     hipLaunchKernelGGL(rh::k_a0_sums, g, dim3(rh::kA0Threads), rh::a0_smem(nnmax, nmmax), s, a);
     RH_HIP(hipGetLastError());
     a.a0 = 1;
+#endif
     return RH_OK;
   };
   // Fast path (rh_solve.hip): XiLast in LDS, 512 threads per case (256 for nw <= 256), nw <= 1024.
@@ -473,8 +476,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
       if (lsm128 <= kMaxLds) {
         if (int r = prep_a0()) return r;
         dim3 grid(cases->ncase), block(rh::kLT / 4);
-        if (nb128 == 1) hipLaunchKernelGGL((rh::k_solve_lds<1, rh::kLT / 4, true>), grid, block, lsm128, s, a);
-        else hipLaunchKernelGGL((rh::k_solve_lds<2, rh::kLT / 4, true>), grid, block, lsm128, s, a);
+        RH_HIP(rh::launch_solve_fast(nb128 == 1 ? rh::kSolve1x128 : rh::kSolve2x128, grid, block, lsm128, s, a));
         return designs_used(ctx, s);
       }
     }
@@ -484,7 +486,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
     if (lsm <= 160 * 1024) {
       if (int r = prep_a0()) return r;
       dim3 grid(cases->ncase), block(lt);
-      auto kern = lt < rh::kLT ? rh::k_solve_lds<1, rh::kLT / 2> : nb == 1 ? rh::k_solve_lds<1> : rh::k_solve_lds<2>;
+      const int kern = lt < rh::kLT ? rh::kSolve1x256 : nb == 1 ? rh::kSolve1x512 : rh::kSolve2x512;
 #ifdef RH_VARIANTS
       // Two passes when the batch needs more than one round of workgroups (measured slower on
       // C2: 0.895 vs 0.828 ms).  Pass 1 runs every case up to its last possible
@@ -492,16 +494,15 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
       const int nloop = cases->nIter + 1;
       if (ctx->two_pass && nloop - 1 > cases->first_iter) {
         int per_cu = 0;
-        RH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, lt, lsm));
+        RH_HIP(rh::occupancy_solve_fast(kern, &per_cu, lt, lsm));
         if (cases->ncase > per_cu * ctx->ncu) {
           a.stop_iter = nloop - 1;
-          hipLaunchKernelGGL(kern, grid, block, lsm, s, a);
-          RH_HIP(hipGetLastError());
+          RH_HIP(rh::launch_solve_fast(kern, grid, block, lsm, s, a));
           a.resume = 1;
         }
       }
 #endif
-      hipLaunchKernelGGL(kern, grid, block, lsm, s, a);
+      RH_HIP(rh::launch_solve_fast(kern, grid, block, lsm, s, a));
       return designs_used(ctx, s);
     }
   }
@@ -789,24 +790,33 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
     // (rh_qtf_mfma.hip)
     const int nt = n2p / 16, ntile = nt * (nt + 1) / 2;
     const int blocks = (ntile - rank + nrank - 1) / nrank;
-    if (blocks > 0 && !ctx->qtf_sep) {
+#ifdef RH_VARIANTS
+    const bool sep = ctx->qtf_sep, t32 = ctx->qtf_t32;
+#else
+    constexpr bool sep = false, t32 = false;
+#endif
+    if (blocks > 0 && !sep) {
       // the Kim & Yue tiles (two per workgroup) and the GEMM coefficient blocks in one launch
       const int nkb = (blocks + 1) / 2, nly = 18 + q->nq + q->nmq;
       hipLaunchKernelGGL(rh::k_qtf_lk, dim3(nkb + nb * nly), dim3(rh::kLkThreads), 0, s, *q, wk, M66, rank, nrank,
                          blocks, nkb, nb);
       RH_HIP(hipGetLastError());
     } else {
+#ifdef RH_VARIANTS
       hipLaunchKernelGGL(rh::k_qtf_lcoef, dim3(nb, 18 + q->nq + q->nmq), dim3(512), 0, s, *q, wk, M66);
       RH_HIP(hipGetLastError());
       if (blocks > 0) {
         hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, s, *q, wk, rank, nrank);
         RH_HIP(hipGetLastError());
       }
+#endif
     }
     if (blocks > 0) {
-      if (nrank == 1 && mirror && ctx->qtf_t32) {   // opt-in for a whole QTF: 32 x 32 pair tiles
+      if (nrank == 1 && mirror && t32) {   // variant builds, a whole QTF: 32 x 32 pair tiles
+#ifdef RH_VARIANTS
         const int nt32 = (nt + 1) / 2;
         hipLaunchKernelGGL(rh::k_qtf_gemm32, dim3(nt32 * (nt32 + 1)), dim3(384), 0, s, *q, wk, qtf);
+#endif
       } else {
         hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(2 * blocks), dim3(384), 0, s, *q, wk, qtf, rank, nrank, mirror);
       }

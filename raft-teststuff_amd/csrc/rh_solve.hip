@@ -12,14 +12,17 @@
 //     3-slot register ring: node n+2 is in flight while node n is reduced.
 //   * Per-node bin sums: a 6-step DPP wave reduction (VALU only, no LDS or SGPR traffic),
 //     one partial per wave, summed in wave order.  Fixed order, so results are deterministic.
-#include "rh_device.h"
+#include "rh_common.h"
+#ifdef RH_VARIANTS
+#include "../../tools/ubench/variants_src/rh_a0_common.h"   // k_a0_sums sums (rh_set_a0)
+#endif
 
 namespace rh {
 
 #ifdef RH_PROF
 // Phase cycle counters (s_memtime of wave 0 of every workgroup), summed over workgroups:
 // [0] prologue [1] A [2] B [3] C excitation [4] C solve [5] flags [6] epilogue [7] iterations
-__device__ unsigned long long rh_prof[8];
+static __device__ unsigned long long rh_prof[8];   // static: one per translation unit (rh_prof_read reads rh_solve_fast.hip's)
 #define PROF_T(v) const unsigned long long v = clock64()
 #define PROF_ADD(i, x) if (tid == 0) atomicAdd(&rh_prof[i], (unsigned long long)(x))
 #else
@@ -30,7 +33,7 @@ __device__ unsigned long long rh_prof[8];
 #ifdef RH_WGTIME
 // Per-workgroup wall-clock (s_memrealtime, 100 MHz) of the fixed point: [2 slot] = start,
 // [2 slot + 1] = end of the loop, by dispatch slot (launch-tail analysis, tools/ubench/wg_times.py)
-__device__ unsigned long long rh_wgt[2 * 8192];
+static __device__ unsigned long long rh_wgt[2 * 8192];
 #endif
 
 constexpr int kLT = 512;          // threads per case workgroup
@@ -282,8 +285,13 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   // chunk sums (in chunk order) take the place of wave 0's partials and the other waves' are 0,
   // so phase B's wave-order sum returns them unchanged; phase A of that iteration is skipped.
   // (Read before the prologue: with GX the same Xi_last block then receives XiLast.)
+#ifdef RH_VARIANTS
   bool skip_a = a.a0 != 0 && it0 == 0;   // uniform
+#else
+  constexpr bool skip_a = false;         // k_a0_sums is a variant kernel (tools/ubench/variants_src/rh_a0.hip)
+#endif
   if (skip_a) {
+#ifdef RH_VARIANTS
     const double* a0s = a0_block(a, ic, nw);
     const int nch = a0_chunks(nw);
     for (int e = tid; e < nn * 3; e += LT) {
@@ -294,6 +302,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       for (int w = 1; w < LW; ++w) red[e * LW + w] = 0.0;
     }
     __syncthreads();
+#endif
   }
 
   // Per-bin scalars live in LDS, not in registers: nothing per-thread stays live across the
@@ -305,15 +314,13 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     const int spec = a.c.spectrum[ic];
     const double Hs = a.c.Hs[ic], Tp = a.c.Tp[ic], gam = a.c.gamma[ic];
     const rh_c128* XI0 = resume ? a.o.Xi_last + c6 : a.c.Xi_init ? a.c.Xi_init + c6 : nullptr;
+    // (the loads first, then the spectrum from LDS: a loop that both loads and evaluates the
+    // spectrum's transcendentals keeps scratch stores beside its loads under the max-ilp scheduler)
 #pragma unroll
     for (int j = 0; j < NBT; ++j) {
       const int b = tid + LT * j;
       const bool okb = b < nw;
-      const double w = d.w[okb ? b : nw - 1];
-      const double zz = sea_amplitude(spec, Hs, Tp, gam, w, d.dw);
-      lw[b] = w;
-      lz[b] = okb ? zz : 0.0;
-      if (okb && a.o.zeta) a.o.zeta[(size_t)ic * nw + b] = zz;
+      lw[b] = d.w[okb ? b : nw - 1];
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
         const cd x0 = okb ? (XI0 ? ld(XI0 + c * nw + b) : mk(a.c.XiStart, 0.0)) : mk(0.0, 0.0);
@@ -323,6 +330,14 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
           xl[c * NWP + b] = x0;
         }
       }
+    }
+#pragma unroll
+    for (int j = 0; j < NBT; ++j) {   // the thread reads back only its own bins: no barrier
+      const int b = tid + LT * j;
+      const bool okb = b < nw;
+      const double zz = sea_amplitude(spec, Hs, Tp, gam, lw[b], d.dw);
+      lz[b] = okb ? zz : 0.0;
+      if (okb && a.o.zeta) a.o.zeta[(size_t)ic * nw + b] = zz;
     }
   }
   rh_c128* Xo = a.o.Xi ? a.o.Xi + c6 : nullptr;   // NULL: the caller wants no response (C4 fixed point)
@@ -504,7 +519,9 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       }
 #endif
     }
+#ifdef RH_VARIANTS
     skip_a = false;
+#endif
     __syncthreads();
     PROF_T(ta1);
     PROF_ADD(1, ta1 - ta0);
@@ -858,6 +875,10 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       }
     }
   }
+  // A case that stopped on a NaN or a singular Z has no response (the reference raises there,
+  // raft/raft_model.py:957): its Xi, PSD, RAO and std are NaN, as in k_solve_cases.  (The
+  // entries of its last iterate were stored only where they passed their test.)
+  const bool failed = status == RH_CASE_NAN || status == RH_CASE_SINGULAR;   // uniform
   double ss[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int j = 0; j < NBT; ++j) {
@@ -866,12 +887,18 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     const double z = lz[b];
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
-      const cd x = ld(Xo + c * nw + b);
+      cd x;
+      if (failed) {
+        x = mk(NAN, NAN);
+        st(Xo + c * nw + b, x);
+      } else {
+        x = ld(Xo + c * nw + b);
+      }
       const cd xd = c >= 3 ? scl(x, kRad2Deg) : x;
       const double m2 = abs2(xd);
       ss[c] += m2;
       if (a.o.psd) a.o.psd[((size_t)ic * 6 + c) * nw + b] = 0.5 * m2 / d.dw;
-      if (a.o.rao) st(a.o.rao + ((size_t)ic * 6 + c) * nw + b, fabs(z) > 1e-6 ? cd{x.r / z, x.i / z} : mk(0, 0));
+      if (a.o.rao) st(a.o.rao + ((size_t)ic * 6 + c) * nw + b, failed ? x : fabs(z) > 1e-6 ? cd{x.r / z, x.i / z} : mk(0, 0));
     }
   }
   if (a.o.std) {

@@ -1,0 +1,60 @@
+// rh_solve_fast.hip -- the second translation unit of librafthip.so: the single-pass instantiations
+// of k_solve_lds (rh_solve.hip; the C2 fixed point <2, 512>, the C4 one <2, 128, SER>, and the small
+// grids), with the host-side launchers rh_abi.hip calls (rh_solve_launch.h).
+//
+// It exists for one compiler flag.  The machine scheduler's max-ilp strategy
+// (-mllvm -amdgpu-sched-strategy=max-ilp) orders the same instructions for latency: the C2 fixed
+// point runs 3.7 % faster in the bench's steady state, but the flag is per
+// translation unit, and under it the two-pass k_solve_lds<2, 512, false, 2> and the general
+// k_solve_cases<NB> keep spill reloads inside their node loops (tools/isa_check.py refuses them).
+// So those stay in rh_abi.hip with the default scheduler, and only what gains is built here
+// (__graft_entry__.py SOLVE_FAST_FLAGS).  Same instructions, another order: the same bits.
+#include "rh_solve.hip"
+#include "rh_solve_launch.h"
+
+namespace rh {
+
+hipError_t launch_solve_fast(int which, dim3 grid, dim3 block, size_t lsm, hipStream_t s, const CaseArgs& a) {
+  switch (which) {
+    case kSolve1x128: hipLaunchKernelGGL((k_solve_lds<1, kLT / 4, true>), grid, block, lsm, s, a); break;
+    case kSolve2x128: hipLaunchKernelGGL((k_solve_lds<2, kLT / 4, true>), grid, block, lsm, s, a); break;
+    case kSolve1x256: hipLaunchKernelGGL((k_solve_lds<1, kLT / 2>), grid, block, lsm, s, a); break;
+    case kSolve1x512: hipLaunchKernelGGL((k_solve_lds<1>), grid, block, lsm, s, a); break;
+    case kSolve2x512: hipLaunchKernelGGL((k_solve_lds<2>), grid, block, lsm, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t occupancy_solve_fast(int which, int* per_cu, int threads, size_t lsm) {
+  switch (which) {
+    case kSolve1x256: return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_solve_lds<1, kLT / 2>, threads, lsm);
+    case kSolve1x512: return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_solve_lds<1>, threads, lsm);
+    case kSolve2x512: return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_solve_lds<2>, threads, lsm);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace rh
+
+// Diagnostics of instrumented builds (tools/ubench/time_solve.py): they read this unit's counters,
+// which the fast kernels write.
+#ifdef RH_PROF
+extern "C" int rh_prof_read(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rh::rh_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -3;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rh::rh_prof), z, sizeof z) != hipSuccess) return -3;
+  }
+  return 0;
+}
+#endif
+
+#ifdef RH_WGTIME
+extern "C" int rh_wgt_read(unsigned long long* out, int n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rh::rh_wgt), sizeof(unsigned long long) * 2 * (n < 8192 ? n : 8192)) !=
+      hipSuccess)
+    return -3;
+  return 0;
+}
+#endif

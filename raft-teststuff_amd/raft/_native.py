@@ -132,6 +132,8 @@ def lib():
             L.rh_version.restype = ctypes.c_int
             L.rh_group_cases.argtypes = []
             L.rh_group_cases.restype = ctypes.c_int
+            L.rh_solve_noxi_max_bins.argtypes = []
+            L.rh_solve_noxi_max_bins.restype = ctypes.c_int
             L.rh_qtf_workspace_bytes.argtypes = [ctypes.POINTER(RhQtfDesign)]
             L.rh_qtf_workspace_bytes.restype = ctypes.c_longlong
             _lib = L

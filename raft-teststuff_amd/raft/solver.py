@@ -70,7 +70,7 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     out = BatchResult()
     c128 = dict(dtype=torch.complex128, device=dev)
     f64 = dict(dtype=torch.float64, device=dev)
-    if "noXi" not in want or nw > 1024:   # "noXi": the linearisation only (zeta / Bmat / B_drag);
+    if "noXi" not in want or nw > N.lib().rh_solve_noxi_max_bins():   # "noXi": the linearisation only (zeta / Bmat / B_drag);
         out["Xi"] = torch.empty([ncase, 6, nw], **c128)   # the two-pass grids store it regardless
     xl = torch.empty([ncase, 6, nw], **c128)
     out["iters"] = torch.empty([ncase], dtype=torch.int32, device=dev)

@@ -61,11 +61,35 @@ def test_pmc_lookup_sections_and_exact_names(tmp_path, monkeypatch):
     p = tmp_path / "pmc.json"
     p.write_text(json.dumps(sec))
     monkeypatch.setattr(bench, "PMC_SUMMARY", str(p))
-    assert bench.pmc_traffic("solve", *bench.solve_kernels(1000, a0=True)) == 33.0
+    assert bench.pmc_traffic("solve", "rh::k_a0_sums", *bench.solve_kernels(1000)) == 33.0
     assert bench.pmc_traffic("solve", *bench.solve_kernels(1000)) == 30.0
     assert bench.pmc_traffic("c4", "rh::k_a0_sums") == 100.0
     assert bench.pmc_traffic("qtf", "k_qtf_kay") == 10.0
-    assert bench.pmc_traffic("c4", *bench.solve_kernels(240, a0=True)) is None
+    assert bench.pmc_traffic("c4", *bench.solve_kernels(240)) is None
     p.write_text(json.dumps(sec["solve"]))
     assert bench.pmc_traffic("qtf", "rh::k_a0_sums") == 3.0
     assert bench.solve_kernels(2000) == ("rh::k_solve_lds<2, 512, false, 2>",)
+
+
+def test_pmc_hw_flops(tmp_path, monkeypatch):
+    """pmc_hw_flops weighs the FP64 instruction counters (FMA 128 FLOPs per wave-instruction,
+    MUL / ADD / transcendental 64, one MFMA_MOPS_F64 unit 512) and returns None when a counter
+    is missing (a summary without the FP64 pass); hw_util turns them into a rate and a fraction."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    full = {"SQ_INSTS_VALU_FMA_F64": 10.0, "SQ_INSTS_VALU_MUL_F64": 2.0, "SQ_INSTS_VALU_ADD_F64": 3.0,
+            "SQ_INSTS_VALU_TRANS_F64": 1.0, "SQ_INSTS_VALU_MFMA_MOPS_F64": 4.0}
+    sec = {"solve": {"void rh::k_solve_lds<2, 512, false, 1>(rh::CaseArgs)": {"counters": full}},
+           "qtf": {"rh::k_qtf_gemm(x)": {"counters": dict(full, SQ_INSTS_VALU_FMA_F64=0.0)},
+                   "rh::k_qtf_lk(x)": {"counters": {"SQ_INSTS_VALU_FMA_F64": 1.0}}}}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps(sec))
+    monkeypatch.setattr(bench, "PMC_SUMMARY", str(p))
+    f = 10 * 128 + (2 + 3 + 1) * 64 + 4 * 512
+    assert bench.pmc_hw_flops("solve", *bench.solve_kernels(1000)) == f
+    assert bench.pmc_hw_flops("qtf", "k_qtf_gemm") == f - 10 * 128
+    assert bench.pmc_hw_flops("qtf", "k_qtf_gemm", "k_qtf_lk") is None
+    u = bench.hw_util("solve", bench.solve_kernels(1000), 1.0)
+    assert u["hw_flops"] == f and abs(u["hw_frac"] - f / 1e-3 / bench.PEAK_FP64) < 1e-15
+    assert bench.hw_util("c4", bench.solve_kernels(240), 1.0)["hw_frac"] is None

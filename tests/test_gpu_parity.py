@@ -291,6 +291,59 @@ def test_fast_and_general_kernels_agree(tag, design, settings, ncase):
     np.testing.assert_array_equal(a["zeta"], b["zeta"])
 
 
+def _singular_copy(dd):
+    """A copy of a DeviceDesign whose M, B, C and node table are zero: no stiffness, no
+    inertia, no drag, so Z(w) = 0 in every bin and the LU meets an exactly zero pivot."""
+    import copy
+    z = copy.copy(dd)
+    z.__dict__ = {k: v for k, v in dd.__dict__.items() if k not in dd._layout and k != "_struct"}
+    z._packed = dd._packed.clone()
+    for name in ("M", "B", "C", "node"):
+        getattr(z, name).zero_()
+    return z
+
+
+@pytest.mark.parametrize("tag,design,settings,ncase", [("c2_nw1000", "VolturnUS-S_example", {"min_freq": 0.0002}, 12),
+                                                       ("c2_nw200", "VolturnUS-S_example", None, 9)])
+def test_failed_cases_fast_and_general_agree(tag, design, settings, ncase):
+    """A batch with a NaN sea state and a case on a singular design: both solve kernels stop
+    those cases with RH_CASE_NAN / RH_CASE_SINGULAR after the same iteration and report no
+    response for them (Xi, PSD, RAO and std all NaN; the reference raises there,
+    raft/raft_model.py:957), while the other cases of the batch are unaffected and agree."""
+    import torch
+    from raft import _native as N
+    from raft.solver import CaseSet, solve_batch
+    T = load_golden(tag)
+    m, f = make_model(design, T, settings)
+    cases = random_cases(ncase, 21)
+    cases[2]["wave_height"] = float("nan")
+    dd = f.device_design()
+    idx = np.zeros(ncase, dtype=np.int32)
+    idx[5] = 1
+    cs = CaseSet(idx, [c["wave_heading"] for c in cases], [c["wave_spectrum"] for c in cases],
+                 [c["wave_height"] for c in cases], [c["wave_period"] for c in cases], [0.0] * ncase)
+    want = ("psd", "std", "zeta", "rao")
+    out = []
+    for solver in (0, 1):
+        N.check(N.lib().rh_set_solver(N.context(0), solver), "rh_set_solver")
+        try:
+            out.append(solve_batch([dd, _singular_copy(dd)], cs, m.nIter, m.XiStart, 0.01, want=want).host())
+        finally:
+            N.check(N.lib().rh_set_solver(N.context(0), 0), "rh_set_solver")
+        torch.cuda.synchronize()
+    a, b = out
+    assert a["status"][2] == N.RH_CASE_NAN and a["status"][5] == N.RH_CASE_SINGULAR, a["status"]
+    np.testing.assert_array_equal(a["status"], b["status"])
+    np.testing.assert_array_equal(a["iters"], b["iters"])
+    for r in (a, b):
+        for k in ("Xi", "psd", "std", "rao"):
+            assert np.all(np.isnan(r[k][[2, 5]])), k
+            ok = np.delete(r[k], [2, 5], axis=0)
+            assert np.all(np.isfinite(ok)), k
+    for ic in set(range(ncase)) - {2, 5}:
+        assert rel(a["Xi"][ic], b["Xi"][ic]) < 1e-12, ic
+
+
 @pytest.mark.parametrize("tag,design,settings,ncase", [("c2_nw1000", "VolturnUS-S_example", {"min_freq": 0.0002}, 160),
                                                        ("c2_nw200", "VolturnUS-S_example", None, 53),
                                                        ("c1_OC3spar", "OC3spar", None, 17)])
@@ -301,6 +354,9 @@ def test_a0_gemm_agrees_with_per_case_phase_a(tag, design, settings, ncase):
     differs).  Random headings, so the 16-case tiles hold several (design, heading) keys; ncase
     not a multiple of 16."""
     from raft import _native as N
+    if N.lib().rh_set_a0(N.context(0), 1) != N.RH_OK:
+        pytest.skip("k_a0_sums is a variant kernel: run with RAFTHIP_LIB set to a tools/build_variants.sh library")
+    N.check(N.lib().rh_set_a0(N.context(0), 0), "rh_set_a0")
     T = load_golden(tag)
     m, f = make_model(design, T, settings)
     cases = random_cases(ncase, 7)

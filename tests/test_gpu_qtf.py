@@ -105,9 +105,10 @@ def test_mfma_path_matches_per_pair_kernel(T, beta_deg, grid):
     against the per-pair kernel k_qtf_pairs (rh_set_qtf_path(ctx, 1)): the same arithmetic
     reassociated, so they agree far inside the 1e-9 parity bar (1e-12 normwise, elementwise
     to 1e-12 of the largest entry), with the moving body and fixed, at 0 and 30 degrees (Q1).
-    The opt-in 32 x 32 GEMM tiles (rh_set_qtf_path(ctx, 2)) and the GEMM coefficients and Kim &
-    Yue sums as two launches (rh_set_qtf_path(ctx, 3), one merged launch by default) give the
-    default's bits."""
+    In a variant library (tools/build_variants.sh, RAFTHIP_LIB) the 32 x 32 GEMM tiles
+    (rh_set_qtf_path(ctx, 2)) and the GEMM coefficients and Kim & Yue sums as two launches
+    (rh_set_qtf_path(ctx, 3), one merged launch by default) give the default's bits; the shipped
+    library refuses those paths."""
     import torch
     from raft import _native as N
     from raft.hydro_math import wave_numbers
@@ -123,18 +124,23 @@ def test_mfma_path_matches_per_pair_kernel(T, beta_deg, grid):
     qd = QtfDevice(f, w2, k2, np.deg2rad(beta_deg), 0)
     assert qd.order == 1
     ctx = N.context(0)
+    variants = N.lib().rh_set_qtf_path(ctx, 2) == N.RH_OK
+    N.check(N.lib().rh_set_qtf_path(ctx, 0), "rh_set_qtf_path")
     for X0 in (T["out_Xi0"], np.zeros_like(T["out_Xi0"])):
         X = torch.tensor(X0, dtype=torch.complex128, device=dd.device)
         out = []
         try:
-            for path in (0, 1, 2, 3):
+            for path in ((0, 1, 2, 3) if variants else (0, 1)):
                 N.check(N.lib().rh_set_qtf_path(ctx, path), "rh_set_qtf_path")
                 out.append(qd.qtf(dd.w, X, M66).cpu().numpy())
         finally:
             N.check(N.lib().rh_set_qtf_path(ctx, 0), "rh_set_qtf_path")
-        a, b, c, d = out
-        np.testing.assert_array_equal(c, a)      # 32 x 32 tiles (opt-in): the same bits as 16 x 16
-        np.testing.assert_array_equal(d, a)      # two launches: the same arithmetic, the same bits
+        a, b = out[:2]
+        if variants:
+            np.testing.assert_array_equal(out[2], a)   # 32 x 32 tiles: the same bits as 16 x 16
+            np.testing.assert_array_equal(out[3], a)   # two launches: the same arithmetic, the same bits
+        else:
+            assert N.lib().rh_set_qtf_path(ctx, 3) == N.RH_EINVAL
         assert rel(a, b) < 1e-12, rel(a, b)
         np.testing.assert_allclose(a, b, rtol=0, atol=1e-12 * np.abs(b).max())
         i, j = np.tril_indices(len(w2), -1)
