@@ -142,7 +142,9 @@ typedef struct {
   int* status;            /* [ncase] RH_CASE_* (required)                      */
   double* zeta;           /* [ncase][nw] wave amplitudes sqrt(2 S dw)          */
   double* B_drag;         /* [ncase][36] final linearised drag damping         */
-  double* Bmat;           /* [ncase][nn][9] final per-node drag matrices       */
+  double* Bmat;           /* [ncase][nn_max][9] final per-node drag matrices; nn_max = the
+                             largest nn of the call's designs (a case with fewer nodes
+                             leaves the rest of its rows untouched)              */
   double* psd;            /* [ncase][6][nw] motion PSD (rotations in deg^2), raft/raft_fowt.py:1836-1874 */
   double* std;            /* [ncase][6] motion RMS                             */
   rh_c128* rao;           /* [ncase][6][nw] Xi / zeta (raft/helpers.py:665)   */
@@ -229,7 +231,8 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
 /* Response to additional sea states of a solved case with the linearisation frozen:
  * Xi_h = Z^-1 (zeta_h finer_h + zeta_h sum_n T_n Bmat_n uhat_h,n)  (raft/raft_model.py:1049-1065).
  * zeta: device [ncase][nw]; head: device [ncase] heading-table index; B_drag [ncase][36] and
- * Bmat [ncase][nn][9] as produced by rh_solve_cases; Xi out: [ncase][6][nw]. */
+ * Bmat [ncase][nn_max][9] as produced by rh_solve_cases (nn_max: the largest nn of the designs
+ * passed here); Xi out: [ncase][6][nw]. */
 int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int ncase,
                         const int* design_idx, const int* head, const double* zeta,
                         const double* B_drag, const double* Bmat, rh_c128* Xi, rh_stream stream);
@@ -308,8 +311,9 @@ int rh_system_solve_batch(rh_ctx* ctx, int ncase, int nf, int nw, const rh_c128*
  * matrices and the case's B_drag), then Xi = (blockdiag(Z_f) + K)^-1 F.  Replaces the
  * rh_wave_excitation + rh_system_solve_batch pair without the per-(case, bin) Z and F arrays.
  * Entries e = ic * nf + f (case-major, FOWT-minor) index design_idx, head, zeta [.][nw],
- * B_drag [.][36] and Bmat [.][nn][9] (as rh_solve_cases writes them; every design must share
- * nw and the submerged node count nn).  K: [6nf][6nf] array stiffness or NULL.
+ * B_drag [.][36] and Bmat [.][nn_max][9] (as rh_solve_cases writes them: nn_max is the largest
+ * node count of the designs, which must share nw; FOWTs of an array may differ in node count).
+ * K: [6nf][6nf] array stiffness or NULL.
  * Xi out: [ncase][6 nf][nw]. */
 int rh_array_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf, int ncase, const int* design_idx,
                       const int* head, const double* zeta, const double* B_drag, const double* Bmat, const double* K,

@@ -405,10 +405,6 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
     if (designs[i].nw != nw) return fail(RH_EINVAL, "rh_solve_cases: all designs must share nw");
     if (designs[i].nn > nnmax) nnmax = designs[i].nn;
   }
-  if (out->Bmat && ndesign > 1) {
-    for (int i = 0; i < ndesign; ++i)
-      if (designs[i].nn != nnmax) return fail(RH_EINVAL, "rh_solve_cases: Bmat output needs equal nn across designs");
-  }
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
@@ -416,6 +412,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   a.designs = staged_designs(ctx);
   a.c = *cases;
   a.o = *out;
+  a.bmat_nn = nnmax;
   int nmmax = 0;
   for (int i = 0; i < ndesign; ++i) nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
 #ifdef RH_VARIANTS
@@ -547,7 +544,7 @@ int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int 
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
-  rh::HeadArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, B_drag, Bmat, Xi, nullptr};
+  rh::HeadArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, B_drag, Bmat, Xi, nullptr, nnmax, ndesign};
   const size_t smem = sizeof(double) * (size_t)(nnmax * 9 + 36 + 108);
   dim3 grid((nw + kThreads - 1) / kThreads, ncase);
   hipLaunchKernelGGL(rh::k_heading_resp, grid, dim3(kThreads), smem, s, a);
@@ -569,7 +566,7 @@ int rh_wave_excitation(rh_ctx* ctx, const rh_design* designs, int ndesign, int n
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
-  rh::HeadArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, nullptr, Bmat, nullptr, F};
+  rh::HeadArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, nullptr, Bmat, nullptr, F, nnmax, ndesign};
   const size_t smem = sizeof(double) * (size_t)(nnmax * 9 + 36 + 108);
   dim3 grid((nw + kThreads - 1) / kThreads, ncase);
   hipLaunchKernelGGL(rh::k_heading_resp, grid, dim3(kThreads), smem, s, a);
@@ -722,12 +719,12 @@ int rh_array_response_stats(rh_ctx* ctx, const rh_design* designs, int ndesign, 
   if (nf < 1 || nf > 2) return fail(RH_EINVAL, "rh_array_response: nf=%d (supported: 1, 2)", nf);
   if (ncase <= 0) return ncase == 0 ? RH_OK : fail(RH_EINVAL, "rh_array_response: ncase=%d", ncase);
   if (ndesign < 1) return fail(RH_EINVAL, "rh_array_response: ndesign=%d", ndesign);
-  const int nw = designs[0].nw, nn = designs[0].nn;
-  int nmmax = 0;
+  const int nw = designs[0].nw;
+  int nn = 0, nmmax = 0;   // nn: the largest node count (the Bmat stride and the LDS layout)
   for (int i = 0; i < ndesign; ++i) {
     if (int r = check_design(designs[i], true)) return r;
-    if (designs[i].nw != nw || designs[i].nn != nn)
-      return fail(RH_EINVAL, "rh_array_response: all designs must share nw and the submerged node count");
+    if (designs[i].nw != nw) return fail(RH_EINVAL, "rh_array_response: all designs must share nw");
+    nn = designs[i].nn > nn ? designs[i].nn : nn;
     nmmax = designs[i].nm > nmmax ? designs[i].nm : nmmax;
   }
   const size_t lsm = rh::array_exc_smem(nn, nmmax);
@@ -761,6 +758,30 @@ long long rh_qtf_workspace_bytes(const rh_qtf_design* q) {
   return (long long)(rh::qtf_work_elems(*q) * sizeof(rh_c128));
 }
 
+// Rank's contiguous block [t0, t1) of the upper triangle's 16 x 16 pair tiles (row-major, T1 <=
+// T2): t_r is the first tile whose preceding tiles hold at least r / nrank of the pairs (i1 <=
+// i2 < n2; a diagonal tile holds 136 pairs, a full one 256), so the ranks' pair counts differ by
+// at most a tile's.  raft/parallel.py qtf_tile_block is the same integer arithmetic.
+static void qtf_tile_block(int n2, int rank, int nrank, int& t0, int& t1) {
+  const int nt = (n2 + 15) / 16;
+  std::vector<long long> cum(1, 0);   // pairs before tile t
+  for (int a = 0; a < nt; ++a) {
+    const long long ra = (16 * a + 16 < n2 ? 16 * a + 16 : n2) - 16 * a;
+    for (int b = a; b < nt; ++b) {
+      const long long cb = (16 * b + 16 < n2 ? 16 * b + 16 : n2) - 16 * b;
+      cum.push_back(cum.back() + (a == b ? ra * (ra + 1) / 2 : ra * cb));
+    }
+  }
+  const long long total = cum.back();
+  auto first = [&](int r) {   // smallest t with cum[t] * nrank >= r * total
+    int t = 0;
+    while (cum[t] * nrank < (long long)r * total) ++t;
+    return t;
+  };
+  t0 = first(rank);
+  t1 = rank + 1 == nrank ? (int)cum.size() - 1 : first(rank + 1);
+}
+
 static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
                       const double* M66, int rank, int nrank, int mirror, rh_c128* qtf, void* work,
                       long long work_bytes, rh_stream stream, const char* who) {
@@ -780,16 +801,35 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   if (!gemm) wk.R = nullptr;                                 // the table kernels skip the GEMM operands
   const int n2p = rh::qtf_n2p(*q);
   const int nb = (n2p + 63) / 64;
+  // This call's pair tiles (MFMA path): the rank's contiguous block [t0, t0 + blocks) of the
+  // upper triangle's 16 x 16 tiles in row-major order, cut at the pair-count quantiles
+  // (qtf_tile_block; raft/parallel.py qtf_tile_block mirrors it).  Its w1 rows are tile rows
+  // T1(t0) .. T1(t0 + blocks - 1); the tables and coefficients of lower frequencies are not read.
+  const int nt = n2p / 16;
+  int t0 = 0, t1 = 0;
+  qtf_tile_block(q->n2, rank, nrank, t0, t1);
+  const int blocks = t1 - t0;
+  auto row_of = [&](int t) {   // tile row of the t-th tile
+    int T1 = 0;
+    while (t >= nt - T1) {
+      t -= nt - T1;
+      ++T1;
+    }
+    return T1;
+  };
+  const int R0 = blocks > 0 ? row_of(t0) : 0, R1 = blocks > 0 ? row_of(t0 + blocks - 1) + 1 : 0;
+  const int fb0 = gemm ? 16 * R0 / 64 : 0;   // first 64-frequency block read (the per-pair path: all)
   // the frequency row, node, waterline and KAY tables (+ GEMM basis and zero K tails): one launch
   const int trows = 1 + q->nq + q->nmq + q->nkr + (gemm ? q->nq + rh::qtf_npad(*q) : 0);
-  hipLaunchKernelGGL(rh::k_qtf_tables, dim3(nb, trows), dim3(64), 0, s, *q, wk, nw, w, Xi0, M66);
-  RH_HIP(hipGetLastError());
+  if (nb > fb0) {
+    hipLaunchKernelGGL(rh::k_qtf_tables, dim3(nb - fb0, trows), dim3(64), 0, s, *q, wk, nw, w, Xi0, M66, fb0);
+    RH_HIP(hipGetLastError());
+  }
   if (gemm) {
-    // the w1-side GEMM coefficients, the Kim & Yue tile sums (both need only the tables), then
-    // the pair tiles: bilinear + potential GEMMs plus the Kim & Yue sums, and the Hermitian fill
-    // (rh_qtf_mfma.hip)
-    const int nt = n2p / 16, ntile = nt * (nt + 1) / 2;
-    const int blocks = (ntile - rank + nrank - 1) / nrank;
+    // the w1-side GEMM coefficients of the call's rows, the Kim & Yue tile sums (both need only
+    // the tables), then the pair tiles: bilinear + potential GEMMs plus the Kim & Yue sums, and
+    // the Hermitian fill (rh_qtf_mfma.hip)
+    const int bx0 = 16 * R0 / 64, nbx = blocks > 0 ? (16 * R1 + 63) / 64 - bx0 : 0;
 #ifdef RH_VARIANTS
     const bool sep = ctx->qtf_sep, t32 = ctx->qtf_t32;
 #else
@@ -798,15 +838,15 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
     if (blocks > 0 && !sep) {
       // the Kim & Yue tiles (two per workgroup) and the GEMM coefficient blocks in one launch
       const int nkb = (blocks + 1) / 2, nly = 18 + q->nq + q->nmq;
-      hipLaunchKernelGGL(rh::k_qtf_lk, dim3(nkb + nb * nly), dim3(rh::kLkThreads), 0, s, *q, wk, M66, rank, nrank,
-                         blocks, nkb, nb);
+      hipLaunchKernelGGL(rh::k_qtf_lk, dim3(nkb + nbx * nly), dim3(rh::kLkThreads), 0, s, *q, wk, M66, t0, blocks,
+                         nkb, bx0, nbx);
       RH_HIP(hipGetLastError());
     } else {
 #ifdef RH_VARIANTS
       hipLaunchKernelGGL(rh::k_qtf_lcoef, dim3(nb, 18 + q->nq + q->nmq), dim3(512), 0, s, *q, wk, M66);
       RH_HIP(hipGetLastError());
       if (blocks > 0) {
-        hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, s, *q, wk, rank, nrank);
+        hipLaunchKernelGGL(rh::k_qtf_kay, dim3(blocks), dim3(rh::kKayThreads), 0, s, *q, wk, t0);
         RH_HIP(hipGetLastError());
       }
 #endif
@@ -818,7 +858,7 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
         hipLaunchKernelGGL(rh::k_qtf_gemm32, dim3(nt32 * (nt32 + 1)), dim3(384), 0, s, *q, wk, qtf);
 #endif
       } else {
-        hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(2 * blocks), dim3(384), 0, s, *q, wk, qtf, rank, nrank, mirror);
+        hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(2 * blocks), dim3(384), 0, s, *q, wk, qtf, t0, mirror);
       }
       RH_HIP(hipGetLastError());
     }

@@ -204,6 +204,9 @@ struct CaseArgs {
   // 1: k_a0_sums has written every case's iteration-0 phase-A sums to its Xi_last block
   // (rh_a0.hip); k_solve_lds skips phase A of iteration 0 and reads them in phase B
   int a0 = 0;
+  // node stride of the Bmat output ([ncase][bmat_nn][9]): the largest nn of the call's designs,
+  // so designs with different node counts share one output array (rh_solve_cases sets it)
+  int bmat_nn = 0;
 };
 constexpr int kCaseStopped = 9;   // internal status between the two passes (never returned)
 

@@ -459,7 +459,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
   }
   if (a.o.B_drag && tid < 36) a.o.B_drag[(size_t)ic * 36 + tid] = bd[tid];
   if (a.o.Bmat)
-    for (int e = tid; e < nn * 9; e += kThreads) a.o.Bmat[(size_t)ic * nn * 9 + e] = bm[e];
+    for (int e = tid; e < nn * 9; e += kThreads) a.o.Bmat[(size_t)ic * a.bmat_nn * 9 + e] = bm[e];
   // a case that stopped on a NaN or a singular Z has no response (the reference raises there,
   // raft/raft_model.py:957): NaN Xi, PSD, RAO and std, as k_solve_lds writes them
   if (status == RH_CASE_NAN || status == RH_CASE_SINGULAR) {   // uniform
@@ -520,21 +520,26 @@ struct HeadArgs {
   const int* head;
   const double* zeta;
   const double* B_drag;
-  const double* Bmat;
+  const double* Bmat;      // [ncase][bmat_nn][9]
   rh_c128* Xi;
   rh_c128* F;             // non-NULL: store the wave excitation only (no solve)
+  int bmat_nn;            // node stride of Bmat: the largest nn of the call's designs
+  int ndesign;            // designs[] entries: a design index outside [0, ndesign) is not read
 };
 
 __global__ __launch_bounds__(kThreads, 2) void k_heading_resp(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int ic = blockIdx.y;
-  const rh_design& d = a.designs[a.design_idx[ic]].d;
+  const int di = a.design_idx[ic];
+  if (di < 0 || di >= a.ndesign) return;   // uniform: a bad index from the caller writes nothing
+  const rh_design& d = a.designs[di].d;
+  if (a.head[ic] < 0 || a.head[ic] >= d.nhead) return;   // ... nor does a heading not tabulated
   const int nw = d.nw, nn = d.nn;
   double* bm = smem;
   double* bd = bm + 9 * nn;
   double* mbc = bd + 36;
   load_mbc(d, mbc, threadIdx.x);
-  for (int e = threadIdx.x; e < nn * 9; e += blockDim.x) bm[e] = a.Bmat[(size_t)ic * nn * 9 + e];
+  for (int e = threadIdx.x; e < nn * 9; e += blockDim.x) bm[e] = a.Bmat[(size_t)ic * a.bmat_nn * 9 + e];
   if (threadIdx.x < 36 && a.B_drag) bd[threadIdx.x] = a.B_drag[(size_t)ic * 36 + threadIdx.x];
   __syncthreads();
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1031,7 +1036,7 @@ struct ArrayArgs {
   const int* head;             // [ncase * NF] heading index of each entry
   const double* zeta;          // [ncase * NF][nw]
   const double* B_drag;        // [ncase * NF][36]
-  const double* Bmat;          // [ncase * NF][nn][9] (equal nn over the FOWTs)
+  const double* Bmat;          // [ncase * NF][nn_max][9] (FOWTs may differ in node count)
   const double* K;             // [6 NF][6 NF] array stiffness, or NULL
   rh_c128* Xi;                 // [ncase][6 NF][nw]: F from k_array_exc, then the response
   int nn_max, nm_max;          // largest node / member counts of the designs (dynamic LDS layout)
@@ -1061,7 +1066,7 @@ __global__ __launch_bounds__(kArrExcThreads) void k_array_exc(ArrayArgs a) {
   const int ic = (int)(e / NF), f = (int)(e % NF);
   const rh_design& d = a.designs[a.design_idx[e]].d;
   const int nn = d.nn, nm = d.nm, nw = d.nw, head = a.head[e];
-  const double* Bm = a.Bmat + e * nn * 9;
+  const double* Bm = a.Bmat + e * nnA * 9;
   for (int n = tid; n < nn; n += kArrExcThreads) {
     double c[3];
 #pragma unroll

@@ -423,11 +423,13 @@ __global__ __launch_bounds__(64) void k_qtf_hankel(int n2, const double* __restr
 // (blockIdx.y = node, then member, then KAY row), after k_qtf_freq.  One launch instead of
 // three small ones whose grids (a few hundred waves each) left the GPU mostly idle.
 __global__ __launch_bounds__(64) void k_qtf_tables(rh_qtf_design q, QtfWork wk, int nw, const double* __restrict__ w,
-                                                    const rh_c128* __restrict__ Xi0, const double* __restrict__ M66) {
+                                                    const rh_c128* __restrict__ Xi0, const double* __restrict__ M66,
+                                                    int fb0) {
   // blockIdx.y: the frequency row (k_qtf_freq before round 4), node tables, waterline tables,
   // KAY tables; on the MFMA path also the node GEMM basis and the zero K-tail rows, as rows of
-  // their own (more waves in flight)
-  const int f = blockIdx.x * 64 + threadIdx.x;
+  // their own (more waves in flight).  Frequencies from 64 fb0: a call that computes only the
+  // pair tiles of rows i1 >= 64 fb0 reads no table entry below (i2 >= i1 on every tile).
+  const int f = (fb0 + blockIdx.x) * 64 + threadIdx.x;
   const bool basis = wk.R != nullptr && f < qtf_n2p(q);   // MFMA path operands (zero padded to n2p)
   int y = blockIdx.y;
   if (y == 0) {

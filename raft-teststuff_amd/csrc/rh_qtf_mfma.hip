@@ -920,8 +920,8 @@ __device__ __forceinline__ void qtf_tile_of(int t, int nt, int& T1, int& T2) {
 // (the three waves of a half share the R tile through L1); the second half's partial sums
 // reach the first through LDS.  Blocks are (tile, DOF half) pairs, remapped so that an XCD
 // works on a contiguous run of tiles (their L rows stay in its L2).
-__global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf, int rank,
-                                                  int nrank, int mirror) {
+__global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf, int t0,
+                                                  int mirror) {
   __shared__ double part[3][16][64];
   __shared__ double pscal[4][256];   // per pair: aux2 (w1 - w2) alpha+, ... alpha- (complex)
   const int lane = (int)threadIdx.x & 63;
@@ -930,7 +930,7 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
   const int n2 = q.n2, n2p = qtf_n2p(q), nt = n2p / 16, kp = qtf_kp(q), kq = qtf_kq(q);
   const int slot = xcd_remap((int)blockIdx.x, (int)gridDim.x);
   const int d = 3 * (slot & 1) + dl;
-  int T1 = 0, t = rank + nrank * (slot >> 1);
+  int T1 = 0, t = t0 + (slot >> 1);   // this call's tiles: t0, t0 + 1, ... (row-major)
   while (t >= nt - T1) {   // block-uniform
     t -= nt - T1;
     ++T1;
@@ -1212,7 +1212,7 @@ constexpr int kLkThreads = 2 * kKayThreads;
 
 static_assert(kLkThreads == 512, "k_qtf_lk: lcoef_block is a 512-thread block");
 __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(RH_KAY_WPE))) void k_qtf_lk(
-    rh_qtf_design q, QtfWork wk, const double* __restrict__ M66, int rank, int nrank, int ntile, int nkb, int nbx) {
+    rh_qtf_design q, QtfWork wk, const double* __restrict__ M66, int t0, int ntile, int nkb, int bx0, int nbx) {
   constexpr int kAcc = 12 * 256, kRed = 8 * 12 * 64;
   constexpr int kSm = 2 * kAcc > kRed ? 2 * kAcc : kRed;
   __shared__ double sm[kSm];                 // two Kim & Yue tile sums, or lcoef_block's wave sums
@@ -1223,14 +1223,15 @@ __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(RH_K
     const int t = 2 * xcd_remap((int)blockIdx.x, nkb) + grp;   // this group's tile of the rank's order
     const bool live = t < ntile;
     int T1 = 0, T2 = 0;
-    if (live) qtf_tile_of(rank + nrank * t, qtf_n2p(q) / 16, T1, T2);
+    if (live) qtf_tile_of(t0 + t, qtf_n2p(q) / 16, T1, T2);
     kay_tile(q, wk, T1, T2, live, tid - grp * kKayThreads, reinterpret_cast<double(*)[256]>(sm + grp * kAcc),
              psg + (kKayS > 1 ? grp * kKayM * (kKayS - 1) * 16 * 64 : 0));
   } else {
     // (k_qtf_lcoef's block order; frequency-block-major runs per XCD cut the launch's HBM reads
-    // from 52 to 31 MB but cost 3.5 us per QTF)
+    // from 52 to 31 MB but cost 3.5 us per QTF); the w1 blocks bx0 .. bx0 + nbx - 1
+    // hold this call's w1 rows
     const int bl = (int)blockIdx.x - nkb;
-    lcoef_block(q, wk, M66, bl % nbx, bl / nbx, reinterpret_cast<double(*)[12][64]>(sm));
+    lcoef_block(q, wk, M66, bx0 + bl % nbx, bl / nbx, reinterpret_cast<double(*)[12][64]>(sm));
   }
 }
 

@@ -205,7 +205,7 @@ __host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB, int LT 
                            + (size_t)(ser && nn * 3 * LW < 27 ? 27 : nn * 3 * LW)   // per-wave node sums (SER: >= 27 entries)
                            + (ser ? (size_t)0 : (size_t)nn * 36)   // per-node B_drag contributions
                            + (size_t)nn * 9           // Bmat
-                           + (size_t)nn * 5           // member-factored drag coefficients
+                           + (size_t)nn * 6           // member-factored drag coefficients (stride 6: 16-B rows)
                            + (size_t)nn               // node axial coordinate t
                            + (size_t)nm * 18          // member cq, c1, c2
                            + (size_t)2 * LT * NB * NP   // w and zeta per (padded) bin
@@ -260,24 +260,27 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   constexpr bool GX = NP > 1;                      // XiLast in the Xi_last block, not in LDS
   cd* xl = reinterpret_cast<cd*>(smem);            // [6][NWP] (one pass only)
   rh_c128* XL = a.o.Xi_last + c6;                  // [6][nw] (GX)
-  double* red = smem + (GX ? 0 : 12 * NWP);        // [nn*3][LW]
+  // The member factors and the node coefficients, read at every member change and node step of
+  // the loops, come first, member- / node-major with 16-byte rows (a member's 18 factors are
+  // 9 ds_read_b128 at one base address instead of 18 scattered reads at nm-strided addresses).
+  double* mbf = smem + (GX ? 0 : 12 * NWP);        // [nm][18] cq, c1, c2
+  double* al = mbf + 18 * nm;                      // [nn][6] (5 used)
+  double* red = al + 6 * nn;                       // [nn*3][LW]
   double* bm = red + (SER && nn * 3 * LW < 27 ? 27 : nn * 3 * LW);   // [nn][9]
-  double* al = bm + nn * 9;                        // [nn][5]
-  double* bd = al + nn * 5;                        // [36]
+  double* bd = bm + nn * 9;                        // [36]
   double* mbc = bd + 36;                           // [108] M, B_lin, C
   double* sred = mbc + 108;                        // [LW][6]
   double* bsum = sred + LW * 6;                   // [36] B_lin + B_drag of this iteration
   double* bdn = bsum + 36;                         // [36][nn] (not with SER)
   double* nt = bdn + (SER ? 0 : 36 * nn);          // [nn]
-  double* mbf = nt + nn;                           // [18][nm]
-  double* lw = mbf + 18 * nm;                      // [NP NWP] w per bin (pad bins: w[nw-1])
+  double* lw = nt + nn;                            // [NP NWP] w per bin (pad bins: w[nw-1])
   double* lz = lw + NP * NWP;                      // [NP NWP] zeta per bin (pad bins: 0)
   double* mred = lz + NP * NWP;                    // [LW] per-wave max of tolCheck
   int* mstart = reinterpret_cast<int*>(mred + LW);  // [nm+1]
   int* sflag = mstart + nm + 1;                      // [2] vote words of even / odd iterations
   load_mbc(d, mbc, tid);
   for (int n = tid; n < nn; n += LT) nt[n] = node[RH_NF_T * nn + n];
-  for (int e = tid; e < 18 * nm; e += LT) mbf[e] = d.memb[e];   // RH_MF_CQ0..C20 are fields 0..17
+  for (int e = tid; e < 18 * nm; e += LT) mbf[e] = d.memb[(e % 18) * nm + e / 18];   // RH_MF_CQ0..C20: fields 0..17
   for (int e = tid; e <= nm; e += LT) mstart[e] = d.mstart[e];
   if (tid < 2) sflag[tid] = 0;
   const int it0 = resume ? stop_iter : a.c.first_iter;
@@ -388,9 +391,9 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
         double cq[6], c1[6], c2[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-          cq[i] = mbf[(RH_MF_CQ0 + i) * nm + m];
-          c1[i] = mbf[(RH_MF_C10 + i) * nm + m];
-          c2[i] = mbf[(RH_MF_C20 + i) * nm + m];
+          cq[i] = mbf[18 * m + RH_MF_CQ0 + i];
+          c1[i] = mbf[18 * m + RH_MF_C10 + i];
+          c2[i] = mbf[18 * m + RH_MF_C20 + i];
         }
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
@@ -543,7 +546,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       double B4[4];
       node_bmat(node, nn, n, rho, sums, bm + 9 * n, B4);
       const double t = nf(node, nn, RH_NF_T, n);
-      double* A = al + 5 * n;
+      double* A = al + 6 * n;
       A[0] = B4[0] + B4[3];     // axial: side + end   (qMat terms of Bmat, raft/raft_fowt.py:1228-1248)
       A[1] = B4[1];
       A[2] = B4[2];
@@ -638,13 +641,13 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
         auto fold = [&]() {   // close member m: F += sum of its nodes (as drag_exc_members)
 #pragma unroll
           for (int i = 0; i < 6; ++i) {
-            const double cq = mbf[(RH_MF_CQ0 + i) * nm + m], c1 = mbf[(RH_MF_C10 + i) * nm + m],
-                         c2 = mbf[(RH_MF_C20 + i) * nm + m];
+            const double cq = mbf[18 * m + RH_MF_CQ0 + i], c1 = mbf[18 * m + RH_MF_C10 + i],
+                         c2 = mbf[18 * m + RH_MF_C20 + i];
             F[i] = add(F[i], add(add(scl(SQ, cq), scl(S1, c1)), scl(S2, c2)));
           }
 #pragma unroll
           for (int i = 0; i < 3; ++i) {
-            const double p1 = mbf[(RH_MF_C10 + i) * nm + m], p2 = mbf[(RH_MF_C20 + i) * nm + m];
+            const double p1 = mbf[18 * m + RH_MF_C10 + i], p2 = mbf[18 * m + RH_MF_C20 + i];
             F[3 + i] = add(F[3 + i], sub(scl(T1, p2), scl(T2, p1)));
           }
           SQ = S1 = S2 = T1 = T2 = mk(0, 0);
@@ -655,7 +658,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
             ++m;
             mnext = mstart[m + 1];
           }
-          const double* A = al + 5 * n;
+          const double* A = al + 6 * n;
           const double A0 = A[0], A1 = A[1], A2 = A[2], A3 = A[3], A4 = A[4];
 #if RH_ABL_C_NOCOMP
           SQ = add(SQ, K[0]); S1 = add(S1, K[1]); S2 = add(S2, K[2]);
@@ -859,7 +862,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   }
   if (a.o.B_drag && tid < 36) a.o.B_drag[(size_t)ic * 36 + tid] = bd[tid];
   if (a.o.Bmat)
-    for (int e = tid; e < nn * 9; e += LT) a.o.Bmat[(size_t)ic * nn * 9 + e] = bm[e];
+    for (int e = tid; e < nn * 9; e += LT) a.o.Bmat[(size_t)ic * a.bmat_nn * 9 + e] = bm[e];
   if (a.o.Z) {   // final impedance fowt.Z (raft/raft_model.py:1013) from the last B_drag, streamed
 #pragma unroll 1
     for (int j = 0; j < NBT; ++j) {

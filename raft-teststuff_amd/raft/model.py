@@ -485,19 +485,35 @@ class Model:
         return self.results
 
     def analyzeCasesBatch(self, cases, tol=0.01, want=("psd", "std", "zeta", "B_drag"), host=True):
-        """Solve many single-sea-state cases in one device call (one workgroup per case).
-        cases: list of case dicts (wave_heading/spectrum/period/height/gamma; with wind_speed
-        > 0 on an operating rotor, that case's aero-servo M and B from calcTurbineConstants).  Returns a dict
-        of arrays: Xi [n,6,nw], iters, status, psd [n,6,nw], std [n,6], ...
+        """Solve many cases in one device call (one workgroup per case's drag fixed point).
+        cases: list of case dicts (wave_heading/spectrum/period/height/gamma, each a scalar or
+        one entry per sea state; with wind_speed > 0 on an operating rotor, that case's
+        aero-servo M and B from calcTurbineConstants).  Returns a dict of arrays: Xi [n,6,nw]
+        (the first sea state), iters, status, psd [n,6,nw], std [n,6], ...
+        A case with several sea states is solved as Model.solveDynamics solves it
+        (raft/raft_model.py:918-1065): the drag linearisation from its first sea state, then the
+        response to each sea state with that linearisation frozen (one rh_heading_response launch
+        for every extra sea state of the batch); Xi_waves [n, nW+1, 6, nw] holds them in the
+        reference's layout (nW = the batch's largest sea-state count, rows of absent sea states
+        and the last row zero) and psd / std sum over the sea states (getPSD / getRMS).
         Arrays (nFOWT > 1) go through analyzeArrayBatch: Xi [n,6N,nw], iters [n,N], ..."""
         if self.nFOWT != 1:
             return self.analyzeArrayBatch(cases, tol=tol, host=host)
         fowt = self.fowtList[0]
-        hd, sp, Hs, Tp, gm = self._case_columns(cases)
+        seas = [self._case_sea_states(c) for c in cases]
+        nws = np.array([len(s[0]) for s in seas], dtype=np.int64)
+        hd, sp, Hs, Tp, gm = ([s[k][0] for s in seas] for k in range(5))
+        multi = len(cases) > 0 and nws.max() > 1
+        want_fp = tuple(want) + (("Bmat", "B_drag") if multi else ())
         aero = [self._operating_rotor(fowt, c) for c in cases]
+        if multi:   # every heading tabulated before the fixed point (its tables stay put)
+            fowt.device_design().ensure_headings(np.concatenate([np.asarray(s[0], dtype=float) for s in seas]) * DEG2RAD)
         if not any(aero):
+            views = [fowt.device_design()]
             cs = CaseSet(np.zeros(len(cases), dtype=np.int32), hd, sp, Hs, Tp, gm)
-            res = solve_batch([fowt.device_design()], cs, self.nIter, self.XiStart, tol, want=want)
+            res = solve_batch(views, cs, self.nIter, self.XiStart, tol, want=want_fp)
+            if multi:
+                self._extra_sea_states(res, views, cs.design_idx, seas, nws, want)
             return res.host() if host else res
         # operating rotors: each such case gets its own per-bin M and B (its rotors' aero-servo
         # added mass and damping, FOWT.calcTurbineConstants) on the shared node and wave tables
@@ -515,8 +531,73 @@ class Model:
                 views.append(CaseMB(base, torch.tensor(M, **f64).contiguous(), torch.tensor(B, **f64).contiguous()))
                 idx[i] = len(views) - 1
         cs = CaseSet(idx, hd, sp, Hs, Tp, gm)
-        res = solve_batch(views, cs, self.nIter, self.XiStart, tol, want=want)
+        res = solve_batch(views, cs, self.nIter, self.XiStart, tol, want=want_fp)
+        if multi:
+            self._extra_sea_states(res, views, idx, seas, nws, want)
         return res.host() if host else res
+
+    @staticmethod
+    def _case_sea_states(case):
+        """The sea states of one case dict, read as FOWT.calcHydroExcitation reads them
+        (raft/raft_fowt.py:982-1014): (heading [deg], spectrum, Hs, Tp, gamma), one entry each
+        per sea state."""
+        c = dict(case)
+        hd = c.get("wave_heading", 0)
+        nW = 1 if np.isscalar(hd) else len(hd)
+        col = lambda k, **kw: list(np.atleast_1d(get_from_dict(c, k, shape=nW, **kw)))   # noqa: E731
+        sp = [str(x) for x in col("wave_spectrum", dtype=str, default="JONSWAP")]
+        for x in sp:
+            if x not in N.SPECTRUM_CODES:
+                raise ValueError(f"Wave spectrum input '{x}' not recognized.")
+        return ([float(x) for x in col("wave_heading", dtype=float, default=0)], sp,
+                [float(x) for x in col("wave_height", dtype=float)], [float(x) for x in col("wave_period", dtype=float)],
+                [float(x) for x in col("wave_gamma", dtype=float, default=0)])
+
+    def _extra_sea_states(self, res, views, idx, seas, nws, want):
+        """The response of every case's further sea states with its drag linearisation frozen
+        (raft/raft_model.py:1049-1065): their spectra (rh_sea_state), one rh_heading_response
+        launch for all of them, Xi_waves [n, nW+1, 6, nw] and psd / std over all sea states
+        (rh_motion_stats, getPSD / getRMS of raft/raft_fowt.py:1831-1875)."""
+        import torch
+        n, nw = len(seas), self.nw
+        nwm = int(nws.max())
+        dd = views[0]
+        dev = dd.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        ext = [(i, h) for i in range(n) for h in range(1, int(nws[i]))]
+        ci = np.array([i for i, _ in ext], dtype=np.int64)
+        pick = lambda k: [seas[i][k][h] for i, h in ext]   # noqa: E731
+        heads = dd.ensure_headings(np.array(pick(0), dtype=float) * DEG2RAD)
+        ctx, s = N.context(self.device), N.stream_handle(torch, dev)
+        m = len(ext)
+        zeta = torch.empty([m, nw], **f64)
+        spec = torch.tensor([N.SPECTRUM_CODES[x] for x in pick(1)], **i32)
+        Hs, Tp, gm = (torch.tensor(pick(k), **f64) for k in (2, 3, 4))
+        N.check(N.lib().rh_sea_state(ctx, m, nw, N.ptr(dd.w), float(dd.dw), N.ptr(spec), N.ptr(Hs), N.ptr(Tp),
+                                     N.ptr(gm), None, N.ptr(zeta), s), "rh_sea_state")
+        sel = torch.tensor(ci, dtype=torch.long, device=dev)
+        bdrag = res["B_drag"].index_select(0, sel).contiguous()
+        bmat = res["Bmat"].index_select(0, sel).contiguous()
+        XiE = torch.empty([m, 6, nw], dtype=torch.complex128, device=dev)
+        arr = (N.RhDesign * len(views))(*[v.struct() for v in views])
+        # (the index tensors are held in names: a temporary freed before the call returns would
+        # hand its block to the next allocation, and the kernel would read the other array)
+        didx = torch.tensor(np.asarray(idx)[ci], **i32)
+        hidx = torch.tensor(heads, **i32)
+        N.check(N.lib().rh_heading_response(ctx, arr, len(views), m, N.ptr(didx), N.ptr(hidx), N.ptr(zeta),
+                                            N.ptr(bdrag), N.ptr(bmat), N.ptr(XiE), s), "rh_heading_response")
+        Xw = torch.zeros([n, nwm + 1, 6, nw], dtype=torch.complex128, device=dev)
+        Xw[:, 0] = res["Xi"]
+        Xw[sel, torch.tensor([h for _, h in ext], dtype=torch.long, device=dev)] = XiE
+        res["Xi_waves"] = Xw
+        if "psd" in want or "std" in want:
+            psd = torch.empty([n, 6, nw], **f64)
+            std = torch.empty([n, 6], **f64)
+            N.check(N.lib().rh_motion_stats(ctx, n, nwm + 1, nw, float(dd.dw), N.ptr(Xw), N.ptr(psd), N.ptr(std), s),
+                    "rh_motion_stats")
+            res["psd"], res["std"] = psd, std
+        res["nWaves"] = torch.tensor(nws, dtype=torch.int64, device=dev)
 
     @staticmethod
     def _operating_rotor(fowt, case):
@@ -529,31 +610,17 @@ class Model:
         speed = get_from_dict(case, "wind_speed", shape=0, default=0.0)
         return status == "operating" and speed > 0.0 and bool(np.any(np.atleast_1d(fowt._aero_mod) > 0))
 
-    @staticmethod
-    def _case_columns(cases):
-        hd, sp, Hs, Tp, gm = [], [], [], [], []
-        for c in cases:
-            c = dict(c)
-            if not np.isscalar(c["wave_heading"]) and len(c["wave_heading"]) != 1:
-                raise NotImplementedError("analyzeCasesBatch: one sea state per case")
-            one = lambda k, dflt=None: (np.atleast_1d(c.get(k, dflt))[0] if c.get(k, dflt) is not None else None)
-            hd.append(float(one("wave_heading", 0)))
-            sp.append(str(one("wave_spectrum", "JONSWAP")))
-            Hs.append(float(one("wave_height")))
-            Tp.append(float(one("wave_period")))
-            gm.append(float(one("wave_gamma", 0)))
-        return hd, sp, Hs, Tp, gm
-
     def prepareArrayBatch(self, cases):
         """The per-batch inputs of analyzeArrayBatch resident on the device: the (case, FOWT)
         case table with its wave tables (solver.prepare_batch), the FOWT descriptors and the
         array stiffness.  Reusable for repeated solves of the same sea states."""
         import torch
         nf, n = self.nFOWT, len(cases)
-        dds = [f.device_design() for f in self.fowtList]
-        if len(set(d.nn for d in dds)) != 1:
-            raise NotImplementedError("analyzeArrayBatch: FOWTs with different submerged node counts")
-        hd, sp, Hs, Tp, gm = self._case_columns(cases)
+        dds = [f.device_design() for f in self.fowtList]   # (node counts may differ: Bmat rows padded to the largest)
+        seas = [self._case_sea_states(c) for c in cases]
+        if any(len(x[0]) != 1 for x in seas):
+            raise NotImplementedError("analyzeArrayBatch: one sea state per case")
+        hd, sp, Hs, Tp, gm = ([x[k][0] for x in seas] for k in range(5))
         rep = lambda v: [x for x in v for _ in range(nf)]          # case-major, FOWT-minor
         cs = CaseSet(np.tile(np.arange(nf, dtype=np.int32), n), rep(hd), rep(sp), rep(Hs), rep(Tp), rep(gm))
         dev = dds[0].device

@@ -7,8 +7,10 @@ One process per GPU, torch.distributed with backend "nccl" (RCCL over xGMI).  Tw
   independent); the responses are gathered once at the end (all_gather), the "final
   response-spectrum gather" of the north star.  Weak scaling in bench.py.
 * QTF (w1, w2) pairs -- the upper triangle in 16 x 16 pair tiles (the MFMA tile of
-  rh_qtf_mfma.hip), numbered row-major and dealt round robin, so every rank gets
-  n2(n2+1)/(2 world) pairs to within about a tile row.  The disjoint tile shards are
+  rh_qtf_mfma.hip), numbered row-major and cut into contiguous blocks at the pair-count quantiles
+  (row blocks balanced by pair count, to within a tile).  A rank's block spans a few w1 tile rows,
+  so it computes the w1-side coefficients of those rows only and the frequency tables from its
+  first row on (rh_qtf_slender_rows), not the whole grid's.  The disjoint tile shards are
   exchanged with one all_gather of each rank's packed upper-triangle pairs (exact copies),
   then the Hermitian lower triangle is filled on every rank.
 
@@ -47,12 +49,34 @@ def case_shard(n, rank, world):
 QTF_TILE = 16
 
 
+def qtf_tile_block(n2, rank, world):
+    """[t0, t1) of rank's contiguous block of the row-major upper-triangle tiles, cut at the
+    pair-count quantiles: t_r is the first tile whose preceding tiles hold at least r / world of
+    the pairs (rh_abi.hip qtf_tile_block, the same integer arithmetic)."""
+    nt = -(-n2 // QTF_TILE)
+    cum = [0]
+    for a in range(nt):
+        ra = min(QTF_TILE * a + QTF_TILE, n2) - QTF_TILE * a
+        for b in range(a, nt):
+            cb = min(QTF_TILE * b + QTF_TILE, n2) - QTF_TILE * b
+            cum.append(cum[-1] + (ra * (ra + 1) // 2 if a == b else ra * cb))
+    total = cum[-1]
+
+    def first(r):
+        t = 0
+        while cum[t] * world < r * total:
+            t += 1
+        return t
+    return first(rank), (len(cum) - 1 if rank + 1 == world else first(rank + 1))
+
+
 def qtf_tiles(n2, rank, world):
     """16 x 16 upper-triangle pair tiles (T1 <= T2) of rank, as rh_qtf_slender_rows deals
-    them: tiles numbered row-major, tile t goes to rank t % world."""
+    them: tiles numbered row-major, rank's contiguous block qtf_tile_block."""
     nt = -(-n2 // QTF_TILE)
     allt = [(a, b) for a in range(nt) for b in range(a, nt)]
-    return allt[rank::world]
+    t0, t1 = qtf_tile_block(n2, rank, world)
+    return allt[t0:t1]
 
 
 def qtf_pair_flat(n2, tiles):

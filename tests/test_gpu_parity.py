@@ -169,6 +169,42 @@ def test_non_convergence_and_xistart():
             assert rel(res["Xi"][ic], r["Xi"][0]) < RTOL
 
 
+def test_multi_sea_state_cases_through_the_batch():
+    """analyzeCasesBatch on cases with several sea states (raft/raft_model.py:918-1065: the drag
+    linearisation from the first, the response to each with it frozen): the reference's
+    multi-heading golden run (2 sea states) reproduced inside a batch that mixes it with
+    single-sea-state cases and a 3-sea-state case -- Xi_waves in the reference's [nW+1, 6, nw]
+    layout, iteration counts, and the motion PSD / std summed over the sea states, at 1e-9;
+    every case of the batch also equals its own Model.solveDynamics."""
+    T = load_golden("multi_heading")
+    m, f = make_model("VolturnUS-S_test", T)
+    gc = golden_cases(T)[0]
+    three = dict(wave_spectrum=["JONSWAP"] * 3, wave_period=[10.0, 7.0, 14.0], wave_height=[4.0, 1.5, 3.0],
+                 wave_heading=[30.0, 90.0, 0.0], wave_gamma=[0.0, 3.3, 1.0])
+    single = dict(wave_spectrum="JONSWAP", wave_period=9.0, wave_height=3.0, wave_heading=60.0, wave_gamma=0.0)
+    cases = [single, dict(gc), three, dict(gc)]
+    res = m.analyzeCasesBatch(cases)
+    assert res["Xi_waves"].shape == (4, 4, 6, m.nw)
+    np.testing.assert_array_equal(res["nWaves"], [1, 2, 3, 2])
+    dofs = ["surge", "sway", "heave", "roll", "pitch", "yaw"]
+    for ic in (1, 3):
+        assert res["iters"][ic] == T["out_iters"][0]
+        assert rel(res["Xi_waves"][ic, :3], T["out_Xi"][0]) < RTOL, rel(res["Xi_waves"][ic, :3], T["out_Xi"][0])
+        assert np.all(res["Xi_waves"][ic, 3] == 0)
+        smax = max(T[f"out_{d}_std"][0] for d in dofs)
+        pmax = max(T[f"out_{d}_PSD"][0].max() for d in dofs)
+        for k, d in enumerate(dofs):
+            np.testing.assert_allclose(res["std"][ic, k], T[f"out_{d}_std"][0], rtol=RTOL, atol=RTOL * smax)
+            np.testing.assert_allclose(res["psd"][ic, k], T[f"out_{d}_PSD"][0], rtol=RTOL, atol=RTOL * pmax)
+    for ic, case in enumerate(cases):
+        Xi = m.solveDynamics(dict(case))
+        nW = Xi.shape[0] - 1
+        assert res["iters"][ic] == f.iterations
+        assert rel(res["Xi_waves"][ic, :nW + 1], Xi) < 1e-12, ic
+        assert rel(res["Xi"][ic], Xi[0]) < 1e-12, ic
+        np.testing.assert_allclose(res["std"][ic], f._stats["std"], rtol=1e-12, atol=1e-15)
+
+
 def test_nan_raises_reference_message():
     T = load_golden("c1_OC3spar")
     m, f = make_model("OC3spar", T)

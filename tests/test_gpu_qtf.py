@@ -219,9 +219,9 @@ def test_qtf_text_outputs(T, tmp_path):
 
 
 def test_tile_sharded_qtf_equals_single_device(T):
-    """rh_qtf_slender_rows over 3 simulated ranks (tiles dealt round robin) + sum +
-    rh_qtf_hermitian_fill reproduces
-    rh_qtf_slender bit for bit (the multi-GPU exchange of raft/parallel.py)."""
+    """rh_qtf_slender_rows over 3 and 8 simulated ranks (contiguous tile blocks, each call
+    computing the tables and w1 coefficients of its own rows only) + sum + rh_qtf_hermitian_fill
+    reproduces rh_qtf_slender bit for bit (the multi-GPU exchange of raft/parallel.py)."""
     import torch
     m, f = make(T)
     f.calcHydroExcitation(_case(T), memberList=f.memberList)
@@ -230,13 +230,14 @@ def test_tile_sharded_qtf_equals_single_device(T):
     dd = f.device_design()
     X = torch.tensor(T["out_Xi0"], dtype=torch.complex128, device=dd.device)
     M66 = torch.tensor(f.M_struc, dtype=torch.float64, device=dd.device).contiguous()
-    acc = torch.zeros([qd.n2, qd.n2, 6], dtype=torch.complex128, device=dd.device)
-    for r in range(3):
-        part = torch.zeros_like(acc)
-        qd.qtf_rows(dd.w, X, M66, part, r, 3)
-        acc += part
-    qd.hermitian_fill(acc)
-    np.testing.assert_array_equal(acc.cpu().numpy(), f.qtf[:, :, 0, :])
+    for world in (3, 8):
+        acc = torch.zeros([qd.n2, qd.n2, 6], dtype=torch.complex128, device=dd.device)
+        for r in range(world):
+            part = torch.zeros_like(acc)
+            qd.qtf_rows(dd.w, X, M66, part, r, world)
+            acc += part
+        qd.hermitian_fill(acc)
+        np.testing.assert_array_equal(acc.cpu().numpy(), f.qtf[:, :, 0, :])
 
 
 def test_force_spectrum_mode_matches_reference(T):

@@ -184,6 +184,43 @@ def test_farm_batch_matches_reference_and_oracle():
         np.testing.assert_allclose(r["std"][:, i], np.sqrt(0.5 * np.sum(np.abs(x) ** 2, axis=2)), rtol=1e-12)
 
 
+def test_heterogeneous_farm_batch_matches_oracle():
+    """A 2-FOWT farm whose platforms differ (raft/raft_model.py:137-156 lets each FOWT take its
+    own platform): the second is a parametersweep variant with 1.5x pontoons, 61 submerged nodes
+    against 53.  analyzeArrayBatch (Bmat rows padded to the larger node count) against
+    oracle.solve_farm on the host-prepared tables of both FOWTs: identical iteration counts,
+    Xi at 1e-9; and the per-case Model.solveDynamics path against the batch."""
+    import raft
+    from conftest import oracle_tables_of
+    from raft.sweep import sweep_variant
+    T = load_golden("c4_farm")
+    Ts = farm_tables(T)
+    d = load_design("VolturnUS-S_farm")
+    d["platforms"] = [d["platform"], sweep_variant({"platform": d["platform"]}, (1.0, 1.0, 1.5, 1.0, 1.0))["platform"]]
+    d["array"]["data"][1][1] = 2
+    m = raft.Model(d, statics=[{"C_moor": t["C_moor"]} for t in Ts])
+    m.K_array = T["K_array"]
+    for f, t in zip(m.fowtList, Ts):
+        f.setPosition(t["r6"])
+        f.calcStatics()
+        f.calcHydroConstants()
+    nns = [f.device_design().nn for f in m.fowtList]
+    assert nns[0] != nns[1], nns
+    rng = np.random.default_rng(46)
+    cases = [dict(wave_spectrum="JONSWAP", wave_period=float(rng.uniform(6, 18)), wave_height=float(rng.uniform(1, 10)),
+                  wave_heading=float(rng.choice([0, 45, 135, 270])), wave_gamma=float(rng.choice([0.0, 2.0])))
+             for _ in range(12)]
+    r = m.analyzeCasesBatch(cases)
+    Tor = [oracle_tables_of(f) for f in m.fowtList]
+    for j in (0, 5, 11):
+        o = O.solve_farm(Tor, dict(cases[j]), int(m.nIter), T["K_array"], float(m.XiStart))
+        assert list(r["iters"][j]) == o["iters"]
+        assert rel(r["Xi"][j], o["Xi"][0]) < RTOL, rel(r["Xi"][j], o["Xi"][0])
+    Xi = m.solveDynamics(dict(cases[3]))
+    assert [f.iterations for f in m.fowtList] == list(r["iters"][3])
+    assert rel(r["Xi"][3], Xi[0]) < 1e-12
+
+
 def test_batched_wave_tables_equal_per_design_tables():
     """rh_wave_tables_batch (one launch for a sweep) writes the same bits as rh_wave_tables
     per design, for designs with different node counts and two headings each."""

@@ -9,6 +9,27 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "raft-teststuff_amd"))
 
 
+def time_ranks(qd, dd, X, M66, world, reps=50):
+    """Each rank's share of a QTF sharded over `world` GPUs (rh_qtf_slender_rows), timed alone
+    on this GPU with HIP events around `reps` back-to-back calls: one line per rank, then the
+    whole QTF (rh_qtf_slender) for comparison."""
+    import torch
+    out = torch.zeros([qd.n2, qd.n2, 6], dtype=torch.complex128, device=dd.device)
+    for r in list(range(world)) + [None]:
+        call = (lambda: qd.qtf(dd.w, X, M66)) if r is None else (lambda: qd.qtf_rows(dd.w, X, M66, out, r, world))
+        for _ in range(5):
+            call()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            call()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / reps * 1e3
+        print(f"{'whole QTF' if r is None else f'rank {r} of {world}':>14s}: {us:8.1f} us per call", flush=True)
+
+
 def main(tag):
     import torch
     import bench
@@ -16,6 +37,9 @@ def main(tag):
     from raft.qtf import QtfDevice
     T, f, dd, X, M66, w2, k2 = bench.build_qtf(0)
     qd = QtfDevice(f, w2, k2, 0.0, 0)
+    if tag == "ranks":
+        time_ranks(qd, dd, X, M66, int(sys.argv[2]) if len(sys.argv) > 2 else 8)
+        return
     ref = None
     # PMC passes: the default path only (MFMA GEMMs on this sorted grid); otherwise the
     # per-pair kernel at 1, 2 and 4 waves per tile

@@ -503,7 +503,7 @@ __global__ __launch_bounds__(kGT, 1) void k_solve_grp(CaseArgs a, const int* __r
     }
     if (a.o.B_drag && tid < 36) a.o.B_drag[(size_t)i * 36 + tid] = bd[c * 36 + tid];
     if (a.o.Bmat)
-      for (int e = tid; e < nn * 9; e += kGT) a.o.Bmat[(size_t)i * nn * 9 + e] = bm[c * nn * 9 + e];
+      for (int e = tid; e < nn * 9; e += kGT) a.o.Bmat[(size_t)i * a.bmat_nn * 9 + e] = bm[c * nn * 9 + e];
     if (a.o.Z) {   // final impedance fowt.Z (raft/raft_model.py:1013)
 #pragma unroll 1
       for (int j = 0; j < npass; ++j) {

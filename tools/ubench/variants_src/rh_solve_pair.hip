@@ -617,7 +617,7 @@ __global__ __launch_bounds__(LT, 4) void k_solve_pair(CaseArgs a) {
   }
   if (a.o.B_drag && tid < 36) a.o.B_drag[(size_t)ic * 36 + tid] = bd[tid];
   if (a.o.Bmat)
-    for (int e = tid; e < nn * 9; e += LT) a.o.Bmat[(size_t)ic * nn * 9 + e] = bm[e];
+    for (int e = tid; e < nn * 9; e += LT) a.o.Bmat[(size_t)ic * a.bmat_nn * 9 + e] = bm[e];
   if (a.o.Z && okb) {   // final impedance fowt.Z (raft/raft_model.py:1013) from the last B_drag
     const double w = lw[b], w2 = -(w * w);
     rh_c128* Zo = a.o.Z + ((size_t)ic * nw + b) * 36;
