@@ -29,7 +29,7 @@ C5_CHUNKS = 5         # C5 design blocks: block k+1 is prepared on the host whil
 PEAK_FP64 = 78.6e12   # MI355X FP64 dense peak (vector = matrix rate), FLOP/s
 # HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950
 # correction of MI355X_MICROARCH.md + WRITE_SIZE), written by tools/pmc_summary.py
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_v10", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_v2", "pmc_summary.json")
 
 
 def pmc_section(workload):
@@ -497,12 +497,13 @@ def bench_c4(device, steps, world, rank, dist, ncase=512):
                          "frac": achieved / PEAK_FP64, "traffic": pmc_traffic("c4", *solve_kernels(dd.nw)),
                          **hw_util("c4", solve_kernels(dd.nw), kern_ms),
                          "kernel": solve_kernel_name(dd.nw), "kernels_timed": list(solve_kernels(dd.nw)),
-                         "chain_traffic": pmc_traffic("c4", *solve_kernels(dd.nw), "rh::k_array_exc<2>",
+                         "chain_traffic": pmc_traffic("c4", *solve_kernels(dd.nw),
                                                       f"rh::k_array_resp<2, {str(dd.nw > 256).lower()}>"),
                          "kernel_ms": kern_ms, "flops_per_launch": flops,
                          "note": "the (case, FOWT) drag fixed point (kernels_timed); SURVEY.md §8(d) formula per "
                                  "(case, FOWT); traffic = HBM bytes of those launches, chain_traffic = of the whole "
-                                 "step (fixed point, excitation, block solve with the motion statistics) from "
+                                 "step (fixed point, which also writes the array excitation F_wave, and the block "
+                                 "solve with the motion statistics) from "
                                  + os.path.relpath(PMC_SUMMARY, ROOT)}}
 
 

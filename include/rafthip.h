@@ -156,6 +156,11 @@ typedef struct {
                              - tol (raft/raft_model.py:961-962) with the smallest |m|.  m < 0 means
                              that iteration passed.  |m| near rounding level marks a case whose
                              iteration count could flip between implementations. */
+  rh_c128* F_wave;        /* [ncase][6][nw] the wave excitation of sea state 0 with the final
+                             linearisation, zeta (F_iner + F_drag(Bmat)) (+ fext), or NULL: the
+                             F_wave of the coupled-array solve (raft/raft_model.py:1049-1061),
+                             formed by the fixed point itself, so rh_array_solve_stats needs no
+                             excitation launch */
 } rh_solve_out;
 
 const char* rh_last_error(void);
@@ -331,6 +336,15 @@ int rh_array_response_stats(rh_ctx* ctx, const rh_design* designs, int ndesign, 
                             const int* design_idx, const int* head, const double* zeta, const double* B_drag,
                             const double* Bmat, const double* K, rh_c128* Xi, double dw, double* psd, double* std_,
                             const int* order, rh_stream stream);
+
+/* The response step of rh_array_response_stats alone, with each FOWT's wave excitation already
+ * in Xi: Xi [ncase][6 nf][nw] holds F_wave on entry (rh_solve_out.F_wave of the (case, FOWT)
+ * fixed points, entries e = ic * nf + f, which is this layout) and the response on return;
+ * Z_f rebuilt from the design and B_drag [ncase * nf][36], Xi = (blockdiag(Z_f) + K)^-1 F, and
+ * the statistics as rh_array_response_stats writes them (psd / std may be NULL). */
+int rh_array_solve_stats(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf, int ncase, const int* design_idx,
+                         const double* B_drag, const double* K, rh_c128* Xi, double dw, double* psd, double* std_,
+                         rh_stream stream);
 
 /* ------------------------------------------------------------------------------------
  * Slender-body second-order QTF (FOWT.calcQTF_slenderBody, raft/raft_fowt.py:1385-1648)

@@ -201,7 +201,7 @@ extern "C" {
 
 const char* rh_last_error(void) { return g_err.c_str(); }
 
-int rh_version(void) { return 3; }
+int rh_version(void) { return 4; }
 
 // (rh_prof_read / rh_wgt_read of instrumented builds live in rh_solve_fast.hip, beside the counters)
 
@@ -746,6 +746,39 @@ int rh_array_response_stats(rh_ctx* ctx, const rh_design* designs, int ndesign, 
   } else {
     hipLaunchKernelGGL(rh::k_array_exc<2>, ge, dim3(rh::kArrExcThreads), lsm, s, a);
     RH_HIP(hipGetLastError());
+    if (multi) hipLaunchKernelGGL((rh::k_array_resp<2, true>), g, gr, 0, s, a);
+    else hipLaunchKernelGGL((rh::k_array_resp<2, false>), g, gr, 0, s, a);
+  }
+  RH_HIP(hipGetLastError());
+  return designs_used(ctx, s);
+}
+
+// The response step alone, with F already in Xi (rh_solve_out.F_wave of the fixed point): the
+// block solve and the statistics of k_array_resp, no excitation launch.
+int rh_array_solve_stats(rh_ctx* ctx, const rh_design* designs, int ndesign, int nf, int ncase, const int* design_idx,
+                         const double* B_drag, const double* K, rh_c128* Xi, double dw, double* psd, double* std_,
+                         rh_stream stream) {
+  if (!ctx || !designs || !design_idx || !B_drag || !Xi) return fail(RH_EINVAL, "rh_array_solve_stats: null argument");
+  if ((psd || std_) && !(dw > 0)) return fail(RH_EINVAL, "rh_array_solve_stats: dw=%g", dw);
+  if (nf < 1 || nf > 2) return fail(RH_EINVAL, "rh_array_solve_stats: nf=%d (supported: 1, 2)", nf);
+  if (ncase <= 0) return ncase == 0 ? RH_OK : fail(RH_EINVAL, "rh_array_solve_stats: ncase=%d", ncase);
+  if (ndesign < 1) return fail(RH_EINVAL, "rh_array_solve_stats: ndesign=%d", ndesign);
+  const int nw = designs[0].nw;
+  for (int i = 0; i < ndesign; ++i) {
+    if (int r = check_design(designs[i], false)) return r;
+    if (designs[i].nw != nw) return fail(RH_EINVAL, "rh_array_solve_stats: all designs must share nw");
+  }
+  RH_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
+  rh::ArrayArgs a{staged_designs(ctx), ncase, design_idx, nullptr, nullptr, B_drag, nullptr, K, Xi, 0, 0, dw, psd, std_,
+                  nullptr};
+  const dim3 g(ncase), gr(rh::kArrRespThreads);
+  const bool multi = nw > rh::kArrRespThreads;
+  if (nf == 1) {
+    if (multi) hipLaunchKernelGGL((rh::k_array_resp<1, true>), g, gr, 0, s, a);
+    else hipLaunchKernelGGL((rh::k_array_resp<1, false>), g, gr, 0, s, a);
+  } else {
     if (multi) hipLaunchKernelGGL((rh::k_array_resp<2, true>), g, gr, 0, s, a);
     else hipLaunchKernelGGL((rh::k_array_resp<2, false>), g, gr, 0, s, a);
   }

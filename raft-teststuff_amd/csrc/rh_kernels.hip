@@ -460,6 +460,26 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
   if (a.o.B_drag && tid < 36) a.o.B_drag[(size_t)ic * 36 + tid] = bd[tid];
   if (a.o.Bmat)
     for (int e = tid; e < nn * 9; e += kThreads) a.o.Bmat[(size_t)ic * a.bmat_nn * 9 + e] = bm[e];
+  if (a.o.F_wave) {   // the excitation with the final linearisation (the arithmetic of phase C)
+#pragma unroll 1
+    for (int j = 0; j < NB; ++j) {
+      const int b = tid + kThreads * j;
+      if (b >= nw) continue;
+      double zj = zt[0];   // (a select chain, as in phase C: no dynamic register index)
+#pragma unroll
+      for (int jj = 1; jj < NB; ++jj) zj = j == jj ? zt[jj] : zj;
+      cd F[6];
+      drag_exc_members(d, al, Kp, nw, b, F);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        cd f = add(scl(ld(Fe + c * nw + b), zj), scl(F[c], zj));
+        if (a.c.fext) f = add(f, ld(a.c.fext + ((size_t)ic * 6 + c) * nw + b));
+        F[c] = f;
+      }
+#pragma unroll
+      for (int c = 0; c < 6; ++c) st(a.o.F_wave + ((size_t)ic * 6 + c) * nw + b, F[c]);
+    }
+  }
   // a case that stopped on a NaN or a singular Z has no response (the reference raises there,
   // raft/raft_model.py:957): NaN Xi, PSD, RAO and std, as k_solve_lds writes them
   if (status == RH_CASE_NAN || status == RH_CASE_SINGULAR) {   // uniform

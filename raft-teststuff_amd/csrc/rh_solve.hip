@@ -356,6 +356,87 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   PROF_T(tp1);
   PROF_ADD(0, tp1 - tp0);
 
+  // The excitation of bin j of this thread with the current node coefficients (al, written by
+  // phase B), member-factored (drag_exc_members' arithmetic):
+  //   f_n = Bmat_n uhat_n = aq q Kq + a1 p1 K1 + a2 p2 K2,  r_n x f_n = rA x f_n + t q x f_n
+  // with q x p1 = p2, q x p2 = -p1 (raft/raft_fowt.py:1255-1259, 1283-1289), then
+  // F = zeta (F_iner + F_drag) (+ fext), phase C of every iteration.
+  auto excite = [&](int j, cd (&F)[6]) {
+    const int bj = tid + LT * j;
+    const unsigned vj = voff(bj);
+    const bool okj = bj < nw;
+    cd fe[6];   // unit inertial excitation of this bin, in flight during the node loop
+#pragma unroll
+    for (int c = 0; c < 6; ++c) fe[c] = bld(bFe, vj, c * nw16);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
+    {
+      cd SQ = mk(0, 0), S1 = mk(0, 0), S2 = mk(0, 0), T1 = mk(0, 0), T2 = mk(0, 0);
+      auto load1 = [&](cd (&K)[3], int n) {
+        const unsigned so = (unsigned)(n < nn ? n : nn - 1) * 3u * nw16;
+#if RH_ABL_C_NOLOAD
+        if (n >= kRingC) return;
+#endif
+#pragma unroll
+        for (int p = 0; p < 3; ++p) K[p] = bld(bK, vj, so + (unsigned)p * nw16);
+      };
+      int m = 0, mnext = nn > 0 ? mstart[1] : 0;
+      auto fold = [&]() {   // close member m: F += sum of its nodes (as drag_exc_members)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const double cq = mbf[18 * m + RH_MF_CQ0 + i], c1 = mbf[18 * m + RH_MF_C10 + i],
+                       c2 = mbf[18 * m + RH_MF_C20 + i];
+          F[i] = add(F[i], add(add(scl(SQ, cq), scl(S1, c1)), scl(S2, c2)));
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const double p1 = mbf[18 * m + RH_MF_C10 + i], p2 = mbf[18 * m + RH_MF_C20 + i];
+          F[3 + i] = add(F[3 + i], sub(scl(T1, p2), scl(T2, p1)));
+        }
+        SQ = S1 = S2 = T1 = T2 = mk(0, 0);
+      };
+      auto step = [&](cd (&K)[3], int n) {
+        while (n == mnext) {   // uniform: member m ended before node n
+          fold();
+          ++m;
+          mnext = mstart[m + 1];
+        }
+        const double* A = al + 6 * n;
+        const double A0 = A[0], A1 = A[1], A2 = A[2], A3 = A[3], A4 = A[4];
+#if RH_ABL_C_NOCOMP
+        SQ = add(SQ, K[0]); S1 = add(S1, K[1]); S2 = add(S2, K[2]);
+        load1(K, n + kRingC);
+        return;
+#endif
+        SQ = add(SQ, scl(K[0], A0));
+        S1 = add(S1, scl(K[1], A1));
+        S2 = add(S2, scl(K[2], A2));
+        T1 = add(T1, scl(K[1], A3));
+        T2 = add(T2, scl(K[2], A4));
+        load1(K, n + kRingC);
+      };
+      cd K[kRingC][3];
+#pragma unroll
+      for (int r = 0; r < kRingC; ++r) load1(K[r], r);
+      for (int n = 0; n < nn; n += kRingC) {
+#pragma unroll
+        for (int r = 0; r < kRingC; ++r)
+          if (n + r < nn) step(K[r], n + r);
+      }
+      if (nn > 0) fold();
+    }
+    const double z = lz[bj];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) F[c] = add(scl(fe[c], z), scl(F[c], z));   // F_lin + F_drag
+    if (has_fx) {
+      cd fx[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) fx[c] = bld(bFx, vj, c * nw16);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) F[c] = add(F[c], mk(okj ? fx[c].r : 0.0, okj ? fx[c].i : 0.0));
+    }
+  };
+
   for (int it = it0; it < itend; ++it) {
     PROF_T(ta0);
     PROF_ADD(7, 1);
@@ -607,7 +688,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
 #endif
     // ---------------- C: excitation, Z(w), LU solve, convergence flags ------------------
     bool my_ok = true, my_nan = false, my_sing = false;
-    double my_tmax = 0.0;
+    double tN = 0.0, tD = 1.0;   // the lane's largest tolCheck so far as tt^2 = tN / tD
     // the last allowed iteration stores every entry of the unrelaxed iterate (uniform)
     const bool last_it = __builtin_amdgcn_readfirstlane(it + 1 == nloop ? 1 : 0) != 0;
 #pragma unroll 1
@@ -617,70 +698,14 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       const int bj = tid + LT * j;
       const unsigned vj = voff(bj);
       const bool okj = bj < nw;
-      // drag excitation of bin j before the zeta factor, member-factored:
-      //   f_n = Bmat_n uhat_n = aq q Kq + a1 p1 K1 + a2 p2 K2,  r_n x f_n = rA x f_n + t q x f_n
-      // with q x p1 = p2, q x p2 = -p1 (raft/raft_fowt.py:1255-1259, 1283-1289).
       PROF_T(tc0);
-      cd fe[6];   // unit inertial excitation of this bin, in flight during the node loop
-#pragma unroll
-      for (int c = 0; c < 6; ++c) fe[c] = bld(bFe, vj, c * nw16);
       cd F[6];
+      excite(j, F);
+      // F_wave: every iteration's excitation overwrites the last one's, so the kernel leaves
+      // the final linearisation's (one 16-B streamed store per entry; F is live for the LU anyway)
+      if (a.o.F_wave && okj) {
 #pragma unroll
-      for (int c = 0; c < 6; ++c) F[c] = mk(0, 0);
-      {
-        cd SQ = mk(0, 0), S1 = mk(0, 0), S2 = mk(0, 0), T1 = mk(0, 0), T2 = mk(0, 0);
-        auto load1 = [&](cd (&K)[3], int n) {
-          const unsigned so = (unsigned)(n < nn ? n : nn - 1) * 3u * nw16;
-#if RH_ABL_C_NOLOAD
-          if (n >= kRingC) return;
-#endif
-#pragma unroll
-          for (int p = 0; p < 3; ++p) K[p] = bld(bK, vj, so + (unsigned)p * nw16);
-        };
-        int m = 0, mnext = nn > 0 ? mstart[1] : 0;
-        auto fold = [&]() {   // close member m: F += sum of its nodes (as drag_exc_members)
-#pragma unroll
-          for (int i = 0; i < 6; ++i) {
-            const double cq = mbf[18 * m + RH_MF_CQ0 + i], c1 = mbf[18 * m + RH_MF_C10 + i],
-                         c2 = mbf[18 * m + RH_MF_C20 + i];
-            F[i] = add(F[i], add(add(scl(SQ, cq), scl(S1, c1)), scl(S2, c2)));
-          }
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            const double p1 = mbf[18 * m + RH_MF_C10 + i], p2 = mbf[18 * m + RH_MF_C20 + i];
-            F[3 + i] = add(F[3 + i], sub(scl(T1, p2), scl(T2, p1)));
-          }
-          SQ = S1 = S2 = T1 = T2 = mk(0, 0);
-        };
-        auto step = [&](cd (&K)[3], int n) {
-          while (n == mnext) {   // uniform: member m ended before node n
-            fold();
-            ++m;
-            mnext = mstart[m + 1];
-          }
-          const double* A = al + 6 * n;
-          const double A0 = A[0], A1 = A[1], A2 = A[2], A3 = A[3], A4 = A[4];
-#if RH_ABL_C_NOCOMP
-          SQ = add(SQ, K[0]); S1 = add(S1, K[1]); S2 = add(S2, K[2]);
-          load1(K, n + kRingC);
-          return;
-#endif
-          SQ = add(SQ, scl(K[0], A0));
-          S1 = add(S1, scl(K[1], A1));
-          S2 = add(S2, scl(K[2], A2));
-          T1 = add(T1, scl(K[1], A3));
-          T2 = add(T2, scl(K[2], A4));
-          load1(K, n + kRingC);
-        };
-        cd K[kRingC][3];
-#pragma unroll
-        for (int r = 0; r < kRingC; ++r) load1(K[r], r);
-        for (int n = 0; n < nn; n += kRingC) {
-#pragma unroll
-          for (int r = 0; r < kRingC; ++r)
-            if (n + r < nn) step(K[r], n + r);
-        }
-        if (nn > 0) fold();
+        for (int c = 0; c < 6; ++c) st_nt(a.o.F_wave + c6 + c * nw + bj, F[c]);
       }
       PROF_T(tc1);
 #ifdef RH_PROF
@@ -696,17 +721,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       if (!__builtin_amdgcn_ballot_w64(okj)) continue;
 #endif
       const int b = tid + LT * j;
-      const unsigned v = vj;
-      const double w = lw[b], z = lz[b];
-#pragma unroll
-      for (int c = 0; c < 6; ++c) F[c] = add(scl(fe[c], z), scl(F[c], z));   // F_lin + F_drag
-      if (has_fx) {
-        cd fx[6];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) fx[c] = bld(bFx, v, c * nw16);
-#pragma unroll
-        for (int c = 0; c < 6; ++c) F[c] = add(F[c], mk(okj ? fx[c].r : 0.0, okj ? fx[c].i : 0.0));
-      }
+      const double w = lw[b];
       cd Z[6][6];
       {
         // index the LDS image with a zero the compiler cannot see through, so that its 144
@@ -751,14 +766,21 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
         my_nan |= okj && ((x.r != x.r) || (x.i != x.i));
         // tolCheck = |Xi - XiLast| / (|Xi| + tol) < tol  (raft/raft_model.py:961-962)
         // (magnitudes as sqrt(re^2 + im^2): within an ulp of np.abs's hypot, far cheaper)
-        const double tt = sqrt(abs2(sub(x, xlast))) / (sqrt(abs2(x)) + tol);
-        my_ok = my_ok && (!okj || tt < tol);
-        my_tmax = okj ? fmax(my_tmax, tt) : my_tmax;
+        // tt < tol as |Xi - XiLast|^2 < (tol (|Xi| + tol))^2: one square root, no division per
+        // entry; the lane keeps its largest tt^2 as a fraction (compared by cross products) and
+        // forms tt itself only for the convergence margin, once per iteration
+        const double n2 = abs2(sub(x, xlast)), den = sqrt(abs2(x)) + tol, d2 = den * den;
+        const double td = tol * den;
+        my_ok = my_ok && (!okj || n2 < td * td);
+        const bool gt = okj && n2 * tD > tN * d2;
+        tN = gt ? n2 : tN;
+        tD = gt ? d2 : tD;
+        const bool pass = n2 < td * td;
         // The unrelaxed iterate leaves the kernel only as the output of the case's final
         // iteration: the one whose test every (bin, DOF) passed, or the last allowed one
         // (raft/raft_model.py:996-1000).  So an entry is stored only when it passed its own test
         // or the loop is at its last iteration; the others are never read.
-        if (okj && (GX || Xo) && (tt < tol || last_it)) {   // stores only (Xi may be NULL with NP == 1)
+        if (okj && (GX || Xo) && (pass || last_it)) {   // stores only (Xi may be NULL with NP == 1)
           st_nt(Xo + c * nw + b, x);   // streamed: only the last iteration's value is kept
         }
         if (okj && XP) st(XP + c * nw + b, xlast);
@@ -778,6 +800,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     PROF_ADD(4, tc_sol);
     PROF_T(ta3);
     if (a.o.margin) {
+      const double my_tmax = sqrt(tN) / sqrt(tD);
       const double mw = wave_max(my_tmax);
       if (lane == 0) mred[wv] = mw;
     }
@@ -883,11 +906,13 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   // entries of its last iterate were stored only where they passed their test.)
   const bool failed = status == RH_CASE_NAN || status == RH_CASE_SINGULAR;   // uniform
   double ss[6] = {0, 0, 0, 0, 0, 0};
+  const double hdw = 0.5 / d.dw;   // psd = |x|^2 hdw and rao = x (1 / zeta): multiplies, not 36 divisions per thread
 #pragma unroll
   for (int j = 0; j < NBT; ++j) {
     const int b = tid + LT * j;
     if (b >= nw || !Xo) continue;   // (psd, std and rao need Xi: checked by the caller)
     const double z = lz[b];
+    const double rz = fabs(z) > 1e-6 ? 1.0 / z : 0.0;
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
       cd x;
@@ -900,8 +925,8 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       const cd xd = c >= 3 ? scl(x, kRad2Deg) : x;
       const double m2 = abs2(xd);
       ss[c] += m2;
-      if (a.o.psd) a.o.psd[((size_t)ic * 6 + c) * nw + b] = 0.5 * m2 / d.dw;
-      if (a.o.rao) st(a.o.rao + ((size_t)ic * 6 + c) * nw + b, failed ? x : fabs(z) > 1e-6 ? cd{x.r / z, x.i / z} : mk(0, 0));
+      if (a.o.psd) a.o.psd[((size_t)ic * 6 + c) * nw + b] = m2 * hdw;
+      if (a.o.rao) st(a.o.rao + ((size_t)ic * 6 + c) * nw + b, failed ? x : scl(x, rz));
     }
   }
   if (a.o.std) {

@@ -47,7 +47,8 @@ class RhCases(ctypes.Structure):
 
 class RhSolveOut(ctypes.Structure):
     _fields_ = [("Xi", _p), ("Xi_last", _p), ("iters", _p), ("status", _p), ("zeta", _p), ("B_drag", _p),
-                ("Bmat", _p), ("psd", _p), ("std", _p), ("rao", _p), ("Z", _p), ("Xi_prev", _p), ("margin", _p)]
+                ("Bmat", _p), ("psd", _p), ("std", _p), ("rao", _p), ("Z", _p), ("Xi_prev", _p), ("margin", _p),
+                ("F_wave", _p)]
 
 
 class RhQtfDesign(ctypes.Structure):
@@ -103,6 +104,8 @@ def lib():
                                       _p, _p, _p, _p, _p, _p],
                 "rh_array_response_stats": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             _p, _p, _p, _p, _p, _p, _p, ctypes.c_double, _p, _p, _p, _p],
+                "rh_array_solve_stats": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.c_int, ctypes.c_int, _p, _p,
+                                         _p, _p, ctypes.c_double, _p, _p, _p],
                 "rh_wave_excitation": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.c_int, _p, _p, _p, _p, _p,
                                        _p],
                 "rh_channel_stats": [_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, _p,

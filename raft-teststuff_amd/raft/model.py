@@ -648,22 +648,25 @@ class Model:
         P = prepared if prepared is not None else self.prepareArrayBatch(cases)
         nf, n, nw = self.nFOWT, P["n"], self.nw
         dds, cs, prep, dev = P["dds"], P["cs"], P["prep"], P["dev"]
+        # X first holds each (case, FOWT)'s F_wave, written by its fixed point with the final
+        # linearisation ([n, 6 nf, nw] is the [n nf, 6, nw] layout of the fixed point's entries),
+        # then the coupled response (rh_array_solve_stats)
+        X = torch.empty([n, 6 * nf, nw], dtype=torch.complex128, device=dev)
         if marks:
             marks[0].record(torch.cuda.current_stream(dev))
-        res = solve_batch(dds, cs, self.nIter, self.XiStart, tol, want=("zeta", "Bmat", "B_drag", "noXi"), prepared=prep)
+        res = solve_batch(dds, cs, self.nIter, self.XiStart, tol, want=("zeta", "Bmat", "B_drag", "noXi"), prepared=prep,
+                          F_wave=X.view(n * nf, 6, nw))
         if marks:
             marks[1].record(torch.cuda.current_stream(dev))
         arr = P["arr"]
         s = N.stream_handle(torch, dev)
         ctx = N.context(self.device)
         K = P["K"]
-        X = torch.empty([n, 6 * nf, nw], dtype=torch.complex128, device=dev)
         psd = torch.empty([n * nf, 6, nw], dtype=torch.float64, device=dev)
         std = torch.empty([n * nf, 6], dtype=torch.float64, device=dev)
-        N.check(N.lib().rh_array_response_stats(ctx, arr, nf, nf, n, N.ptr(prep["design"]), N.ptr(prep["head"]),
-                                                N.ptr(res["zeta"]), N.ptr(res["B_drag"]), N.ptr(res["Bmat"]),
-                                                N.ptr(K), N.ptr(X), float(self.fowtList[0].dw), N.ptr(psd),
-                                                N.ptr(std), N.ptr(prep["order"]), s), "rh_array_response_stats")
+        N.check(N.lib().rh_array_solve_stats(ctx, arr, nf, nf, n, N.ptr(prep["design"]), N.ptr(res["B_drag"]), N.ptr(K),
+                                             N.ptr(X), float(self.fowtList[0].dw), N.ptr(psd), N.ptr(std), s),
+                "rh_array_solve_stats")
         out = {"Xi": X, "iters": res["iters"].view(n, nf), "status": res["status"].view(n, nf),
                "psd": psd.view(n, nf, 6, nw), "std": std.view(n, nf, 6), "zeta": res["zeta"].view(n, nf, nw)[:, 0]}
         out["_keep"] = (res, arr, K)

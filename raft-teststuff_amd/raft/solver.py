@@ -50,14 +50,16 @@ class BatchResult(dict):
 
 
 def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std", "zeta", "B_drag"),
-                fext=None, stream=None, prepared=None, Xi_init=None, first_iter=0):
+                fext=None, stream=None, prepared=None, Xi_init=None, first_iter=0, F_wave=None):
     """Run rh_solve_cases.  `designs`: list of DeviceDesign (same nw); `cases`: CaseSet.
     Returns a BatchResult of device tensors (stream-ordered; caller synchronises).
     want may include "Xi_prev" (the un-relaxed XiLast of the final iteration), "margin"
     (the closest call of the convergence test per case, rh_solve_out.margin) and "noXi" (no
     response output: the linearisation only, for callers that form the response themselves,
     Model.analyzeArrayBatch; then no psd / std / rao either); Xi_init /
-    first_iter restart a fixed point from such a state (potSecOrder=1 second pass)."""
+    first_iter restart a fixed point from such a state (potSecOrder=1 second pass).  F_wave: a
+    contiguous complex128 [ncase, 6, nw] tensor that receives each case's wave excitation with
+    its final linearisation (rh_solve_out.F_wave; the F of an array solve, Model.analyzeArrayBatch)."""
     d0 = designs[0]
     torch = d0.torch
     dev = d0.device
@@ -94,7 +96,7 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
         out["Xi_prev"] = torch.empty([ncase, 6, nw], **c128)
     if "margin" in want:
         out["margin"] = torch.empty([ncase], **f64)
-    for t, shape in ((fext, [ncase, 6, nw]), (Xi_init, [ncase, 6, nw])):
+    for t, shape in ((fext, [ncase, 6, nw]), (Xi_init, [ncase, 6, nw]), (F_wave, [ncase, 6, nw])):
         if t is not None and (list(t.shape) != shape or t.dtype != torch.complex128 or not t.is_contiguous()):
             raise ValueError(f"expected a contiguous complex128 tensor of shape {shape}")
     cs = N.RhCases()
@@ -110,11 +112,12 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     o.Xi, o.Xi_last, o.iters, o.status = N.ptr(out.get("Xi")), N.ptr(xl), N.ptr(out["iters"]), N.ptr(out["status"])
     for k in ["zeta", "B_drag", "Bmat", "psd", "std", "rao", "Z", "Xi_prev", "margin"]:
         setattr(o, k, N.ptr(out.get(k)))
+    o.F_wave = N.ptr(F_wave)
     arr = (N.RhDesign * len(designs))(*[d.struct() for d in designs])
     s = stream if stream is not None else N.stream_handle(torch, dev)
     N.check(N.lib().rh_solve_cases(N.context(d0.dev_index), arr, len(designs), ctypes.byref(cs), ctypes.byref(o), s),
             "rh_solve_cases")
-    out._keep = (xl, prep, arr, fext, Xi_init)
+    out._keep = (xl, prep, arr, fext, Xi_init, F_wave)
     return out
 
 
