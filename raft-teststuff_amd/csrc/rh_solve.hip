@@ -22,7 +22,7 @@ namespace rh {
 #ifdef RH_PROF
 // Phase cycle counters (s_memtime of wave 0 of every workgroup), summed over workgroups:
 // [0] prologue [1] A [2] B [3] C excitation [4] C solve [5] flags [6] epilogue [7] iterations
-static __device__ unsigned long long rh_prof[8];   // static: one per translation unit (rh_prof_read reads rh_solve_fast.hip's)
+static __device__ unsigned long long rh_prof[12];   // static: one per translation unit (rh_prof_read reads rh_solve_fast.hip's)
 #define PROF_T(v) const unsigned long long v = clock64()
 #define PROF_ADD(i, x) if (tid == 0) atomicAdd(&rh_prof[i], (unsigned long long)(x))
 #else
@@ -42,6 +42,9 @@ constexpr int kRingA = 3;         // wave-table prefetch depth (nodes) of phase 
 constexpr int kRingC = 6;         // ... of phase C (one bin per pass: less work per node)
 #ifndef RH_ONE_VOTE
 #define RH_ONE_VOTE 0                 // 1: one barrier (LDS flag word) for the three end-of-iteration votes
+#endif
+#ifndef RH_XI_STORE
+#define RH_XI_STORE 1                 // 0: per-entry stores of passing entries; 1: while the iteration may be final; 2: traffic floor (A/B)
 #endif
 #ifndef RH_A_BATCH
 #define RH_A_BATCH 0                  // > 0: phase-A nodes in batches of RH_A_BATCH, one tbfly16 per batch
@@ -277,12 +280,13 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   double* lz = lw + NP * NWP;                      // [NP NWP] zeta per bin (pad bins: 0)
   double* mred = lz + NP * NWP;                    // [LW] per-wave max of tolCheck
   int* mstart = reinterpret_cast<int*>(mred + LW);  // [nm+1]
-  int* sflag = mstart + nm + 1;                      // [2] vote words of even / odd iterations
+  int* sflag = mstart + nm + 1;                      // [2] vote words of even / odd iterations,
+                                                     // [2]: it + 1 once a test of iteration it failed
   load_mbc(d, mbc, tid);
   for (int n = tid; n < nn; n += LT) nt[n] = node[RH_NF_T * nn + n];
   for (int e = tid; e < 18 * nm; e += LT) mbf[e] = d.memb[(e % 18) * nm + e / 18];   // RH_MF_CQ0..C20: fields 0..17
   for (int e = tid; e <= nm; e += LT) mstart[e] = d.mstart[e];
-  if (tid < 2) sflag[tid] = 0;
+  if (tid < 3) sflag[tid] = 0;
   const int it0 = resume ? stop_iter : a.c.first_iter;
   // Iteration 0's phase-A sums formed for the whole batch by k_a0_sums (rh_a0.hip): their
   // chunk sums (in chunk order) take the place of wave 0's partials and the other waves' are 0,
@@ -684,13 +688,26 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     PROF_T(ta2);
     PROF_ADD(2, ta2 - ta0 - (ta1 - ta0));
 #ifdef RH_PROF
-    unsigned long long tc_exc = 0, tc_sol = 0;
+    unsigned long long tc_exc = 0, tc_sol = 0, tc_z = 0, tc_lu = 0;
 #endif
     // ---------------- C: excitation, Z(w), LU solve, convergence flags ------------------
     bool my_ok = true, my_nan = false, my_sing = false;
     double tN = 0.0, tD = 1.0;   // the lane's largest tolCheck so far as tt^2 = tN / tD
     // the last allowed iteration stores every entry of the unrelaxed iterate (uniform)
     const bool last_it = __builtin_amdgcn_readfirstlane(it + 1 == nloop ? 1 : 0) != 0;
+    // The outputs of the final iteration (Xi, F_wave) are stored by every iteration that may be
+    // the final one: the last allowed, or one whose tests have all passed so far.  A wave that
+    // sees a failed test (any lane, this bin or an earlier one) marks the iteration in LDS
+    // (sflag[2]); the other waves read the mark at their next store (a stale read only stores
+    // more).  (uniform)
+    auto may_be_final = [&]() -> bool {
+      if (last_it) return true;
+      if (__builtin_amdgcn_ballot_w64(!my_ok)) {
+        if (lane == 0) __hip_atomic_store(&sflag[2], it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return false;
+      }
+      return __builtin_amdgcn_readfirstlane(__hip_atomic_load(&sflag[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != it + 1;
+    };
 #pragma unroll 1
     for (int j = 0; j < NBT; ++j) {
       // per-bin scalars picked without dynamic register indexing (the loop is not unrolled,
@@ -701,11 +718,13 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       PROF_T(tc0);
       cd F[6];
       excite(j, F);
-      // F_wave: every iteration's excitation overwrites the last one's, so the kernel leaves
-      // the final linearisation's (one 16-B streamed store per entry; F is live for the LU anyway)
-      if (a.o.F_wave && okj) {
+      // F_wave: the excitation of the final iteration, which every iteration's overwrites (F is
+      // live for the LU anyway), skipped once the iteration is known not to be final (below)
+      if (a.o.F_wave && may_be_final()) {
+        if (okj) {
 #pragma unroll
-        for (int c = 0; c < 6; ++c) st_nt(a.o.F_wave + c6 + c * nw + bj, F[c]);
+          for (int c = 0; c < 6; ++c) st_nt(a.o.F_wave + c6 + c * nw + bj, F[c]);
+        }
       }
       PROF_T(tc1);
 #ifdef RH_PROF
@@ -751,8 +770,15 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
           }
         }
       }
+#ifdef RH_PROF
+      const unsigned long long tcz = clock64();
+      tc_z += tcz - tc1;
+#endif
       const bool ok_lu = lu_solve<6>(Z, F);
       my_sing |= okj && !ok_lu;
+#ifdef RH_PROF
+      tc_lu += clock64() - tcz;
+#endif
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
         const cd x = F[c];
@@ -775,14 +801,13 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
         const bool gt = okj && n2 * tD > tN * d2;
         tN = gt ? n2 : tN;
         tD = gt ? d2 : tD;
-        const bool pass = n2 < td * td;
-        // The unrelaxed iterate leaves the kernel only as the output of the case's final
-        // iteration: the one whose test every (bin, DOF) passed, or the last allowed one
-        // (raft/raft_model.py:996-1000).  So an entry is stored only when it passed its own test
-        // or the loop is at its last iteration; the others are never read.
-        if (okj && (GX || Xo) && (pass || last_it)) {   // stores only (Xi may be NULL with NP == 1)
-          st_nt(Xo + c * nw + b, x);   // streamed: only the last iteration's value is kept
-        }
+        [[maybe_unused]] const bool pass = n2 < td * td;
+#if RH_XI_STORE == 0
+        // (round 4: an entry stored whenever it passed its own test or at the last iteration)
+        if (okj && (GX || Xo) && (pass || last_it)) st_nt(Xo + c * nw + b, x);
+#elif RH_XI_STORE == 2
+        if (okj && (GX || Xo) && last_it) st_nt(Xo + c * nw + b, x);   // traffic floor (A/B only: wrong Xi)
+#endif
         if (okj && XP) st(XP + c * nw + b, xlast);
         // XiLast = 0.2 XiLast + 0.8 Xi  (:991), only consumed if not converged (pads: 0)
         const cd xr = add(scl(xlast, 0.2), scl(x, 0.8));
@@ -792,12 +817,27 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
           xl[c * NWP + b] = xr;
         }
       }
+#if RH_XI_STORE == 1
+      // The unrelaxed iterate leaves the kernel only as the output of the case's final
+      // iteration: the one whose test every (bin, DOF) passed, or the last allowed one
+      // (raft/raft_model.py:996-1000).  So the bin's six entries are stored only while this
+      // iteration may still be that one (may_be_final, with this bin's tests counted);
+      // streamed: the final iteration's stores are the ones kept.  (Xi may be NULL with NP == 1.)
+      if ((GX || Xo) && may_be_final()) {
+        if (okj) {
+#pragma unroll
+          for (int c = 0; c < 6; ++c) st_nt(Xo + c * nw + b, F[c]);
+        }
+      }
+#endif
 #ifdef RH_PROF
       tc_sol += clock64() - tc1;
 #endif
     }
     PROF_ADD(3, tc_exc);
     PROF_ADD(4, tc_sol);
+    PROF_ADD(8, tc_z);
+    PROF_ADD(9, tc_lu);
     PROF_T(ta3);
     if (a.o.margin) {
       const double my_tmax = sqrt(tN) / sqrt(tD);

@@ -41,9 +41,9 @@ hipError_t occupancy_solve_fast(int which, int* per_cu, int threads, size_t lsm)
 // which the fast kernels write.
 #ifdef RH_PROF
 extern "C" int rh_prof_read(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rh::rh_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -3;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rh::rh_prof), sizeof(unsigned long long) * 12) != hipSuccess) return -3;
   if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[12] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(rh::rh_prof), z, sizeof z) != hipSuccess) return -3;
   }
   return 0;

@@ -41,16 +41,17 @@ def main():
         ms = e0.elapsed_time(e1) / 10
         line = f"mode {mode}: {ms:8.3f} ms/launch  {nc / ms * 1e3:10.0f} cases/s"
         if hasattr(L, "rh_prof_read"):
-            buf = (ctypes.c_ulonglong * 8)()
+            buf = (ctypes.c_ulonglong * 12)()
             L.rh_prof_read(buf, 1)
             res = solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=want, prepared=prep)
             torch.cuda.synchronize()
             L.rh_prof_read(buf, 1)
             v = list(buf)
-            nwg = int(prep["ngroup"]) if mode == 0 else nc
+            nwg = int(prep["ngroup"]) or nc
             nit = max(v[7], 1)
-            names = ["prologue/WG", "A/it", "B/it", "Cexc/it", "Csolve/it", "flags/it", "epilogue/WG"]
-            per = [v[0] / nwg, v[1] / nit, v[2] / nit, v[3] / nit, v[4] / nit, v[5] / nit, v[6] / nwg]
+            names = ["prologue/WG", "A/it", "B/it", "Cexc/it", "Csolve/it", "(Z/it", "LU/it)", "flags/it", "epilogue/WG"]
+            per = [v[0] / nwg, v[1] / nit, v[2] / nit, v[3] / nit, v[4] / nit, v[8] / nit, v[9] / nit, v[5] / nit,
+                   v[6] / nwg]
             line += f"  WG-iterations {nit}  " + "  ".join(f"{n}={x:,.0f}" for n, x in zip(names, per))
         print(line, flush=True)
 
