@@ -43,6 +43,9 @@ constexpr int kRingC = 6;         // ... of phase C (one bin per pass: less work
 #ifndef RH_ONE_VOTE
 #define RH_ONE_VOTE 0                 // 1: one barrier (LDS flag word) for the three end-of-iteration votes
 #endif
+#ifndef RH_OVERLAP
+#define RH_OVERLAP 1                  // 1: no barrier vote between phase C and the next phase A (single-pass kernels)
+#endif
 #ifndef RH_XI_STORE
 #define RH_XI_STORE 1                 // 0: per-entry stores of passing entries; 1: while the iteration may be final; 2: traffic floor (A/B)
 #endif
@@ -214,7 +217,7 @@ __host__ __device__ inline size_t solve_lds_smem(int nn, int nm, int NB, int LT 
                            + (size_t)2 * LT * NB * NP   // w and zeta per (padded) bin
                            + 36 + 108 + LW * 6 + 36  // B_drag, M|B|C image, std partials, B_lin+B_drag
                            + LW)                     // convergence-margin partials
-         + sizeof(int) * ((size_t)nm + 4);            // member node ranges, vote words
+         + sizeof(int) * ((size_t)nm + 6);            // member node ranges, vote words, wave counters
 }
 
 // LT threads per case: 512 (8 waves), or 256 for nw <= 256 (two cases per CU; C4 has 240 bins),
@@ -261,6 +264,16 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   constexpr int NWP = LT * NB;                    // padded bins of one pass
   constexpr int NBT = NB * NP;                     // bins per thread over all passes
   constexpr bool GX = NP > 1;                      // XiLast in the Xi_last block, not in LDS
+#if RH_OVERLAP && !defined(RH_VARIANTS)
+  constexpr bool kOv = !GX;                        // the vote deferred into the next phase A (below)
+#else
+  constexpr bool kOv = false;                      // (variants: the two-pass launch stops mid-loop)
+#endif
+  auto wave_maxes = [&](const double* m) {         // max of the per-wave convergence-margin partials
+    double mx = m[0];
+    for (int w = 1; w < LW; ++w) mx = fmax(mx, m[w]);
+    return mx;
+  };
   cd* xl = reinterpret_cast<cd*>(smem);            // [6][NWP] (one pass only)
   rh_c128* XL = a.o.Xi_last + c6;                  // [6][nw] (GX)
   // The member factors and the node coefficients, read at every member change and node step of
@@ -281,12 +294,13 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   double* mred = lz + NP * NWP;                    // [LW] per-wave max of tolCheck
   int* mstart = reinterpret_cast<int*>(mred + LW);  // [nm+1]
   int* sflag = mstart + nm + 1;                      // [2] vote words of even / odd iterations,
-                                                     // [2]: it + 1 once a test of iteration it failed
+                                                     // [2]: it + 1 once a test of iteration it failed,
+                                                     // [3 + (it & 1)]: waves done with phase C of iteration it
   load_mbc(d, mbc, tid);
   for (int n = tid; n < nn; n += LT) nt[n] = node[RH_NF_T * nn + n];
   for (int e = tid; e < 18 * nm; e += LT) mbf[e] = d.memb[(e % 18) * nm + e / 18];   // RH_MF_CQ0..C20: fields 0..17
   for (int e = tid; e <= nm; e += LT) mstart[e] = d.mstart[e];
-  if (tid < 3) sflag[tid] = 0;
+  if (tid < 5) sflag[tid] = 0;
   const int it0 = resume ? stop_iter : a.c.first_iter;
   // Iteration 0's phase-A sums formed for the whole batch by k_a0_sums (rh_a0.hip): their
   // chunk sums (in chunk order) take the place of wave 0's partials and the other waves' are 0,
@@ -365,8 +379,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   //   f_n = Bmat_n uhat_n = aq q Kq + a1 p1 K1 + a2 p2 K2,  r_n x f_n = rA x f_n + t q x f_n
   // with q x p1 = p2, q x p2 = -p1 (raft/raft_fowt.py:1255-1259, 1283-1289), then
   // F = zeta (F_iner + F_drag) (+ fext), phase C of every iteration.
-  auto excite = [&](int j, cd (&F)[6]) {
-    const int bj = tid + LT * j;
+  auto excite = [&](int bj, cd (&F)[6]) {
     const unsigned vj = voff(bj);
     const bool okj = bj < nw;
     cd fe[6];   // unit inertial excitation of this bin, in flight during the node loop
@@ -611,6 +624,19 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     skip_a = false;
 #endif
     __syncthreads();
+    if constexpr (kOv) {
+      // the deferred vote of iteration it - 1 (every wave finished its phase C before this
+      // barrier; they came here because some test of it - 1 failed, so it did not converge)
+      if (it > it0) {
+        const int fl = sflag[(it - 1) & 1];
+        if (a.o.margin && tid == 0) margin = closer_call(margin, wave_maxes(mred) - tol);
+        if (fl & 6) {
+          status = (fl & 2) ? RH_CASE_NAN : RH_CASE_SINGULAR;
+          iters = it;
+          break;
+        }
+      }
+    }
     PROF_T(ta1);
     PROF_ADD(1, ta1 - ta0);
     // ---------------- B: node drag matrices and B_drag ----------------------------------
@@ -708,16 +734,22 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       }
       return __builtin_amdgcn_readfirstlane(__hip_atomic_load(&sflag[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != it + 1;
     };
+    if constexpr (kOv) {
+      // the words of iteration it + 1: their last readers (iteration it - 1's vote) are done
+      if (tid == 0) {
+        sflag[(it + 1) & 1] = 0;
+        sflag[3 + ((it + 1) & 1)] = 0;
+      }
+    }
 #pragma unroll 1
     for (int j = 0; j < NBT; ++j) {
       // per-bin scalars picked without dynamic register indexing (the loop is not unrolled,
       // so only one bin's LU is ever live)
       const int bj = tid + LT * j;
-      const unsigned vj = voff(bj);
       const bool okj = bj < nw;
       PROF_T(tc0);
       cd F[6];
-      excite(j, F);
+      excite(bj, F);
       // F_wave: the excitation of the final iteration, which every iteration's overwrites (F is
       // live for the LU anyway), skipped once the iteration is known not to be final (below)
       if (a.o.F_wave && may_be_final()) {
@@ -739,7 +771,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       // clamped last bin with a zero right-hand side (zeta = 0, x = 0 exactly) and store nothing.
       if (!__builtin_amdgcn_ballot_w64(okj)) continue;
 #endif
-      const int b = tid + LT * j;
+      const int b = bj;
       const double w = lw[b];
       cd Z[6][6];
       {
@@ -844,6 +876,53 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       const double mw = wave_max(my_tmax);
       if (lane == 0) mred[wv] = mw;
     }
+    if constexpr (kOv) {
+      // No barrier here.  Each wave ORs its flag bits (1 = a bin not converged, 2 = NaN,
+      // 4 = singular) into this iteration's word and counts itself done (release: the bits, the
+      // mark and mred first).  A wave that knows the loop goes on (one of its own tests failed,
+      // or another wave's mark) starts the next phase A at once, overlapping the waves still in
+      // phase C: phase A reads only the XiLast entries this very thread wrote, and writes only
+      // the node partials, which phase B consumed before this iteration's phase C.  The vote is
+      // then read after the next phase-A barrier (above).  Otherwise the wave waits for every
+      // wave to be done or for a mark, whichever comes first; with all done and no mark the
+      // iteration is the final one, the same verdict for every wave (a mark is written before
+      // its wave's done count).  The last allowed iteration always waits for all.
+      const bool last = it + 1 == nloop;
+      const unsigned long long bn = __builtin_amdgcn_ballot_w64(!my_ok), bx = __builtin_amdgcn_ballot_w64(my_nan),
+                               bs = __builtin_amdgcn_ballot_w64(my_sing);
+      const int bits = (bn ? 1 : 0) | (bx ? 2 : 0) | (bs ? 4 : 0);
+      if (lane == 0) {
+        if (bits) __hip_atomic_fetch_or(&sflag[it & 1], bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (bn) __hip_atomic_store(&sflag[2], it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&sflag[3 + (it & 1)], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      bool go_on = !last && bn != 0;
+      if (!go_on) {
+#pragma unroll 1
+        while (true) {
+          const int dn = __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(&sflag[3 + (it & 1)], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+          const int mk = __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(&sflag[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          if (!last && mk == it + 1) {
+            go_on = true;
+            break;
+          }
+          if (dn == LW) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      PROF_T(ta4);
+      PROF_ADD(5, ta4 - ta3);
+      if (go_on) continue;
+      // the final iteration: every wave is done and no test failed (or it was the last allowed)
+      const int fl = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(&sflag[it & 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (a.o.margin && tid == 0) margin = closer_call(margin, wave_maxes(mred) - tol);
+      status = (fl & 2) ? RH_CASE_NAN : (fl & 4) ? RH_CASE_SINGULAR : (fl & 1) ? RH_CASE_NOT_CONVERGED : RH_CASE_CONVERGED;
+      iters = it + 1;
+      break;
+    } else {
 #if RH_ONE_VOTE
     // One barrier for the three votes: each wave ORs its flag bits (1 = a bin not converged,
     // 2 = NaN, 4 = singular) into this iteration's LDS word; tid 0 clears the other word for
@@ -890,6 +969,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       status = RH_CASE_CONVERGED;
       iters = it + 1;
       break;
+    }
     }
   }
 
