@@ -38,8 +38,14 @@ static __device__ unsigned long long rh_wgt[2 * 8192];
 
 constexpr int kLT = 512;          // threads per case workgroup
 constexpr int kLW = kLT / 64;     // waves per case workgroup
-constexpr int kRingA = 3;         // wave-table prefetch depth (nodes) of phase A
-constexpr int kRingC = 6;         // ... of phase C (one bin per pass: less work per node)
+#ifndef RH_RING_A
+#define RH_RING_A 4               // (3 in the two-pass kernel: 4 moves its spills into the streaming loops)
+#endif
+#ifndef RH_RING_C
+#define RH_RING_C 6
+#endif
+constexpr int kRingA1 = RH_RING_A; // wave-table prefetch depth (nodes) of phase A
+constexpr int kRingC = RH_RING_C; // ... of phase C (one bin per pass: less work per node)
 #ifndef RH_ONE_VOTE
 #define RH_ONE_VOTE 0                 // 1: one barrier (LDS flag word) for the three end-of-iteration votes
 #endif
@@ -264,6 +270,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   constexpr int NWP = LT * NB;                    // padded bins of one pass
   constexpr int NBT = NB * NP;                     // bins per thread over all passes
   constexpr bool GX = NP > 1;                      // XiLast in the Xi_last block, not in LDS
+  constexpr int kRingA = GX ? 3 : kRingA1;
 #if RH_OVERLAP && !defined(RH_VARIANTS)
   constexpr bool kOv = !GX;                        // the vote deferred into the next phase A (below)
 #else

@@ -140,8 +140,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--asm")
     ap.add_argument("--out")
+    ap.add_argument("-D", action="append", default=[], help="extra preprocessor define (A/B variants)")
     args = ap.parse_args()
-    path = args.asm or compile_asm()
+    path = args.asm or compile_asm(["-D" + d for d in args.D])
     with open(path) as fh:
         ks = kernels(fh.read().split("\n"))
     rows, fails = [], []
