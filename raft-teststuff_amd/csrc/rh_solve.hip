@@ -491,7 +491,11 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
           }
         }
       }
+      // (defined here, not just before their first use: left undefined, the register allocator
+      // may keep the previous iteration's values live, and spill them, across phase C)
       cd Bq[NB], B1[NB], B2[NB], E1[NB], E2[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) Bq[j] = B1[j] = B2[j] = E1[j] = E2[j] = mk(0.0, 0.0);
       auto member_terms = [&](int m) {
         double cq[6], c1[6], c2[6];
 #pragma unroll
