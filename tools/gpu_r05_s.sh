@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 5 (s): the spill-free k_solve_lds with the deferred vote: full GPU suite, bench line,
+# kernel trace of the bench, then the PMC passes of the benched library (tools/gpu_pmc_r05.sh).
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/r05s
+mkdir -p $OUT
+cd $R
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+rc=$?; echo "gpu tests rc=$rc"; tail -3 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 bench.py > $OUT/bench.log 2>&1 || { tail -5 $OUT/bench.log; exit 1; }
+tail -1 $OUT/bench.log | cut -c1-600
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py > $OUT/prof.log 2>&1
+rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+cd $R
+bash tools/gpu_pmc_r05.sh > $OUT/pmc.log 2>&1
+rc=$?; echo "pmc rc=$rc"; tail -3 $OUT/pmc.log
+exit $rc
