@@ -52,9 +52,13 @@ constexpr int kRingC = RH_RING_C; // ... of phase C (one bin per pass: less work
 #ifndef RH_OVERLAP
 #define RH_OVERLAP 1                  // 1: no barrier vote between phase C and the next phase A (single-pass kernels)
 #endif
+#ifndef RH_STATS_C
+#define RH_STATS_C 1                  // 1: PSD / RAO / RMS sums formed where phase C stores Xi (no read-back)
+#endif
 #ifndef RH_XI_STORE
 #define RH_XI_STORE 1                 // 0: per-entry stores of passing entries; 1: while the iteration may be final; 2: traffic floor (A/B)
 #endif
+#define XI_STORE_MODE RH_XI_STORE
 #ifndef RH_A_BATCH
 #define RH_A_BATCH 0                  // > 0: phase-A nodes in batches of RH_A_BATCH, one tbfly16 per batch
 #endif
@@ -271,6 +275,9 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   constexpr int NBT = NB * NP;                     // bins per thread over all passes
   constexpr bool GX = NP > 1;                      // XiLast in the Xi_last block, not in LDS
   constexpr int kRingA = GX ? 3 : kRingA1;
+  // PSD / RAO / RMS sums formed in phase C (RH_STATS_C) by the 512-thread kernels; the SER
+  // kernels (C4's fixed point: no response output) keep them in the epilogue
+  constexpr bool kStatsC = RH_STATS_C && (XI_STORE_MODE == 1) && !SER && NB > 1;
 #if RH_OVERLAP && !defined(RH_VARIANTS)
   constexpr bool kOv = !GX;                        // the vote deferred into the next phase A (below)
 #else
@@ -461,6 +468,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     }
   };
 
+  const double hdw = 0.5 / d.dw;   // psd = |x|^2 hdw and rao = x (1 / zeta): multiplies, not 36 divisions per thread
   for (int it = it0; it < itend; ++it) {
     PROF_T(ta0);
     PROF_ADD(7, 1);
@@ -745,6 +753,8 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       }
       return __builtin_amdgcn_readfirstlane(__hip_atomic_load(&sflag[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != it + 1;
     };
+    if constexpr (kStatsC)
+      if (lane < 6) sred[wv * 6 + lane] = 0.0;   // this wave's RMS sums: only the final iteration's are kept
     if constexpr (kOv) {
       // the words of iteration it + 1: their last readers (iteration it - 1's vote) are done
       if (tid == 0) {
@@ -867,7 +877,33 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       // iteration may still be that one (may_be_final, with this bin's tests counted);
       // streamed: the final iteration's stores are the ones kept.  (Xi may be NULL with NP == 1.)
       if ((GX || Xo) && may_be_final()) {
-        if (okj) {
+        if constexpr (kStatsC) {
+          // PSD, RAO and the RMS sums from x in registers (the epilogue's arithmetic,
+          // k_motion_stats with one row): the final iteration's values are the ones kept, and
+          // nothing is read back
+          const double z = lz[b];
+          const double rz = fabs(z) > 1e-6 ? 1.0 / z : 0.0;
+          double m2v[6];
+#pragma unroll
+          for (int c = 0; c < 6; ++c) m2v[c] = okj ? abs2(c >= 3 ? scl(F[c], kRad2Deg) : F[c]) : 0.0;
+          if (okj) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+              st_nt(Xo + c * nw + b, F[c]);
+              if (a.o.psd) __builtin_nontemporal_store(m2v[c] * hdw, a.o.psd + ((size_t)ic * 6 + c) * nw + b);
+              if (a.o.rao) st_nt(a.o.rao + ((size_t)ic * 6 + c) * nw + b, scl(F[c], rz));
+            }
+          }
+          if (a.o.std) {   // the bin's six sums over the wave by two transposing butterflies
+            const int ln = lane_here();
+            const double t0 = tbfly3(m2v[0], m2v[1], m2v[2], ln), t1 = tbfly3(m2v[3], m2v[4], m2v[5], ln);
+            if (ln < 3) {
+              const int k = tbfly3_index(ln);
+              sred[wv * 6 + k] += t0;
+              sred[wv * 6 + 3 + k] += t1;
+            }
+          }
+        } else if (okj) {
 #pragma unroll
           for (int c = 0; c < 6; ++c) st_nt(Xo + c * nw + b, F[c]);
         }
@@ -1036,8 +1072,9 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
   // raft/raft_model.py:957): its Xi, PSD, RAO and std are NaN, as in k_solve_cases.  (The
   // entries of its last iterate were stored only where they passed their test.)
   const bool failed = status == RH_CASE_NAN || status == RH_CASE_SINGULAR;   // uniform
+  // (kStatsC: phase C formed PSD / RAO / the RMS sums of a case that did not fail)
   double ss[6] = {0, 0, 0, 0, 0, 0};
-  const double hdw = 0.5 / d.dw;   // psd = |x|^2 hdw and rao = x (1 / zeta): multiplies, not 36 divisions per thread
+  if (!kStatsC || failed) {
 #pragma unroll
   for (int j = 0; j < NBT; ++j) {
     const int b = tid + LT * j;
@@ -1060,11 +1097,14 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       if (a.o.rao) st(a.o.rao + ((size_t)ic * 6 + c) * nw + b, failed ? x : scl(x, rz));
     }
   }
+  }
   if (a.o.std) {
+    if (!kStatsC || failed) {
 #pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      const double s = wave_sum(ss[c]);
-      if (lane == 0) sred[wv * 6 + c] = s;
+      for (int c = 0; c < 6; ++c) {
+        const double s = wave_sum(ss[c]);
+        if (lane == 0) sred[wv * 6 + c] = s;
+      }
     }
     __syncthreads();
     if (tid < 6) {
