@@ -459,7 +459,8 @@ int rh_force_2nd_spectrum(rh_ctx* ctx, int n2, const double* w2, const rh_c128* 
  * interpreter time per design.  spec: one float64 record per design, design i at
  * spec[spec_off[i] .. spec_off[i+1]) (format: rh_prep.h; writer: raft/native_prep.py).
  * w, k [nw]: the shared frequency grid and wave numbers.  nthreads <= 0: all host cores.
- * Designs with MacCamy-Fuchs members are refused (RH_EINVAL): the Python path prepares them. */
+ * MacCamy-Fuchs members (raft/raft_member.py:1053-1088) get their frequency-dependent inertial
+ * excitation matrices, one [9][nw] block per node: rh_prep_imat. */
 typedef struct rh_prep rh_prep;
 int rh_prep_designs(int ndesign, const double* spec, const long long* spec_off, int nw, const double* w,
                     const double* k, int nthreads, rh_prep** out);
@@ -471,6 +472,11 @@ int rh_prep_layout(const rh_prep* p, long long* info);
 /* packed [total], mstart [total]; statics (optional) [ndesign][5][36] = M_struc, B_struc,
  * C_struc, C_hydro, A_hydro_morison. */
 int rh_prep_copy(const rh_prep* p, double* packed, int* mstart, double* statics);
+/* Design `design`'s MacCamy-Fuchs inertia table, the rh_design.imat_mcf of raft/prep.py
+ * node_table: [nn][9][nw] complex (zeros for the other nodes).  Returns its number of entries
+ * (nn 9 nw; 0 when no node of the design is MacCamy-Fuchs), and copies them when imat != NULL;
+ * RH_EINVAL for a bad handle or index. */
+long long rh_prep_imat(const rh_prep* p, int design, rh_c128* imat);
 void rh_prep_free(rh_prep* p);
 
 #ifdef __cplusplus

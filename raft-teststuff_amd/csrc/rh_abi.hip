@@ -1055,6 +1055,13 @@ int rh_prep_copy(const rh_prep* p, double* packed, int* mstart, double* statics)
   return RH_OK;
 }
 
+long long rh_prep_imat(const rh_prep* p, int design, rh_c128* imat) {
+  if (!p || design < 0 || design >= (int)p->res.size()) return fail(RH_EINVAL, "rh_prep_imat: bad arguments");
+  const auto& v = p->res[design].imat;
+  if (imat && !v.empty()) std::memcpy(imat, v.data(), v.size() * sizeof(double));
+  return (long long)(v.size() / 2);
+}
+
 void rh_prep_free(rh_prep* p) { delete p; }
 
 }  // extern "C"

@@ -29,6 +29,8 @@
 #include <thread>
 #include <vector>
 
+#include "rh_bessel.h"   // J_n, Y_n of real x: the MacCamy-Fuchs Hankel functions (host side here)
+
 #pragma clang fp contract(off)   // NumPy rounds every product and sum separately
 
 namespace rhp {
@@ -167,6 +169,7 @@ struct Member {
   // hydro constants
   std::vector<double> a_i;
   std::vector<M3> Imat;
+  std::vector<double> imat_mcf;   // MacCamy-Fuchs members: [ns][9][nw] complex (re, im), else empty
   M6 M_struc{};
   std::vector<double> mfill, pfill;
 
@@ -266,9 +269,47 @@ struct Member {
     }
   }
 
-  // raft/member.py calcHydroConstants without MacCamy-Fuchs (raft/raft_member.py:877-1050)
-  M6 hydro_constants(const V3& r_ref, double rho) {
+  // raft/member.py getCmSides (raft/raft_member.py:1053-1088): the side inertia coefficients
+  // at wave number k, MacCamy-Fuchs Cm = 4i / (pi (kR)^2 H1'(kR)) with
+  // H1'(x) = (H_0(x) - H_2(x)) / 2 (H = H^(1) = J + iY), blended from the plain 1 + Ca at
+  // k = 0 to Cm at k = pi / (5 R) by a cosine ramp
+  void cm_sides(int il, double k, double* c1, double* c2) const {   // c1, c2: (re, im)
+    const double Cm_p1_0 = 1. + coef(cap1, il), Cm_p2_0 = 1. + coef(cap2, il);
+    const double R = ds0[il] / 2;
+    const double x = k * R;
+    double Cr = 0.0, Ci = 0.0;
+    if (x > 0) {
+      double J[13], Y[13];
+      rh::bessel_jy12(x, J, Y);
+      const double hr = 0.5 * (J[0] - J[2]), hi = 0.5 * (Y[0] - Y[2]);   // H1'(x)
+      const double s = kPi * (x * x);
+      const double dr = s * hr, di = s * hi;                             // pi (kR)^2 H1'
+      // 4i / (dr + i di) in the form of NumPy's complex scalar division (Smith's, by a reciprocal)
+      if (std::fabs(dr) >= std::fabs(di)) {
+        const double rat = di / dr, scl = 1.0 / (dr + di * rat);
+        Cr = (0.0 + 4.0 * rat) * scl;
+        Ci = (4.0 - 0.0 * rat) * scl;
+      } else {
+        const double rat = dr / di, scl = 1.0 / (di + dr * rat);
+        Cr = (0.0 * rat + 4.0) * scl;
+        Ci = (4.0 * rat - 0.0) * scl;
+      }
+    }
+    const double Tr = kPi / 5 / R;
+    double ramp = k < Tr ? 0.5 * (1 - std::cos(kPi * (k - 0) / Tr)) : 1.0;
+    if (k <= 0) ramp = 0.0;
+    c1[0] = Cr * ramp + Cm_p1_0 * (1 - ramp);
+    c1[1] = Ci * ramp;
+    c2[0] = Cr * ramp + Cm_p2_0 * (1 - ramp);
+    c2[1] = Ci * ramp;
+  }
+
+  // raft/member.py calcHydroConstants (raft/raft_member.py:877-1050); a MacCamy-Fuchs member's
+  // inertial excitation matrix per wave number k[nw] goes to imat_mcf (its Imat stays zero, as
+  // in the Python path), every other member's Imat is frequency independent
+  M6 hydro_constants(const V3& r_ref, double rho, const double* kw, int nw) {
     M6 A = zero6();
+    if (mcf) imat_mcf.assign((size_t)ns * 9 * nw * 2, 0.0);
     for (int il = 0; il < ns; ++il) {
       if (!(r[il][2] < 0) || potMod) continue;
       const double v_side = side_volume(il);
@@ -283,7 +324,23 @@ struct Member {
           I.a[i][j] = rvs * (c1 * p1Mat.a[i][j] + c2 * p2Mat.a[i][j]) + rve * qMat.a[i][j];
           Am.a[i][j] = rvs * (Ca_p1 * p1Mat.a[i][j] + Ca_p2 * p2Mat.a[i][j]) + rve * qMat.a[i][j];
         }
-      Imat[il] = I;
+      if (mcf) {
+        // rho v_side (c1 p1Mat + c2 p2Mat) + I_end with complex c1, c2 (NumPy's order)
+        double* Im = imat_mcf.data() + (size_t)il * 9 * nw * 2;
+        for (int ik = 0; ik < nw; ++ik) {
+          double m1[2], m2[2];
+          cm_sides(il, kw[ik], m1, m2);
+          for (int e = 0; e < 9; ++e) {
+            const int i = e / 3, j = e % 3;
+            const double tr = m1[0] * p1Mat.a[i][j] + m2[0] * p2Mat.a[i][j];
+            const double ti = m1[1] * p1Mat.a[i][j] + m2[1] * p2Mat.a[i][j];
+            Im[((size_t)e * nw + ik) * 2] = rvs * tr + rve * qMat.a[i][j];
+            Im[((size_t)e * nw + ik) * 2 + 1] = rvs * ti;
+          }
+        }
+      } else {
+        Imat[il] = I;
+      }
       a_i[il] = a_end;
       acc6(A, translate_3to6(Am, sub(r[il], r_ref)));
     }
@@ -603,6 +660,7 @@ struct Result {
   std::vector<double> packed;   // w, k, node [NF][max(nn,1)], memb [MF][max(nm,1)], M, B, C
   std::vector<int> mstart;
   double statics[5 * 36] = {};  // M_struc, B_struc, C_struc, C_hydro, A_hydro_morison
+  std::vector<double> imat;     // [nn][9][nw] complex (re, im) when a node is MacCamy-Fuchs, else empty
 };
 
 struct Reader {
@@ -705,10 +763,7 @@ inline void prep_one(const double* spec, long long len, int nw, const double* w,
     rd.vec(b.cap_t, ncap);
     rd.vec(b.cap_d, ncap);
     if (rd.bad) break;
-    if (b.mcf) {
-      out.err = "rh_prep_designs: MacCamy-Fuchs members are prepared by the Python path (raft/member.py)";
-      return;
-    }
+    if (b.mcf && !b.circ) b.mcf = 0;   // (raft/member.py: MCF applies to circular members only)
     if (nst < 2) {
       out.err = "At least two stations entries must be provided";
       return;
@@ -838,12 +893,13 @@ inline void prep_one(const double* spec, long long len, int nw, const double* w,
 
   // added mass and inertial excitation (raft/fowt.py calcHydroConstants)
   M6 A_hydro = zero6();
-  for (auto& m : mems) acc6(A_hydro, m.hydro_constants(rP, rho));
+  for (auto& m : mems) acc6(A_hydro, m.hydro_constants(rP, rho, k, nw));
 
   // tables (raft/prep.py node_table / linear_matrices / host_tables)
   constexpr int NF = RH_NF_COUNT, MF = RH_MF_COUNT;
   std::vector<std::vector<double>> cols;
   std::vector<std::vector<double>> mcols;
+  std::vector<const double*> mcf_blocks;   // per node: its [9][nw] complex block, or NULL
   out.mstart = {0};
   for (auto& m : mems) {
     int nsub = 0;
@@ -876,7 +932,8 @@ inline void prep_one(const double* spec, long long len, int nw, const double* w,
       std::vector<double> c = {r[0], r[1], r[2], rr[0], rr[1], rr[2], m.q[0], m.q[1], m.q[2], m.p1[0], m.p1[1],
                                m.p1[2], m.p2[0], m.p2[1], m.p2[2], aq, ap1, ap2, aend, m.coef(m.cdq, il),
                                m.coef(m.cdp1, il), m.coef(m.cdp2, il), m.coef(m.cdend, il), m.circ ? 1.0 : 0.0,
-                               m.a_i[il], 0.0};
+                               m.a_i[il], m.mcf ? 1.0 : 0.0};
+      mcf_blocks.push_back(m.mcf ? m.imat_mcf.data() + (size_t)il * 9 * nw * 2 : nullptr);
       for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) c.push_back(m.Imat[il].a[i][j]);
       c.push_back(m.ls[il]);
@@ -887,6 +944,13 @@ inline void prep_one(const double* spec, long long len, int nw, const double* w,
   const int nnc = nn ? nn : 1, nmc = nm ? nm : 1;
   out.nn = nn;
   out.nm = nm;
+  bool any_mcf = false;
+  for (const double* blk : mcf_blocks) any_mcf |= blk != nullptr;
+  if (any_mcf) {   // (raft/prep.py node_table: zeros for the other nodes)
+    out.imat.assign((size_t)nn * 9 * nw * 2, 0.0);
+    for (int n = 0; n < nn; ++n)
+      if (mcf_blocks[n]) std::copy(mcf_blocks[n], mcf_blocks[n] + (size_t)9 * nw * 2, out.imat.data() + (size_t)n * 9 * nw * 2);
+  }
   out.packed.assign((size_t)2 * nw + (size_t)NF * nnc + (size_t)MF * nmc + 3 * 36, 0.0);
   double* P = out.packed.data();
   std::copy(w, w + nw, P);

@@ -132,6 +132,8 @@ def lib():
                 fn.restype = ctypes.c_int
             L.rh_prep_free.argtypes = [_p]
             L.rh_prep_free.restype = None
+            L.rh_prep_imat.argtypes = [_p, ctypes.c_int, _p]
+            L.rh_prep_imat.restype = ctypes.c_longlong
             L.rh_version.restype = ctypes.c_int
             L.rh_group_cases.argtypes = []
             L.rh_group_cases.restype = ctypes.c_int

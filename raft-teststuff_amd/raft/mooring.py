@@ -199,11 +199,14 @@ class Line:
         load's direction, with the same seabed-contact rule (the seabed plane then taken
         normal to the load through the lower end), and forces and stiffness are rotated back.
         Zero current gives the plain solve bit for bit.
-        Approximation (parity unpinned): with current, seabed contact is decided
-        from the lower end's global depth as without it; a net load that points away from the
-        seabed (a buoyant line in current) has no seabed contact at all, and the ends are then
-        ordered by height along the load (the catenary hangs "below" the end that is upstream
-        of the load)."""
+        Approximation (parity unpinned): with current, the ends of EVERY line are
+        ordered by height along the load, not by global depth (the catenary hangs "below" the
+        end that is upstream of the load), and seabed contact is decided from the global depth
+        of the end that ordering calls lower, as without current.  So a heavy line whose load
+        current tilts far enough toward the fairlead (the anchor then ranks upper) is solved
+        fully suspended, whatever the anchor's depth; a net load that points away from the
+        seabed (a buoyant line in current) never has seabed contact
+        (tests/test_mooring.py::test_heavy_line_ordering_flip_in_current)."""
         W = self.type["w"]
         R = None
         up = False                                     # the net load points away from the seabed

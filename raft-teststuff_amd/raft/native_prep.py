@@ -253,6 +253,15 @@ class PreparedDesigns:
             self.statics = np.empty([nd, 5, 6, 6], dtype=float)
             N.check(L.rh_prep_copy(h, self.packed.ctypes.data, self.mstart.ctypes.data, self.statics.ctypes.data),
                     "rh_prep_copy")
+            # MacCamy-Fuchs designs: their [nn][9][nw] inertia tables (raft/prep.py node_table)
+            self.imat = {}
+            for i in range(nd):
+                n = L.rh_prep_imat(h, i, None)
+                N.check(0 if n >= 0 else int(n), "rh_prep_imat")
+                if n > 0:
+                    a = np.empty(int(n), dtype=complex)
+                    L.rh_prep_imat(h, i, a.ctypes.data)
+                    self.imat[i] = a.reshape(int(info[5 * i + 3]), 9, len(w))
         finally:
             L.rh_prep_free(h)
         self.info = info[:5 * nd].reshape(nd, 5)
@@ -277,5 +286,5 @@ class PreparedDesigns:
             cached = self._layouts[(nn, nm)] = (layout, off)
         layout, total = cached
         assert total == n
-        return dict(packed=self.packed[o:o + n], layout=layout, imat=None, mstart=self.mstart[mo:mo + nm + 1],
+        return dict(packed=self.packed[o:o + n], layout=layout, imat=self.imat.get(i), mstart=self.mstart[mo:mo + nm + 1],
                     nn=nn, nm=nm, per_bin=False)

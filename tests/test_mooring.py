@@ -243,6 +243,31 @@ def test_buoyant_line_in_current(U):
     assert np.abs(ln.fA - fA).max() < 1e-7 * T and np.abs(ln.fB - fB).max() < 1e-7 * T
 
 
+@pytest.mark.parametrize("U", [3.5, 4.0])
+def test_heavy_line_ordering_flip_in_current(U):
+    """A heavy line (net weight 215 N/m) from an anchor on the seabed to a fairlead 220 m away,
+    in a current strong enough to tilt its load toward the fairlead past the chord: along the
+    load the anchor is then the upper end, so the solve orders the ends that way and treats the
+    line as fully suspended (no seabed contact; documented in Line.static_solve).  That solution
+    balances the distributed load and is the continuous elastic line's (shooting solve, no
+    seabed), and the anchor is pulled up."""
+    from raft.mooring import MooringSystem, Point
+    ms = MooringSystem(depth=200.0)
+    ms.add_line_type("chain", 0.15, 40.0, 500e6, 1.2, 0.1)
+    a = ms.add_point(Point.FIXED, [-220.0, 0.0, -200.0])
+    b = ms.add_point(Point.FIXED, [0.0, 0.0, -20.0])
+    ln = ms.add_line(300.0, "chain", a, b)
+    Uv = np.array([U, 0.0, 0.0])
+    f = np.array([0.0, 0.0, -ln.type["w"]]) + ln.current_load(Uv, ms.rho)
+    assert f[2] < 0 and np.dot(f, b.r - a.r) > 0          # a downward load, tilted past the chord
+    ln.static_solve(ms.depth, 1e-10, Uv, ms.rho)
+    assert np.allclose(ln.fA + ln.fB, f * ln.L, rtol=1e-8, atol=1e-6 * np.linalg.norm(f) * ln.L)
+    fA, fB = _shooting_end_forces(ln, f, ln.fA * 1.05)
+    T = np.linalg.norm(ln.fB)
+    assert np.abs(ln.fA - fA).max() < 1e-7 * T and np.abs(ln.fB - fB).max() < 1e-7 * T
+    assert ln.fA[2] > 0
+
+
 def test_line_current_stiffness_matches_differences():
     """End stiffness of the rotated solve against central differences of its end forces (the
     current load held at the base geometry's value, as the analytic stiffness assumes)."""

@@ -114,13 +114,27 @@ def test_native_statics_given_override():
     _compare(h, P.host_tables(0))
 
 
-def test_native_refuses_maccamy_fuchs_and_bad_specs():
+def test_native_maccamy_fuchs_matches_python():
+    """OC4semi (MacCamy-Fuchs columns, raft/raft_member.py:1053-1088): the node tables as
+    above, and the frequency-dependent inertia table rh_prep_imat against raft/member.py's
+    Imat_MCF (scipy's hankel1 there, rh_bessel.h's series / recurrences here: 1e-13 of the
+    table's largest entry)."""
+    d = load_design("OC4semi-RAFT_QTF")
+    st = {"C_moor": C_MOOR}
+    h, f = _python_tables(d, st)
+    P = _native([d], [st])
+    n = P.host_tables(0)
+    _compare(h, n)
+    assert h["imat"] is not None and n["imat"] is not None
+    assert n["imat"].shape == h["imat"].shape
+    err = np.abs(n["imat"] - h["imat"]).max()
+    assert err <= 1e-13 * np.abs(h["imat"]).max(), err
+
+
+def test_native_bad_specs():
     from raft import _native as N
     from raft.native_prep import PreparedDesigns, design_spec
-    d = load_design("OC4semi-RAFT_QTF")
     w = np.arange(1, 11) * 0.1
-    with pytest.raises(ValueError, match="MacCamy-Fuchs"):
-        PreparedDesigns([design_spec(d, statics={"C_moor": C_MOOR})], w, w)
     s = design_spec(load_design("OC3spar"), statics={"C_moor": C_MOOR})
     with pytest.raises(ValueError, match="spec record"):
         PreparedDesigns([s[:-1]], w, w)
@@ -129,3 +143,4 @@ def test_native_refuses_maccamy_fuchs_and_bad_specs():
     with pytest.raises(ValueError, match="magic"):
         PreparedDesigns([bad], w, w)
     assert N.lib().rh_prep_layout(None, None) == N.RH_EINVAL
+    assert N.lib().rh_prep_imat(None, 0, None) == N.RH_EINVAL
