@@ -1208,19 +1208,20 @@ __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& 
 // the rest are k_qtf_lcoef's (x, y) blocks, so the coefficient blocks fill the CUs the Kim & Yue
 // tiles leave idle instead of running before them.  Per tile and per block the arithmetic is
 // that of the two kernels: the same bits.
-constexpr int kLkThreads = 2 * kKayThreads;
+constexpr int kLkTiles = 512 / kKayThreads;   // Kim & Yue tiles per k_qtf_lk block (2, or 1 when split)
+constexpr int kLkThreads = kLkTiles * kKayThreads;
 
 static_assert(kLkThreads == 512, "k_qtf_lk: lcoef_block is a 512-thread block");
 __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(RH_KAY_WPE))) void k_qtf_lk(
     rh_qtf_design q, QtfWork wk, const double* __restrict__ M66, int t0, int ntile, int nkb, int bx0, int nbx) {
   constexpr int kAcc = 12 * 256, kRed = 8 * 12 * 64;
   constexpr int kSm = 2 * kAcc > kRed ? 2 * kAcc : kRed;
-  __shared__ double sm[kSm];                 // two Kim & Yue tile sums, or lcoef_block's wave sums
-  __shared__ double psg[kKayS > 1 ? 2 * kKayM * (kKayS - 1) * 16 * 64 : 1];
+  __shared__ double sm[kSm];                 // kLkTiles Kim & Yue tile sums, or lcoef_block's wave sums
+  __shared__ double psg[kKayS > 1 ? kLkTiles * kKayM * (kKayS - 1) * 16 * 64 : 1];
   const int tid = (int)threadIdx.x;
   if ((int)blockIdx.x < nkb) {               // block-uniform
     const int grp = __builtin_amdgcn_readfirstlane(tid / kKayThreads);   // wave-uniform: the tile indices stay scalar
-    const int t = 2 * xcd_remap((int)blockIdx.x, nkb) + grp;   // this group's tile of the rank's order
+    const int t = kLkTiles * xcd_remap((int)blockIdx.x, nkb) + grp;   // this group's tile of the rank's order
     const bool live = t < ntile;
     int T1 = 0, T2 = 0;
     if (live) qtf_tile_of(t0 + t, qtf_n2p(q) / 16, T1, T2);
