@@ -62,30 +62,36 @@ __device__ __forceinline__ double nrm2(const double* node, int nn, int f, int n)
   return a * a + b * b + c * c;
 }
 
-__device__ __forceinline__ void node_bmat(const double* node, int nn, int n, double rho, const double* sums,
-                                          double* bm, double* B4 = nullptr) {
-  const bool circ = nf(node, nn, RH_NF_CIRC, n) != 0.0;
+// One node's drag matrix Bmat = Bq (qq^T) + Bp1 (p1p1^T) + Bp2 (p2p2^T) + Be (qq^T) from its
+// RMS sums (raft/raft_fowt.py:1205-1248); F(field) reads the node's RH_NF_* fields.
+template <class Fld>
+__device__ __forceinline__ void node_bmat_f(Fld F, double rho, const double* sums, double* bm, double* B4 = nullptr) {
+  const bool circ = F(RH_NF_CIRC) != 0.0;
   const double vq = sqrt(0.5 * sums[0]);
   const double vp1 = sqrt(0.5 * sums[1]);
   const double vp2 = circ ? vp1 : sqrt(0.5 * sums[2]);
-  const double Bq = kSqrt8Pi * vq * 0.5 * rho * nf(node, nn, RH_NF_AQ, n) * nf(node, nn, RH_NF_CDQ, n);
-  const double Bp1 = kSqrt8Pi * vp1 * 0.5 * rho * nf(node, nn, RH_NF_AP1, n) * nf(node, nn, RH_NF_CDP1, n);
-  const double Bp2 = kSqrt8Pi * vp2 * 0.5 * rho * nf(node, nn, RH_NF_AP2, n) * nf(node, nn, RH_NF_CDP2, n);
-  const double Be = kSqrt8Pi * vq * 0.5 * rho * nf(node, nn, RH_NF_AEND, n) * nf(node, nn, RH_NF_CDEND, n);
+  const double Bq = kSqrt8Pi * vq * 0.5 * rho * F(RH_NF_AQ) * F(RH_NF_CDQ);
+  const double Bp1 = kSqrt8Pi * vp1 * 0.5 * rho * F(RH_NF_AP1) * F(RH_NF_CDP1);
+  const double Bp2 = kSqrt8Pi * vp2 * 0.5 * rho * F(RH_NF_AP2) * F(RH_NF_CDP2);
+  const double Be = kSqrt8Pi * vq * 0.5 * rho * F(RH_NF_AEND) * F(RH_NF_CDEND);
   if (B4) {
     B4[0] = Bq;
     B4[1] = Bp1;
     B4[2] = Bp2;
     B4[3] = Be;
   }
-  const double q[3] = {nf(node, nn, RH_NF_QX, n), nf(node, nn, RH_NF_QY, n), nf(node, nn, RH_NF_QZ, n)};
-  const double p1[3] = {nf(node, nn, RH_NF_P1X, n), nf(node, nn, RH_NF_P1Y, n), nf(node, nn, RH_NF_P1Z, n)};
-  const double p2[3] = {nf(node, nn, RH_NF_P2X, n), nf(node, nn, RH_NF_P2Y, n), nf(node, nn, RH_NF_P2Z, n)};
+  const double q[3] = {F(RH_NF_QX), F(RH_NF_QY), F(RH_NF_QZ)};
+  const double p1[3] = {F(RH_NF_P1X), F(RH_NF_P1Y), F(RH_NF_P1Z)};
+  const double p2[3] = {F(RH_NF_P2X), F(RH_NF_P2Y), F(RH_NF_P2Z)};
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       bm[3 * i + j] = (Bq * (q[i] * q[j]) + Bp1 * (p1[i] * p1[j]) + Bp2 * (p2[i] * p2[j])) + Be * (q[i] * q[j]);
+}
+__device__ __forceinline__ void node_bmat(const double* node, int nn, int n, double rho, const double* sums,
+                                          double* bm, double* B4 = nullptr) {
+  node_bmat_f([&](int f) { return nf(node, nn, f, n); }, rho, sums, bm, B4);
 }
 
 // Entry (i,j) of translateMatrix3to6DOF(Bm, r) (raft/helpers.py:455-478).

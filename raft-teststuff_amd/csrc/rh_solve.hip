@@ -660,6 +660,14 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     PROF_ADD(1, ta1 - ta0);
     // ---------------- B: node drag matrices and B_drag ----------------------------------
     for (int n = tid; n < nn; n += LT) {
+      // the node's fields XX .. CIRC and T, all loads issued before any use (left to the
+      // scheduler, each load waited on before the next was issued: eight serial L2 round trips)
+      double fv[RH_NF_CIRC - RH_NF_XX + 2];
+#pragma unroll
+      for (int f = RH_NF_XX; f <= RH_NF_CIRC; ++f) fv[f - RH_NF_XX] = node[(size_t)f * nn + n];
+      fv[RH_NF_CIRC - RH_NF_XX + 1] = node[(size_t)RH_NF_T * nn + n];
+      __builtin_amdgcn_sched_barrier(0);
+      auto F = [&](int f) { return f == RH_NF_T ? fv[RH_NF_CIRC - RH_NF_XX + 1] : fv[f - RH_NF_XX]; };
       double r3[3];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
@@ -670,12 +678,13 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
         r3[c] = s;
       }
       // sum|vrel_q|^2 = sum|s_q|^2 |q|^2 ; circular: |vrel_p|^2 = |s_1|^2|p1|^2 + |s_2|^2|p2|^2
-      const double qq = nrm2(node, nn, RH_NF_QX, n), pp1 = nrm2(node, nn, RH_NF_P1X, n), pp2 = nrm2(node, nn, RH_NF_P2X, n);
-      const bool circ = nf(node, nn, RH_NF_CIRC, n) != 0.0;
+      auto n2 = [&](int f) { const double a = F(f), b = F(f + 1), c = F(f + 2); return a * a + b * b + c * c; };
+      const double qq = n2(RH_NF_QX), pp1 = n2(RH_NF_P1X), pp2 = n2(RH_NF_P2X);
+      const bool circ = F(RH_NF_CIRC) != 0.0;
       const double sums[3] = {r3[0] * qq, circ ? r3[1] * pp1 + r3[2] * pp2 : r3[1] * pp1, r3[2] * pp2};
       double B4[4];
-      node_bmat(node, nn, n, rho, sums, bm + 9 * n, B4);
-      const double t = nf(node, nn, RH_NF_T, n);
+      node_bmat_f(F, rho, sums, bm + 9 * n, B4);
+      const double t = F(RH_NF_T);
       double* A = al + 6 * n;
       A[0] = B4[0] + B4[3];     // axial: side + end   (qMat terms of Bmat, raft/raft_fowt.py:1228-1248)
       A[1] = B4[1];
@@ -684,7 +693,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       A[4] = t * B4[2];
       if (!SER) {
         // this node's translateMatrix3to6DOF (raft/helpers.py:455-478), summed below in node order
-        const double rx = nf(node, nn, RH_NF_XX, n), ry = nf(node, nn, RH_NF_XY, n), rz = nf(node, nn, RH_NF_XZ, n);
+        const double rx = F(RH_NF_XX), ry = F(RH_NF_XY), rz = F(RH_NF_XZ);
 #pragma unroll
         for (int e = 0; e < 36; ++e) bdn[e * nn + n] = t3to6(bm + 9 * n, rx, ry, rz, e / 6, e % 6);
       }
