@@ -568,15 +568,14 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
           s2 += abs2(sp2);
         }
       };
-#if RH_A_BATCH
+      if constexpr (RH_A_BATCH > 0 && !GX) {
       // Nodes in batches of kB (= the ring depth): the three sums of each node of a batch are
       // independent chains, and the 3 kB values are reduced over the wave by ONE transposing
       // butterfly (tbfly16: 17 exchange steps for up to 16 values, against 8 per node for
       // tbfly3); lanes 0..15 then hold the totals.  The ring slot of node n is refilled with
       // node n + kB as soon as n is summed.
-      constexpr int kB = RH_A_BATCH;
+      constexpr int kB = RH_A_BATCH > 0 ? RH_A_BATCH : 1;
       static_assert(3 * kB <= 16, "tbfly16 reduces at most 16 values");
-      static_assert(NP == 1, "RH_A_BATCH: single-pass grids only");
       cd K[kB][3][NB];
 #pragma unroll
       for (int r = 0; r < kB; ++r) load_node(K[r], r);
@@ -604,7 +603,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
         const int vi = tbfly16_index(ln);
         if (ln < 16 && vi < 3 * kB && n + vi / 3 < nn) red[((n + vi / 3) * 3 + vi % 3) * LW + wv_s] = tot;
       }
-#else
+      } else {
       // the three sums of a node are reduced over the wave together (tbfly3); lane k < 3
       // writes sum k.  The ring slot of node n is refilled with node n + kRingA.
       cd K[kRingA][3][NB];
@@ -637,7 +636,7 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
           }
         }
       }
-#endif
+      }
     }
 #ifdef RH_VARIANTS
     skip_a = false;
