@@ -18,11 +18,11 @@ if __name__ == "__main__":
     L = N.lib()
     if hasattr(L, "rh_prof_read"):      # RH_PROF builds: phase cycles of the fixed-point launches
         import ctypes
-        buf = (ctypes.c_ulonglong * 8)()
+        buf = (ctypes.c_ulonglong * 12)()
         L.rh_prof_read(buf, 0)
         v = list(buf)
         nit = max(v[7], 1)
         names = ["A/iter", "B/iter", "C-exc/iter", "C-solve/iter", "flags/iter"]
         print("  cycles (s_memtime, wave 0, all launches): " + "  ".join(
-            f"{n}={x / nit:,.0f}" for n, x in zip(names, v[1:6])) + f"  prologue+epilogue total/iter={(v[0] + v[6]) / nit:,.0f}",
-            flush=True)
+            f"{n}={x / nit:,.0f}" for n, x in zip(names, v[1:6])) + f"  (Z/iter={v[8] / nit:,.0f}  LU/iter={v[9] / nit:,.0f})"
+            f"  prologue+epilogue total/iter={(v[0] + v[6]) / nit:,.0f}", flush=True)
