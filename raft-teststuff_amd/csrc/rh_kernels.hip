@@ -190,7 +190,9 @@ __global__ __launch_bounds__(256) void k_wave_force_sum(int nw, int nn, int nhea
   const int b = t % nw, c = (t / nw) % 6, h = t / (6 * nw);
   const rh_c128* p = fw + ((size_t)h * nn * 6 + c) * nw + b;
   cd F = mk(0, 0);
-#pragma unroll 4
+  // (the loads of 16 nodes issued ahead of their in-order adds: one thread per (heading, DOF,
+  // bin) is only about one wave per CU, so the loop runs on load latency)
+#pragma unroll 16
   for (int n = 0; n < nn; ++n) F = add(F, ld(p + (size_t)n * 6 * nw));
   st(finer + ((size_t)h * 6 + c) * nw + b, F);
 }
