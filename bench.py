@@ -722,16 +722,28 @@ def main():
     prep = prepare_batch([dd], cs)
     want = ("psd", "std", "zeta", "rao")
     stream = torch.cuda.current_stream()
+    # Pipelined steps: consecutive steps alternate between two streams, each with its own wave
+    # tables (a second DeviceDesign of the same FOWT) and its own outputs, so step i + 1's tables
+    # and first workgroups start on the CUs that step i's last cases leave idle (its makespan
+    # tail).  Every step still tabulates and solves its whole batch.
+    from raft.prep import DeviceDesign
+    streams = [stream, torch.cuda.Stream(device)]
+    dds = [dd, DeviceDesign(f, device=device)]
+    with torch.cuda.stream(streams[1]):
+        preps = [prep, prepare_batch([dds[1]], cs)]
+    torch.cuda.synchronize()
 
-    def step(e=None):
-        """One C2 step: the per-heading wave tables of the design (k_wave_tables, all headings
-        of the batch in one launch) and the batched drag fixed point (k_solve_lds)."""
-        if e is not None:
-            e[0].record(stream)
-        dd.retabulate()
-        if e is not None:
-            e[1].record(stream)
-        return solve_batch([dd], cs, m.nIter, m.XiStart, 0.01, want=want, prepared=prep)
+    def step(e=None, k=0):
+        """One C2 step on stream k: the per-heading wave tables of the design (k_wave_tables,
+        all headings of the batch in one launch) and the batched drag fixed point (k_solve_lds)."""
+        s = streams[k]
+        with torch.cuda.stream(s):
+            if e is not None:
+                e[0].record(s)
+            dds[k].retabulate()
+            if e is not None:
+                e[1].record(s)
+            return solve_batch([dds[k]], cs, m.nIter, m.XiStart, 0.01, want=want, prepared=preps[k])
 
     comm = torch.cuda.Stream(device) if world > 1 else None
 
@@ -759,20 +771,22 @@ def main():
         legs["c4"] = bench_c4(device, max(3, args.steps // 2), world, rank, dist)
     if not args.no_c5:
         legs["c5"] = bench_c5(device, max(3, args.steps // 4), world, rank, dist, pool, nproc)
-    for _ in range(args.warmup):
-        res = step()
+    for i in range(args.warmup):
+        res = step(None, i % 2)
         if world > 1:
             e = torch.cuda.Event()
-            e.record(stream)
+            e.record(streams[i % 2])
             w, _, _ = gather_async(res, e)
             w.wait()
     torch.cuda.synchronize()
 
-    def timed(gather):
-        # two events per step: before the wave tables and before the solve; the solve of step i
-        # ends where step i + 1 begins (ev[i + 1][0], or `end` after the last step), nothing runs
-        # between them on the stream.  (Each timing event is a barrier packet: a third one per
-        # step cost 4 us of the 0.87 ms step, tools/ubench/event_cost.py.)
+    def timed(gather, pipelined=False):
+        # serial (one stream): two events per step, before the wave tables and before the solve;
+        # the solve of step i ends where step i + 1 begins (ev[i + 1][0], or `end` after the last
+        # step), nothing runs between them on the stream: the kernel times of the roofline.
+        # (Each timing event is a barrier packet: a third one per step cost 4 us of the 0.87 ms
+        # step, tools/ubench/event_cost.py.)  pipelined: steps alternate between the two streams,
+        # no per-step events; the host clock between the synchronisations times the K steps.
         ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
         end = torch.cuda.Event(enable_timing=True)
         pend = []
@@ -781,10 +795,11 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            r = step(ev[i])
+            k = i % 2 if pipelined else 0
+            r = step(None if pipelined else ev[i], k)
             if gather:
                 e_done = torch.cuda.Event()
-                e_done.record(stream)
+                e_done.record(streams[k])
                 pend.append(gather_async(r, e_done))
         end.record(stream)
         for work, _, _ in pend:
@@ -806,10 +821,13 @@ def main():
             assert out.shape[0] == world * args.ncase and torch.all(out[:, -1] >= 1)
         return float(t.item()), (ev, end), r, gms
 
-    dt_ng, (ev, end), res, _ = timed(False)
+    dt_serial, (ev, end), res, _ = timed(False)
+    dt_ng, _, r_pipe, _ = timed(False, pipelined=True)
+    # the pipelined steps solve the same batch: the same bits as the serial pass
+    assert all(torch.equal(r_pipe[k], res[k]) for k in ("iters", "std", "psd")), "pipelined C2 step differs"
     dt_max, gather_ms = dt_ng, None
     if world > 1:
-        dt_max, _, _, gather_ms = timed(True)
+        dt_max, _, _, gather_ms = timed(True, pipelined=True)
     tab_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     nxt = [e[0] for e in ev[1:]] + [end]
     kern_ms = float(np.mean([e[1].elapsed_time(n) for e, n in zip(ev, nxt)]))
@@ -839,7 +857,11 @@ def main():
                                "(step = per-heading wave tables + batched drag fixed point)",
                    "cases_per_step_per_gpu": args.ncase, "nw": dd.nw, "submerged_nodes": dd.nn,
                    "nodes_circ_rect": [nc, nr], "nIter": int(m.nIter), "headings": len(dd.headings),
-                   "parallelism": f"case-sharded x{world}"},
+                   "parallelism": f"case-sharded x{world}",
+                   "pipeline": "consecutive steps alternate between two HIP streams with their own wave "
+                               "tables and outputs (value, ms_per_step); kernel_ms and the roofline from a "
+                               "serial pass of the same K steps on one stream",
+                   "ms_per_step_serial": dt_serial / args.steps * 1e3},
         "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_FP64 / 1e12, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP64, "traffic": pmc_traffic("solve", *solve_kernels(dd.nw)),
                      **hw_util("solve", solve_kernels(dd.nw), kern_ms),
