@@ -727,10 +727,13 @@ def main():
     # and first workgroups start on the CUs that step i's last cases leave idle (its makespan
     # tail).  Every step still tabulates and solves its whole batch.
     from raft.prep import DeviceDesign
-    streams = [stream, torch.cuda.Stream(device)]
-    dds = [dd, DeviceDesign(f, device=device)]
-    with torch.cuda.stream(streams[1]):
-        preps = [prep, prepare_batch([dds[1]], cs)]
+    nstream = int(os.environ.get("RAFT_BENCH_STREAMS", "2"))
+    streams = [stream] + [torch.cuda.Stream(device) for _ in range(nstream - 1)]
+    dds = [dd] + [DeviceDesign(f, device=device) for _ in range(nstream - 1)]
+    preps = [prep]
+    for k in range(1, nstream):
+        with torch.cuda.stream(streams[k]):
+            preps.append(prepare_batch([dds[k]], cs))
     torch.cuda.synchronize()
 
     def step(e=None, k=0):
@@ -772,10 +775,10 @@ def main():
     if not args.no_c5:
         legs["c5"] = bench_c5(device, max(3, args.steps // 4), world, rank, dist, pool, nproc)
     for i in range(args.warmup):
-        res = step(None, i % 2)
+        res = step(None, i % nstream)
         if world > 1:
             e = torch.cuda.Event()
-            e.record(streams[i % 2])
+            e.record(streams[i % nstream])
             w, _, _ = gather_async(res, e)
             w.wait()
     torch.cuda.synchronize()
@@ -795,7 +798,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            k = i % 2 if pipelined else 0
+            k = i % nstream if pipelined else 0
             r = step(None if pipelined else ev[i], k)
             if gather:
                 e_done = torch.cuda.Event()
@@ -858,7 +861,7 @@ def main():
                    "cases_per_step_per_gpu": args.ncase, "nw": dd.nw, "submerged_nodes": dd.nn,
                    "nodes_circ_rect": [nc, nr], "nIter": int(m.nIter), "headings": len(dd.headings),
                    "parallelism": f"case-sharded x{world}",
-                   "pipeline": "consecutive steps alternate between two HIP streams with their own wave "
+                   "pipeline": f"consecutive steps rotate over {nstream} HIP streams with their own wave "
                                "tables and outputs (value, ms_per_step); kernel_ms and the roofline from a "
                                "serial pass of the same K steps on one stream",
                    "ms_per_step_serial": dt_serial / args.steps * 1e3},
