@@ -1,20 +1,18 @@
 #!/bin/bash
-# Round 5 (g): GPU suite (member-major LDS rows in k_solve_lds, contiguous QTF tile blocks),
-# per-rank QTF timing (rank r of 8 alone on one GPU), the bench legs and their kernel trace.
+# Round 5 (g, pipelined bench legs): the spill-free k_solve_lds with the deferred vote: full GPU suite, bench line,
+# kernel trace of the bench, then the PMC passes of the benched library (tools/gpu_pmc_r05.sh).
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r05g
 mkdir -p $OUT
 cd $R
-timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/gpu_tests.log
-if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" $OUT/gpu_tests.log | head -30; exit $rc; fi
-timeout -k 10 120 python3 tools/ubench/time_qtf.py ranks 8 > $OUT/qtf_ranks.log 2>&1 || { tail -5 $OUT/qtf_ranks.log; exit 1; }
-grep -v amdgpu.ids $OUT/qtf_ranks.log
-timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/bench.log 2>&1
-rc=$?; echo "bench rc=$rc"; tail -1 $OUT/bench.log | cut -c1-400
-if [ $rc -ne 0 ]; then tail -20 $OUT/bench.log; exit $rc; fi
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+rc=$?; echo "gpu tests rc=$rc"; tail -3 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 bench.py > $OUT/bench.log 2>&1 || { tail -5 $OUT/bench.log; exit 1; }
+tail -1 $OUT/bench.log | cut -c1-600
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-c5 > $OUT/bench_prof.log 2>&1
-rc=$?; echo "rocprof rc=$rc"
-find $OUT/prof -name "*kernel_stats.csv" | head -2
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py > $OUT/prof.log 2>&1
+rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+cd $R
+bash tools/gpu_pmc_r05.sh > $OUT/pmc.log 2>&1
+rc=$?; echo "pmc rc=$rc"; tail -3 $OUT/pmc.log
 exit $rc
