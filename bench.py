@@ -401,24 +401,25 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
         # above is reported beside it.  The pipelined outputs equal a whole QTF bit for bit.
         if world > 1:
             q = qd.qtf(dd.w, X, M66)      # this GPU's whole QTF (the check below)
-        qds = [qd, QtfDevice(f, w2, k2, 0.0, device)]
-        streams = [stream, torch.cuda.Stream(device)]
-        outs = [torch.empty_like(q), torch.empty_like(q)]
-        for i in range(4):
-            with torch.cuda.stream(streams[i % 2]):
-                qds[i % 2].qtf(dd.w, X, M66, out=outs[i % 2])
+        nqs = int(os.environ.get("RAFT_BENCH_QTF_STREAMS", "2"))
+        qds = [qd] + [QtfDevice(f, w2, k2, 0.0, device) for _ in range(nqs - 1)]
+        streams = [stream] + [torch.cuda.Stream(device) for _ in range(nqs - 1)]
+        outs = [torch.empty_like(q) for _ in range(nqs)]
+        for i in range(2 * nqs):
+            with torch.cuda.stream(streams[i % nqs]):
+                qds[i % nqs].qtf(dd.w, X, M66, out=outs[i % nqs])
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
-            with torch.cuda.stream(streams[i % 2]):
-                qds[i % 2].qtf(dd.w, X, M66, out=outs[i % 2])
+            with torch.cuda.stream(streams[i % nqs]):
+                qds[i % nqs].qtf(dd.w, X, M66, out=outs[i % nqs])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        assert torch.equal(outs[0], q) and torch.equal(outs[1], q), "pipelined QTF differs"
+        assert all(torch.equal(o, q) for o in outs), "pipelined QTF differs"
     t = torch.tensor([dt, t_e2e, t_tables, t_first, dt_serial], dtype=torch.float64, device=f"cuda:{device}")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -430,7 +431,7 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
     achieved = fpp * mine / (ms * 1e-3)
     out = {"metric": "QTF pairs/sec", "value": world * npair * steps / dt_max, "unit": "pairs/s", "steps": steps,
            "ms_per_qtf": dt_max / steps * 1e3,
-           "pipeline": "each GPU's QTFs alternate between two HIP streams with their own tables and workspace "
+           "pipeline": f"each GPU's QTFs rotate over {nqs} HIP streams with their own tables and workspace "
                        "(value, ms_per_qtf); kernel_ms and the roofline from the serial pass",
            "end_to_end_ms": e2e_max * 1e3, "host_tables_ms": tab_max * 1e3,
            "first_call_ms": first_max * 1e3,
