@@ -62,6 +62,9 @@ constexpr int kRingC = RH_RING_C; // ... of phase C (one bin per pass: less work
 #ifndef RH_A_BATCH
 #define RH_A_BATCH 0                  // > 0: phase-A nodes in batches of RH_A_BATCH, one tbfly16 per batch
 #endif
+#ifndef RH_A_PAIR
+#define RH_A_PAIR 1                   // 1: phase-A sums of two nodes per butterfly (tbfly6)
+#endif
 #ifndef RH_LDS_LANE_BRANCH
 #define RH_LDS_LANE_BRANCH 0          // 1: the round-2 per-lane `continue` before the solve (A/B only)
 #endif
@@ -165,6 +168,35 @@ __device__ __forceinline__ double tbfly3(double a, double b, double c, int lane)
 }
 // value held by a lane after tbfly3: 2 f0 + f1 -> lane 0: a (0), lane 1: c (2), lane 2: b (1)
 __device__ __forceinline__ int tbfly3_index(int lane) { return 2 * (lane & 1) + ((lane >> 1) & 1); }
+
+// Six wave sums at once: the three sums of two nodes.  Transposing stages with tbfly16's lane
+// flags (partners i^1, i^2, i^7 within the 16-lane row): (a0, a1), (b0, b1), (c0, c1) -> three
+// values, (v0, v1), (v2, 0) -> two, then one; the row halves (i^15) hold the same value and
+// are added, then the rows (lane^16, lane^32).  9 exchanges instead of 2 x 7 for two tbfly3.
+struct Bfly6 {   // a lane's stage flags and the sum it holds after tbfly6 (formed once per phase A)
+  bool f0, f1, f2;
+  int vi;         // 3 node + sum, or -1 (pad; lanes >= 8 hold copies)
+};
+__device__ __forceinline__ Bfly6 bfly6_lane(int lane) {
+  const int i = lane & 15;
+  Bfly6 b;
+  b.f0 = ((i ^ (i >> 2)) & 1) != 0;
+  b.f1 = (((i >> 1) ^ (i >> 2)) & 1) != 0;
+  b.f2 = (((i >> 2) ^ (i >> 3)) & 1) != 0;
+  b.vi = lane >= 8 ? -1 : b.f2 ? (b.f1 ? -1 : 3 * b.f0 + 2) : 3 * b.f0 + b.f1;
+  return b;
+}
+__device__ __forceinline__ double tbfly6(double a0, double b0, double c0, double a1, double b1, double c1, const Bfly6& L) {
+  const bool f0 = L.f0, f1 = L.f1, f2 = L.f2;
+  const double v0 = (f0 ? a1 : a0) + dpp_mov<0xB1>(f0 ? a0 : a1);
+  const double v1 = (f0 ? b1 : b0) + dpp_mov<0xB1>(f0 ? b0 : b1);
+  const double v2 = (f0 ? c1 : c0) + dpp_mov<0xB1>(f0 ? c0 : c1);
+  const double w0 = (f1 ? v1 : v0) + dpp_mov<0x4E>(f1 ? v0 : v1);
+  const double w1 = (f1 ? 0.0 : v2) + dpp_mov<0x4E>(f1 ? v2 : 0.0);
+  double t = (f2 ? w1 : w0) + dpp_mov<0x141>(f2 ? w0 : w1);
+  t += dpp_mov<0x140>(t);
+  return xsum32(xsum16(t));
+}
 
 template <int CTRL, int ROWS>
 __device__ __forceinline__ double dpp_mov_rows(double v) {   // rows outside ROWS receive 0
@@ -611,6 +643,12 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
       for (int r = 0; r < kRingA; ++r) load_node(K[r], r);
       int m = -1, mnext = 0;
       const int nA = skip_a ? 0 : nn;   // no node steps when iteration 0's sums came from k_a0_sums
+      // RH_A_PAIR: the sums of nodes 2k and 2k + 1 reduced together (tbfly6; even ring depth)
+      constexpr bool kPair = RH_A_PAIR && (kRingA % 2 == 0);
+      double h0 = 0.0, h1 = 0.0, h2 = 0.0;   // (kPair) the even node's sums
+      // (kPair) the butterfly's lane flags: formed here, live through the node loop only
+      // (lane_here is not hoisted out of the iteration loop)
+      const Bfly6 bl = bfly6_lane(kPair ? lane_here() : 0);
       for (int n = 0; n < nA; n += kRingA) {
 #pragma unroll
         for (int r = 0; r < kRingA; ++r) {
@@ -623,6 +661,20 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
             double s0, s1, s2;
             node_sums(K[r], nr, s0, s1, s2);
             load_node(K[r], nr + kRingA);
+            if constexpr (kPair) {
+              if ((r & 1) == 0 && nr + 1 < nA) {   // uniform: held for the odd node
+                h0 = s0; h1 = s1; h2 = s2;
+                continue;
+              }
+              const int n0 = (r & 1) ? nr - 1 : nr;   // the pair's even node
+              const double tot = (r & 1) ? tbfly6(h0, h1, h2, s0, s1, s2, bl)
+                                         : tbfly6(s0, s1, s2, 0.0, 0.0, 0.0, bl);   // the last node alone
+              if ((r & 1) ? bl.vi >= 0 : (unsigned)bl.vi < 3u) {
+                double& rr = red[(n0 * 3 + bl.vi) * LW + wv_s];
+                rr = (GX && p > 0) ? rr + tot : tot;   // passes add in pass order
+              }
+              continue;
+            }
             const int ln = lane_here();
 #if RH_ABL_A_NOBFLY
             const double tot = s0 + s1 + s2;
