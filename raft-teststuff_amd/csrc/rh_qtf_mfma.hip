@@ -863,17 +863,19 @@ __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const
 
 // The pair scalars of the second-order potential (raft/helpers.py:254-291) of pair (w1, w2):
 // aux2 (w1 - w2) alpha+ and aux2 (w1 - w2) alpha-, with
-// cosh(nk (z+h)) / cosh(nk h) = alpha+ e^{nk z} + alpha- e^{-nk z}.  Shared by both GEMM kernels,
-// with contraction off, so that they produce the same bits.
-__device__ __forceinline__ void qtf_pot_scalars(double w1, double k1, double w2, double k2, double cb, double sb,
-                                                double h, double g, cd& sp, cd& sm) {
+// cosh(nk (z+h)) / cosh(nk h) = alpha+ e^{nk z} + alpha- e^{-nk z}.  t1, t2 = tanh(k1 h),
+// tanh(k2 h) (per frequency, formed once per tile); tanh(nk h) = -m / (2 + m) with
+// m = expm1(-2 nk h), accurate for small nk h.  Shared by both GEMM kernels, with contraction
+// off, so that they produce the same bits.
+__device__ __forceinline__ void qtf_pot_scalars(double w1, double k1, double t1, double w2, double k2, double t2,
+                                                double cb, double sb, double h, double g, cd& sp, cd& sm) {
 #pragma clang fp contract(off)
   sp = cd{0.0, 0.0};
   sm = cd{0.0, 0.0};
   if ((w1 != w2) && (k1 > 0) && (k2 > 0)) {
     const double kx = k1 * cb - k2 * cb, ky = k1 * sb - k2 * sb;
     const double nk = sqrt(kx * kx + ky * ky);
-    const double t1 = tanh(k1 * h), t2 = tanh(k2 * h), tnh = tanh(nk * h);
+    const double em = expm1(-2.0 * nk * h), tnh = -em / (2.0 + em);
     const double den12 = (w1 - w2) * (w1 - w2) / g - nk * tnh;
     const double den21 = (w2 - w1) * (w2 - w1) / g - nk * tnh;
     const double n12 = (k1 * k1) * (1 - t1 * t1) - 2 * k1 * k2 * (1 + t1 * t2);
@@ -924,6 +926,7 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
                                                   int mirror) {
   __shared__ double part[3][16][64];
   __shared__ double pscal[4][256];   // per pair: aux2 (w1 - w2) alpha+, ... alpha- (complex)
+  __shared__ double tkh[32];         // tanh(k h) of the tile's rows (i1) and columns (i2)
   const int lane = (int)threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int half = w / 3, dl = w % 3;
@@ -938,6 +941,32 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
   const int T2 = T1 + t;
   const int mr = lane & 15, kr = lane >> 4;
   const int i1b = 16 * T1, i2b = 16 * T2;
+  const double h = q.depth, g = q.g;
+  // The pair scalars of the second-order potential (raft/helpers.py:254-291), once per pair,
+  // before the GEMM (their transcendentals overlap the other waves' operand loads):
+  // tanh(k h) of the tile's 16 rows and 16 columns first, then one pair per thread.
+  {
+    const int x = (int)threadIdx.x;
+    if (x < 32) {
+      const int i = min(x < 16 ? i1b + x : i2b + x - 16, n2 - 1);
+      tkh[x] = tanh(q.k2[i] * h);
+    }
+    __syncthreads();
+    if (x < 256) {
+      const double bt = q.beta * kDeg2Rad, cb = cos(bt), sb = sin(bt);
+      const int i1 = min(i1b + (x >> 4), n2 - 1), i2 = min(i2b + (x & 15), n2 - 1);
+      cd sp, sm;
+#if RH_ABL_G_NOPOT   // timing ablation (wrong results)
+      sp = cd{q.w2[i1], tkh[x >> 4]}; sm = cd{q.w2[i2], tkh[16 + (x & 15)]};
+#else
+      qtf_pot_scalars(q.w2[i1], q.k2[i1], tkh[x >> 4], q.w2[i2], q.k2[i2], tkh[16 + (x & 15)], cb, sb, h, g, sp, sm);
+#endif
+      pscal[0][x] = sp.r;
+      pscal[1][x] = sp.i;
+      pscal[2][x] = sm.r;
+      pscal[3][x] = sm.i;
+    }
+  }
   const size_t step = (size_t)4 * n2p;
   const int ns = kp / 4, ns0 = 4 * ((ns / 4 + 1) / 2);
   const int k0 = half == 0 ? 0 : ns0, nk = half == 0 ? ns0 : ns - ns0;
@@ -949,7 +978,6 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
   cgemm_steps(wk.Lp + (((size_t)half * 6 + d) * kq + kr) * n2p + i1b + mr,
               wk.Rp + ((size_t)half * kq + kr) * n2p + i2b + mr, step, kq / 4, c1, c2, c3);
   const d4 mre = p1 - p2, mim = p3 - p1 - p2, cre = c1 - c2, cim = c3 - c1 - c2;
-  const double h = q.depth, g = q.g, bt = q.beta * kDeg2Rad, cb = cos(bt), sb = sin(bt);
   if (half == 1) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -957,18 +985,6 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
       part[dl][4 + r][lane] = mim[r];
       part[dl][8 + r][lane] = cre[r];
       part[dl][12 + r][lane] = cim[r];
-    }
-    // the pair scalars of the second-order potential (raft/helpers.py:254-291), once per pair:
-    // aux2 (w1 - w2) alpha+ and aux2 (w1 - w2) alpha-, with
-    // cosh(nk (z+h)) / cosh(nk h) = alpha+ e^{nk z} + alpha- e^{-nk z}
-    for (int e = (int)threadIdx.x - 192; e < 256; e += 192) {
-      const int i1 = min(i1b + (e >> 4), n2 - 1), i2 = min(i2b + (e & 15), n2 - 1);
-      cd sp, sm;
-      qtf_pot_scalars(q.w2[i1], q.k2[i1], q.w2[i2], q.k2[i2], cb, sb, h, g, sp, sm);
-      pscal[0][e] = sp.r;
-      pscal[1][e] = sp.i;
-      pscal[2][e] = sm.r;
-      pscal[3][e] = sm.i;
     }
   }
   __syncthreads();
@@ -988,6 +1004,14 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
                                part[dl][8 + r][lane], part[dl][12 + r][lane], pscal[0][e], pscal[1][e], pscal[2][e],
                                pscal[3][e], ks[(2 * d) * 256 + ek], ks[(2 * d + 1) * 256 + ek]);
     rh_c128* up = qtf + ((size_t)i1 * n2 + i2) * 6 + d;
+#if RH_ABL_G_NOSTORE   // timing ablation: no stores (wrong results)
+    if (Qf.r == 1.2345e300) st(up, Qf);
+    continue;
+#endif
+#if RH_ABL_G_NOMIRROR  // timing ablation: upper triangle only (wrong results)
+    st(up, Qf);
+    continue;
+#endif
     if (!mirror) {
       st(up, Qf);
     } else if (i1 == i2) {

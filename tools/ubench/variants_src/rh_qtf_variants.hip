@@ -104,7 +104,7 @@ __global__ __launch_bounds__(384) void k_qtf_gemm32(rh_qtf_design q, QtfWork wk,
       const int t = e >> 8, x = t >> 1, y = t & 1, el = e & 255;
       const int i1 = min(i1b + 16 * x + (el >> 4), n2 - 1), i2 = min(i2b + 16 * y + (el & 15), n2 - 1);
       cd sp, sm;
-      qtf_pot_scalars(q.w2[i1], q.k2[i1], q.w2[i2], q.k2[i2], cb, sb, h, g, sp, sm);
+      qtf_pot_scalars(q.w2[i1], q.k2[i1], tanh(q.k2[i1] * h), q.w2[i2], q.k2[i2], tanh(q.k2[i2] * h), cb, sb, h, g, sp, sm);
       pscal[t][0][el] = sp.r;
       pscal[t][1][el] = sp.i;
       pscal[t][2][el] = sm.r;
