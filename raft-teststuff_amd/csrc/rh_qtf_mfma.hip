@@ -971,12 +971,16 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
   const int ns = kp / 4, ns0 = 4 * ((ns / 4 + 1) / 2);
   const int k0 = half == 0 ? 0 : ns0, nk = half == 0 ? ns0 : ns - ns0;
   d4 p1 = {0, 0, 0, 0}, p2 = p1, p3 = p1;
+#if !RH_ABL_G_NOBIL   // timing ablation: no bilinear GEMM (wrong results)
   if (nk > 0)
     cgemm_steps(wk.L + ((size_t)d * kp + 4 * k0 + kr) * n2p + i1b + mr, wk.R + ((size_t)4 * k0 + kr) * n2p + i2b + mr,
                 step, nk, p1, p2, p3);
+#endif
   d4 c1 = {0, 0, 0, 0}, c2 = c1, c3 = c1;   // potential channel c = half
+#if !RH_ABL_G_NOPCH   // timing ablation: no potential-channel GEMM (wrong results)
   cgemm_steps(wk.Lp + (((size_t)half * 6 + d) * kq + kr) * n2p + i1b + mr,
               wk.Rp + ((size_t)half * kq + kr) * n2p + i2b + mr, step, kq / 4, c1, c2, c3);
+#endif
   const d4 mre = p1 - p2, mim = p3 - p1 - p2, cre = c1 - c2, cim = c3 - c1 - c2;
   if (half == 1) {
 #pragma unroll
