@@ -801,6 +801,9 @@ __device__ __forceinline__ void lcoef_block(const rh_qtf_design& q, const QtfWor
 #ifndef RH_QTF_PF
 #define RH_QTF_PF 4   // k-steps per operand batch (tools/ubench variant: 8)
 #endif
+#ifndef RH_QTF_CHAIN
+#define RH_QTF_CHAIN 1   // 1: the bilinear and potential-channel k-steps as one operand stream (cgemm_steps2)
+#endif
 #ifndef RH_QTF_SPLIT
 #define RH_QTF_SPLIT 0   // 1: even / odd k-steps in two accumulator sets (tools/ubench variant)
 #endif
@@ -859,6 +862,72 @@ __device__ __forceinline__ void cgemm_steps(const rh_c128* __restrict__ A, const
   p2 += q2;
   p3 += q3;
 #endif
+}
+
+// The bilinear steps (A1, B1: n1 steps, into p) and the potential channel's (A2, B2: n2 steps,
+// into c) as one operand stream: the channel's first batch is loaded while the last bilinear
+// batch runs, instead of after it.  Each accumulator sees its k-steps in the same order as with
+// two cgemm_steps calls (the same bits).  n1 and n2 are multiples of 4.
+__device__ __forceinline__ void cgemm_steps2(const rh_c128* __restrict__ A1, const rh_c128* __restrict__ B1, int n1,
+                                             const rh_c128* __restrict__ A2, const rh_c128* __restrict__ B2, int n2,
+                                             size_t step, d4& p1, d4& p2, d4& p3, d4& c1, d4& c2, d4& c3) {
+  constexpr int PF = 4;
+  const int nt = n1 + n2;
+  auto src = [&](int s, const rh_c128*& a, const rh_c128*& b) {   // operands of k-step s (uniform)
+    if (s < n1) {
+      a = A1 + s * step;
+      b = B1 + s * step;
+    } else {
+      a = A2 + (s - n1) * step;
+      b = B2 + (s - n1) * step;
+    }
+  };
+  cd a[PF], b[PF];
+  {
+    const rh_c128 *pa, *pb;
+    src(0, pa, pb);
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      a[j] = ld(pa + j * step);
+      b[j] = ld(pb + j * step);
+    }
+  }
+#pragma unroll 1
+  for (int s = 0; s < nt; s += PF) {
+    cd an[PF], bn[PF];
+    const bool more = s + PF < nt;
+    if (more) {
+      const rh_c128 *pa, *pb;
+      src(s + PF, pa, pb);
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        an[j] = ld(pa + j * step);
+        bn[j] = ld(pb + j * step);
+      }
+    }
+    if (s < n1) {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        p1 = mfma64(a[j].r, b[j].r, p1);
+        p2 = mfma64(a[j].i, b[j].i, p2);
+        p3 = mfma64(a[j].r + a[j].i, b[j].r + b[j].i, p3);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        c1 = mfma64(a[j].r, b[j].r, c1);
+        c2 = mfma64(a[j].i, b[j].i, c2);
+        c3 = mfma64(a[j].r + a[j].i, b[j].r + b[j].i, c3);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        a[j] = an[j];
+        b[j] = bn[j];
+      }
+    }
+  }
 }
 
 // The pair scalars of the second-order potential (raft/helpers.py:254-291) of pair (w1, w2):
@@ -971,15 +1040,21 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
   const int ns = kp / 4, ns0 = 4 * ((ns / 4 + 1) / 2);
   const int k0 = half == 0 ? 0 : ns0, nk = half == 0 ? ns0 : ns - ns0;
   d4 p1 = {0, 0, 0, 0}, p2 = p1, p3 = p1;
+  d4 c1 = {0, 0, 0, 0}, c2 = c1, c3 = c1;   // potential channel c = half
+#if RH_QTF_CHAIN && !RH_ABL_G_NOBIL && !RH_ABL_G_NOPCH
+  cgemm_steps2(wk.L + ((size_t)d * kp + 4 * k0 + kr) * n2p + i1b + mr, wk.R + ((size_t)4 * k0 + kr) * n2p + i2b + mr, nk,
+               wk.Lp + (((size_t)half * 6 + d) * kq + kr) * n2p + i1b + mr,
+               wk.Rp + ((size_t)half * kq + kr) * n2p + i2b + mr, kq / 4, step, p1, p2, p3, c1, c2, c3);
+#else
 #if !RH_ABL_G_NOBIL   // timing ablation: no bilinear GEMM (wrong results)
   if (nk > 0)
     cgemm_steps(wk.L + ((size_t)d * kp + 4 * k0 + kr) * n2p + i1b + mr, wk.R + ((size_t)4 * k0 + kr) * n2p + i2b + mr,
                 step, nk, p1, p2, p3);
 #endif
-  d4 c1 = {0, 0, 0, 0}, c2 = c1, c3 = c1;   // potential channel c = half
 #if !RH_ABL_G_NOPCH   // timing ablation: no potential-channel GEMM (wrong results)
   cgemm_steps(wk.Lp + (((size_t)half * 6 + d) * kq + kr) * n2p + i1b + mr,
               wk.Rp + ((size_t)half * kq + kr) * n2p + i2b + mr, step, kq / 4, c1, c2, c3);
+#endif
 #endif
   const d4 mre = p1 - p2, mim = p3 - p1 - p2, cre = c1 - c2, cim = c3 - c1 - c2;
   if (half == 1) {

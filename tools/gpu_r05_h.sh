@@ -1,15 +1,17 @@
 #!/bin/bash
-# Round 5 (h): per-rank QTF timing with pair-balanced tile blocks, a kernel trace of the rank
-# calls (which launch holds the per-rank time), then the round-5 PMC passes (FP64 counters).
+# Round 5 (h): paired phase-A butterflies, QTF pair scalars before the GEMM: full GPU suite, bench line,
+# kernel trace of the bench, then the PMC passes of the benched library (tools/gpu_pmc_r05.sh).
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r05h
 mkdir -p $OUT
 cd $R
-timeout -k 10 120 python3 tools/ubench/time_qtf.py ranks 8 > $OUT/qtf_ranks.log 2>&1 || { tail -5 $OUT/qtf_ranks.log; exit 1; }
-grep -v amdgpu.ids $OUT/qtf_ranks.log
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+rc=$?; echo "gpu tests rc=$rc"; tail -3 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 bench.py > $OUT/bench.log 2>&1 || { tail -5 $OUT/bench.log; exit 1; }
+tail -1 $OUT/bench.log | cut -c1-600
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $OUT/qprof -o run --output-format csv -- python3 $R/tools/ubench/time_qtf.py ranks 8 > $OUT/qprof.log 2>&1
-rc=$?; echo "qtf rocprof rc=$rc"; if [ $rc -ne 0 ]; then tail -5 $OUT/qprof.log; exit $rc; fi
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py > $OUT/prof.log 2>&1
+rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd $R
 bash tools/gpu_pmc_r05.sh > $OUT/pmc.log 2>&1
 rc=$?; echo "pmc rc=$rc"; tail -3 $OUT/pmc.log
