@@ -891,7 +891,7 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
         hipLaunchKernelGGL(rh::k_qtf_gemm32, dim3(nt32 * (nt32 + 1)), dim3(384), 0, s, *q, wk, qtf);
 #endif
       } else {
-        hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(2 * blocks), dim3(384), 0, s, *q, wk, qtf, t0, mirror);
+        hipLaunchKernelGGL(rh::k_qtf_gemm, dim3(6 / rh::kGD * blocks), dim3(rh::kGThreads), 0, s, *q, wk, qtf, t0, mirror);
       }
       RH_HIP(hipGetLastError());
     }

@@ -930,6 +930,60 @@ __device__ __forceinline__ void cgemm_steps2(const rh_c128* __restrict__ A1, con
   }
 }
 
+// cgemm_steps2 with a ring of operand registers instead of a double buffer: k-step s + j is
+// consumed from slot j, which is then refilled with k-step s + PF + j, so PF steps stay in flight
+// with half the operand registers (the kernel fits 128 VGPRs: four waves per SIMD).  Same MFMA
+// order per accumulator, the same bits.
+__device__ __forceinline__ void cgemm_ring2(const rh_c128* __restrict__ A1, const rh_c128* __restrict__ B1, int n1,
+                                            const rh_c128* __restrict__ A2, const rh_c128* __restrict__ B2, int n2,
+                                            size_t step, d4& p1, d4& p2, d4& p3, d4& c1, d4& c2, d4& c3) {
+  constexpr int PF = 4;
+  cd a[PF], b[PF];
+  auto mf = [&](const cd& x, const cd& y, d4& q1, d4& q2, d4& q3) {
+    q1 = mfma64(x.r, y.r, q1);
+    q2 = mfma64(x.i, y.i, q2);
+    q3 = mfma64(x.r + x.i, y.r + y.i, q3);
+  };
+  {
+    const rh_c128* pa = n1 > 0 ? A1 : A2;   // (uniform)
+    const rh_c128* pb = n1 > 0 ? B1 : B2;
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      a[j] = ld(pa + j * step);
+      b[j] = ld(pb + j * step);
+    }
+  }
+  if (n1 > 0) {
+    // bilinear k-steps; each slot is refilled with the step PF ahead, from the channel's first
+    // steps during the last batch
+#pragma unroll 1
+    for (int s = 0; s < n1 - PF; s += PF) {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        mf(a[j], b[j], p1, p2, p3);
+        a[j] = ld(A1 + (s + PF + j) * step);
+        b[j] = ld(B1 + (s + PF + j) * step);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      mf(a[j], b[j], p1, p2, p3);
+      a[j] = ld(A2 + j * step);
+      b[j] = ld(B2 + j * step);
+    }
+  }
+#pragma unroll 1
+  for (int s = 0; s < n2; s += PF) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      mf(a[j], b[j], c1, c2, c3);
+      const int r = min(s + PF + j, n2 - 1);   // (the last batch reloads the last step: not used)
+      a[j] = ld(A2 + r * step);
+      b[j] = ld(B2 + r * step);
+    }
+  }
+}
+
 // The pair scalars of the second-order potential (raft/helpers.py:254-291) of pair (w1, w2):
 // aux2 (w1 - w2) alpha+ and aux2 (w1 - w2) alpha-, with
 // cosh(nk (z+h)) / cosh(nk h) = alpha+ e^{nk z} + alpha- e^{-nk z}.  t1, t2 = tanh(k1 h),
@@ -986,23 +1040,38 @@ __device__ __forceinline__ void qtf_tile_of(int t, int nt, int& T1, int& T2) {
 
 
 // Q_d over the bilinear terms and the two potential channels for one tile and three DOFs.
-// Workgroup = 6 waves: wave w takes DOF 3 dg + (w % 3) (dg = the block's DOF half) and half
-// w / 3 of the work: the first half of K and channel +, or the second half and channel -
-// (the three waves of a half share the R tile through L1); the second half's partial sums
-// reach the first through LDS.  Blocks are (tile, DOF half) pairs, remapped so that an XCD
-// works on a contiguous run of tiles (their L rows stay in its L2).
-__global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf, int t0,
-                                                  int mirror) {
-  __shared__ double part[3][16][64];
+// Workgroup = 2 kGD waves: wave w takes DOF kGD dg + (w % kGD) (dg = the block's DOF group) and
+// half w / kGD of the work: the first half of K and channel +, or the second half and channel -
+// (the kGD waves of a half share the R tile through L1); the second half's partial sums reach
+// the first through LDS.  Blocks are (tile, DOF group) pairs, remapped so that an XCD works on a
+// contiguous run of tiles (their L rows stay in its L2).  kGD = 2: 4-wave workgroups at <= 128
+// VGPRs, so the C3 grid (325 tiles x 3) is resident at once (four per CU); with kGD = 3 the
+// 6-wave workgroups fit two per CU at three waves per SIMD, and 650 of them took two rounds.
+#ifndef RH_QTF_GDOF
+#define RH_QTF_GDOF 2   // DOFs per k_qtf_gemm workgroup: 2 (4 waves, 3 workgroups per tile) or 3 (6 waves, 2)
+#endif
+#ifndef RH_QTF_RING
+#define RH_QTF_RING 1   // 1: operand ring (cgemm_ring2), 0: double buffer (cgemm_steps2)
+#endif
+constexpr int kGD = RH_QTF_GDOF;
+constexpr int kGThreads = 128 * kGD;
+static_assert(6 % kGD == 0, "the DOFs split evenly over a tile's workgroups");
+#ifndef RH_QTF_GWPE
+#define RH_QTF_GWPE 4   // k_qtf_gemm waves per SIMD asked of the register allocator (<= 128 VGPRs)
+#endif
+__global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(RH_QTF_GWPE))) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, rh_c128* __restrict__ qtf, int t0,
+                                                        int mirror) {
+  __shared__ double part[kGD][16][64];
   __shared__ double pscal[4][256];   // per pair: aux2 (w1 - w2) alpha+, ... alpha- (complex)
   __shared__ double tkh[32];         // tanh(k h) of the tile's rows (i1) and columns (i2)
   const int lane = (int)threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int half = w / 3, dl = w % 3;
+  const int half = w / kGD, dl = w % kGD;
   const int n2 = q.n2, n2p = qtf_n2p(q), nt = n2p / 16, kp = qtf_kp(q), kq = qtf_kq(q);
   const int slot = xcd_remap((int)blockIdx.x, (int)gridDim.x);
-  const int d = 3 * (slot & 1) + dl;
-  int T1 = 0, t = t0 + (slot >> 1);   // this call's tiles: t0, t0 + 1, ... (row-major)
+  constexpr int kGB = 6 / kGD;   // workgroups per tile
+  const int d = kGD * (slot % kGB) + dl;
+  int T1 = 0, t = t0 + slot / kGB;   // this call's tiles: t0, t0 + 1, ... (row-major)
   while (t >= nt - T1) {   // block-uniform
     t -= nt - T1;
     ++T1;
@@ -1041,7 +1110,11 @@ __global__ __launch_bounds__(384) void k_qtf_gemm(rh_qtf_design q, QtfWork wk, r
   const int k0 = half == 0 ? 0 : ns0, nk = half == 0 ? ns0 : ns - ns0;
   d4 p1 = {0, 0, 0, 0}, p2 = p1, p3 = p1;
   d4 c1 = {0, 0, 0, 0}, c2 = c1, c3 = c1;   // potential channel c = half
-#if RH_QTF_CHAIN && !RH_ABL_G_NOBIL && !RH_ABL_G_NOPCH
+#if RH_QTF_CHAIN && RH_QTF_RING && !RH_ABL_G_NOBIL && !RH_ABL_G_NOPCH
+  cgemm_ring2(wk.L + ((size_t)d * kp + 4 * k0 + kr) * n2p + i1b + mr, wk.R + ((size_t)4 * k0 + kr) * n2p + i2b + mr, nk,
+              wk.Lp + (((size_t)half * 6 + d) * kq + kr) * n2p + i1b + mr,
+              wk.Rp + ((size_t)half * kq + kr) * n2p + i2b + mr, kq / 4, step, p1, p2, p3, c1, c2, c3);
+#elif RH_QTF_CHAIN && !RH_ABL_G_NOBIL && !RH_ABL_G_NOPCH
   cgemm_steps2(wk.L + ((size_t)d * kp + 4 * k0 + kr) * n2p + i1b + mr, wk.R + ((size_t)4 * k0 + kr) * n2p + i2b + mr, nk,
                wk.Lp + (((size_t)half * 6 + d) * kq + kr) * n2p + i1b + mr,
                wk.Rp + ((size_t)half * kq + kr) * n2p + i2b + mr, kq / 4, step, p1, p2, p3, c1, c2, c3);
