@@ -870,7 +870,13 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
 #endif
     if (blocks > 0 && !sep) {
       // the Kim & Yue tiles (two per workgroup) and the GEMM coefficient blocks in one launch
-      const int nkb = (blocks + rh::kLkTiles - 1) / rh::kLkTiles, nly = 18 + q->nq + q->nmq;
+      int nkb = (blocks + rh::kLkTiles - 1) / rh::kLkTiles, nly = 18 + q->nq + q->nmq;
+#if RH_ABL_LK_NOKAY    // timing ablation: no Kim & Yue tiles (wrong results)
+      nkb = 0;
+#endif
+#if RH_ABL_LK_NOCOEF   // timing ablation: no coefficient blocks (wrong results)
+      nly = 0;
+#endif
       hipLaunchKernelGGL(rh::k_qtf_lk, dim3(nkb + nbx * nly), dim3(rh::kLkThreads), 0, s, *q, wk, M66, t0, blocks,
                          nkb, bx0, nbx);
       RH_HIP(hipGetLastError());
