@@ -1,20 +1,18 @@
 #!/bin/bash
-# Round 5 (i): A/B of the tolCheck without division / square root per entry (tol), the epilogue
-# by multiplies (epi), both; then the parity subset with both.
+# Round 5 (i): 4-wave QTF GEMM workgroups with the operand ring: full GPU suite, bench line,
+# kernel trace of the bench, then the PMC passes of the benched library (tools/gpu_pmc_r05.sh).
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r05i
 mkdir -p $OUT
 cd $R
-V=$R/raft-teststuff_amd/variants
-for lib in base tol epi both base tol epi both; do
-  RAFTHIP_LIB=$V/lib_$lib.so timeout -k 10 120 python3 tools/ubench/time_solve.py $lib >> $OUT/ab.log 2>&1 || { tail -5 $OUT/ab.log; exit 1; }
-done
-for lib in base both; do
-  echo "c4 $lib" >> $OUT/ab.log
-  RAFTHIP_LIB=$V/lib_$lib.so timeout -k 10 120 python3 tools/ubench/time_c4.py 50 >> $OUT/ab.log 2>&1 || { tail -5 $OUT/ab.log; exit 1; }
-done
-grep -v amdgpu.ids $OUT/ab.log
-RAFTHIP_LIB=$V/lib_both.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sweep.py -x -v -m gpu --timeout 300 --timeout-method thread \
-  -k "fast_and_general or every_case or failed_cases or odd_grids or farm or margin or full_size" > $OUT/both_tests.log 2>&1
-rc=$?; echo "both parity rc=$rc"; tail -3 $OUT/both_tests.log
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+rc=$?; echo "gpu tests rc=$rc"; tail -3 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 bench.py > $OUT/bench.log 2>&1 || { tail -5 $OUT/bench.log; exit 1; }
+tail -1 $OUT/bench.log | cut -c1-600
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py > $OUT/prof.log 2>&1
+rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+cd $R
+bash tools/gpu_pmc_r05.sh > $OUT/pmc.log 2>&1
+rc=$?; echo "pmc rc=$rc"; tail -3 $OUT/pmc.log
 exit $rc
