@@ -394,14 +394,15 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
     dt = time.perf_counter() - t0
     dt_serial = dt                         # one GPU: a QTF at a time; N GPUs: each QTF tile-sharded
     if True:
-        # The QTF stream pipelined over two HIP streams, each with its own tables and workspace
-        # (QtfDevice): one QTF's short table and coefficient launches run beside the other's
-        # GEMM.  On N GPUs every rank runs its own stream of QTFs (weak scaling, no exchange:
+        # The QTF stream pipelined over RAFT_BENCH_QTF_STREAMS HIP streams (default 3: with the
+        # 4-wave GEMM, 3 streams 1.13e9 against 1.05e9 pairs/s for 2), each with its own tables and
+        # workspace (QtfDevice): one QTF's short table and coefficient launches run beside the
+        # others' GEMMs.  On N GPUs every rank runs its own stream of QTFs (weak scaling, no exchange:
         # QTFs of different headings / designs are independent); the tile-sharded QTF timed
         # above is reported beside it.  The pipelined outputs equal a whole QTF bit for bit.
         if world > 1:
             q = qd.qtf(dd.w, X, M66)      # this GPU's whole QTF (the check below)
-        nqs = int(os.environ.get("RAFT_BENCH_QTF_STREAMS", "2"))
+        nqs = int(os.environ.get("RAFT_BENCH_QTF_STREAMS", "3"))
         qds = [qd] + [QtfDevice(f, w2, k2, 0.0, device) for _ in range(nqs - 1)]
         streams = [stream] + [torch.cuda.Stream(device) for _ in range(nqs - 1)]
         outs = [torch.empty_like(q) for _ in range(nqs)]
