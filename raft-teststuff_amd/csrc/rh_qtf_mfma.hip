@@ -1056,6 +1056,7 @@ __device__ __forceinline__ void qtf_tile_of(int t, int nt, int& T1, int& T2) {
 constexpr int kGD = RH_QTF_GDOF;
 constexpr int kGThreads = 128 * kGD;
 static_assert(6 % kGD == 0, "the DOFs split evenly over a tile's workgroups");
+static_assert(kGThreads >= 256, "the pair scalars: one pair per thread of the 16 x 16 tile");
 #ifndef RH_QTF_GWPE
 #define RH_QTF_GWPE 4   // k_qtf_gemm waves per SIMD asked of the register allocator (<= 128 VGPRs)
 #endif
