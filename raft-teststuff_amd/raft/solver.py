@@ -171,10 +171,9 @@ def balanced_order(cases, head, nxcd=8):
     collects the long cases, and within a slice the long ones are dispatched first.  The
     order changes placement only, never results.  Measured on the C2 bench batch (512
     cases, 2 per CU): the last CU finishes after 9.5 instead of 10.5 case-iterations
-    (tools/ubench/makespan.py).  The re-deal keeps the (design, heading) order of the pair's
-    cases (periods descending within each table), and a pair whose cases span more than two
-    wave tables is not re-dealt at all: its slices already hold whole tables with their full
-    period mix.  Sorting the whole pair by period had put the cases of ~12 designs (12 wave
+    (tools/ubench/makespan.py).  A pair whose cases span more than two wave tables is not
+    re-dealt: its slices already hold whole tables with their full period mix.  Sorting such
+    a pair by period had put the cases of ~12 designs (12 wave
     tables of 2.5 MB) on an XCD at once in the C5 sweep: its L2 hit rate fell to 47 % and a
     2000-case launch fetched 25 GB (profiles/r05_v9/c5_order.txt)."""
     order = np.lexsort((-cases.Tp, head, cases.design_idx))
@@ -188,6 +187,7 @@ def balanced_order(cases, head, nxcd=8):
         tables = np.unique(cases.design_idx[seg].astype(np.int64) * (int(np.max(head)) + 1) + head[seg])
         if len(tables) > 2:
             continue
+        seg = seg[np.argsort(-cases.Tp[seg], kind="stable")]
         na, nb = a1 - a0, a2 - a1
         m = min(na, nb)
         to_a = np.zeros(na + nb, dtype=bool)
