@@ -34,7 +34,7 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_v9", "pmc_summary.json")
 
 def pmc_section(workload):
     """The per-kernel PMC records of one workload ("solve", "qtf", "c4") from PMC_SUMMARY
-    (a summary with one section per workload, tools/gpu_pmc_r04.sh; older flat summaries
+    (a summary with one section per workload, tools/gpu.sh pmc; older flat summaries
     serve every workload), or None."""
     try:
         with open(PMC_SUMMARY) as fh:

@@ -242,6 +242,19 @@ int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int 
                         const int* design_idx, const int* head, const double* zeta,
                         const double* B_drag, const double* Bmat, rh_c128* Xi, rh_stream stream);
 
+/* rh_heading_response with the Bmat row stride explicit and an extra excitation:
+ * Xi_h = Z^-1 (zeta_h finer_h + zeta_h sum_n T_n Bmat_n uhat_h,n + fext_h), the F_wave of
+ * raft/raft_model.py:1061 with the second-order force Fhydro_2nd[ih] of that sea state
+ * (:1059-1060, an external .12d QTF; FOWT.calcHydroForce_2ndOrd).  bmat_nn: the node stride of
+ * Bmat (0 = the largest nn of the designs passed; RH_EINVAL when smaller than that), so a call
+ * over a subset of the designs of the rh_solve_cases call that wrote Bmat reads it correctly.
+ * fext: [ncase][6][nw] or NULL.  A case whose design or heading index is out of range gets NaN
+ * rows (no table is read). */
+int rh_heading_response_ext(rh_ctx* ctx, const rh_design* designs, int ndesign, int ncase,
+                            const int* design_idx, const int* head, const double* zeta,
+                            const double* B_drag, const double* Bmat, int bmat_nn, const rh_c128* fext,
+                            rh_c128* Xi, rh_stream stream);
+
 /* Wave excitation of solved cases with the final linearisation, without the solve:
  * F = zeta_h finer_h + zeta_h sum_n T_n Bmat_n uhat_h,n  -- F_wave of the system solve of an
  * array (raft/raft_model.py:1049-1061).  Arguments as rh_heading_response; F out: [ncase][6][nw]. */
@@ -442,6 +455,15 @@ int rh_qtf_hermitian_fill(rh_ctx* ctx, int n2, rh_c128* qtf, rh_stream stream);
  * (uniform spacing dw) -> f [6][nw] (already shifted by one bin), f_mean [6]. */
 int rh_force_2nd(rh_ctx* ctx, int n2, const double* w2, const rh_c128* qtf, int nw, const double* w, double dw,
                  const double* S0, double* f, double* f_mean, rh_stream stream);
+
+/* rh_force_2nd for a batch of sea states in one launch (the per-case second-order loads of a
+ * batched solve, Model.analyzeCasesBatch): case c uses the QTF qidx[c] of the stack
+ * qtf [nq][n2][n2][6] (qidx: device [ncase], or NULL for QTF 0) and its spectrum S0 [c][nw];
+ * f out: [ncase][6][nw] complex with zero imaginary part (the fext rows of rh_cases, the same
+ * values as rh_force_2nd bit for bit), f_mean [ncase][6].  A qidx outside [0, nq) gives NaN. */
+int rh_force_2nd_batch(rh_ctx* ctx, int ncase, int n2, const double* w2, const rh_c128* qtf, int nq,
+                       const int* qidx, int nw, const double* w, double dw, const double* S0, rh_c128* f,
+                       double* f_mean, rh_stream stream);
 
 /* Second-order force spectrum, 'spectrum' interpolation mode (raft/raft_fowt.py:1760-1784,
  * 1809-1810): S = interp(w2, w, S0) (0 outside w), force spectrum on the QTF grid

@@ -528,12 +528,13 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   return designs_used(ctx, s);
 }
 
-int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int ncase, const int* design_idx,
-                        const int* head, const double* zeta, const double* B_drag, const double* Bmat, rh_c128* Xi,
-                        rh_stream stream) {
+int rh_heading_response_ext(rh_ctx* ctx, const rh_design* designs, int ndesign, int ncase, const int* design_idx,
+                            const int* head, const double* zeta, const double* B_drag, const double* Bmat, int bmat_nn,
+                            const rh_c128* fext, rh_c128* Xi, rh_stream stream) {
   if (!ctx || !designs || !design_idx || !head || !zeta || !B_drag || !Bmat || !Xi)
     return fail(RH_EINVAL, "rh_heading_response: null argument");
   if (ncase <= 0) return ncase == 0 ? RH_OK : fail(RH_EINVAL, "ncase=%d", ncase);
+  if (ndesign < 1) return fail(RH_EINVAL, "rh_heading_response: ndesign=%d", ndesign);
   const int nw = designs[0].nw;
   int nnmax = 0;
   for (int i = 0; i < ndesign; ++i) {
@@ -541,14 +542,24 @@ int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int 
     if (designs[i].nw != nw) return fail(RH_EINVAL, "rh_heading_response: all designs must share nw");
     if (designs[i].nn > nnmax) nnmax = designs[i].nn;
   }
+  if (bmat_nn == 0) bmat_nn = nnmax;
+  if (bmat_nn < nnmax)
+    return fail(RH_EINVAL, "rh_heading_response: Bmat row stride %d < %d nodes of a design passed", bmat_nn, nnmax);
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
-  rh::HeadArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, B_drag, Bmat, Xi, nullptr, nnmax, ndesign};
+  rh::HeadArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, B_drag, Bmat, Xi, nullptr, bmat_nn, ndesign, fext};
   const size_t smem = sizeof(double) * (size_t)(nnmax * 9 + 36 + 108);
   dim3 grid((nw + kThreads - 1) / kThreads, ncase);
   hipLaunchKernelGGL(rh::k_heading_resp, grid, dim3(kThreads), smem, s, a);
   return designs_used(ctx, s);
+}
+
+int rh_heading_response(rh_ctx* ctx, const rh_design* designs, int ndesign, int ncase, const int* design_idx,
+                        const int* head, const double* zeta, const double* B_drag, const double* Bmat, rh_c128* Xi,
+                        rh_stream stream) {
+  return rh_heading_response_ext(ctx, designs, ndesign, ncase, design_idx, head, zeta, B_drag, Bmat, 0, nullptr, Xi,
+                                 stream);
 }
 
 int rh_wave_excitation(rh_ctx* ctx, const rh_design* designs, int ndesign, int ncase, const int* design_idx,
@@ -566,7 +577,7 @@ int rh_wave_excitation(rh_ctx* ctx, const rh_design* designs, int ndesign, int n
   RH_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
   if (int r = stage_designs(ctx, designs, ndesign, s)) return r;
-  rh::HeadArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, nullptr, Bmat, nullptr, F, nnmax, ndesign};
+  rh::HeadArgs a{staged_designs(ctx), ncase, design_idx, head, zeta, nullptr, Bmat, nullptr, F, nnmax, ndesign, nullptr};
   const size_t smem = sizeof(double) * (size_t)(nnmax * 9 + 36 + 108);
   dim3 grid((nw + kThreads - 1) / kThreads, ncase);
   hipLaunchKernelGGL(rh::k_heading_resp, grid, dim3(kThreads), smem, s, a);
@@ -964,6 +975,20 @@ int rh_force_2nd(rh_ctx* ctx, int n2, const double* w2, const rh_c128* qtf, int 
   if (n2 < 2 || nw < 2 || !(dw > 0)) return fail(RH_EINVAL, "rh_force_2nd: bad sizes");
   RH_HIP(hipSetDevice(ctx->device));
   hipLaunchKernelGGL(rh::k_force2nd, dim3(nw), dim3(256), 0, (hipStream_t)stream, n2, w2, qtf, nw, w, dw, S0, f, f_mean);
+  RH_HIP(hipGetLastError());
+  return RH_OK;
+}
+
+int rh_force_2nd_batch(rh_ctx* ctx, int ncase, int n2, const double* w2, const rh_c128* qtf, int nq, const int* qidx,
+                       int nw, const double* w, double dw, const double* S0, rh_c128* f, double* f_mean,
+                       rh_stream stream) {
+  if (!ctx || !w2 || !qtf || !w || !S0 || !f || !f_mean) return fail(RH_EINVAL, "rh_force_2nd_batch: null argument");
+  if (ncase < 0 || n2 < 2 || nw < 2 || nq < 1 || !(dw > 0)) return fail(RH_EINVAL, "rh_force_2nd_batch: bad sizes");
+  if (ncase == 0) return RH_OK;
+  if (ncase > 65535) return fail(RH_EINVAL, "rh_force_2nd_batch: ncase=%d > 65535 per call", ncase);
+  RH_HIP(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(rh::k_force2nd_batch, dim3(nw, ncase), dim3(256), 0, (hipStream_t)stream, n2, w2, qtf, qidx, nq,
+                     nw, w, dw, S0, f, f_mean);
   RH_HIP(hipGetLastError());
   return RH_OK;
 }

@@ -483,7 +483,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
     }
   }
   // a case that stopped on a NaN or a singular Z has no response (the reference raises there,
-  // raft/raft_model.py:957): NaN Xi, PSD, RAO and std, as k_solve_lds writes them
+  // raft/raft_model.py:957): NaN Xi, F_wave, PSD, RAO and std, as k_solve_lds writes them
   if (status == RH_CASE_NAN || status == RH_CASE_SINGULAR) {   // uniform
 #pragma unroll 1
     for (int j = 0; j < NB; ++j) {
@@ -492,6 +492,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_solve_cases(CaseArgs a) {
 #pragma unroll 1
       for (int c = 0; c < 6; ++c) {
         if (Xo) st(Xo + c * nw + b, mk(NAN, NAN));
+        if (a.o.F_wave) st(a.o.F_wave + ((size_t)ic * 6 + c) * nw + b, mk(NAN, NAN));   // no excitation either
         if (a.o.psd) a.o.psd[((size_t)ic * 6 + c) * nw + b] = NAN;
         if (a.o.rao) st(a.o.rao + ((size_t)ic * 6 + c) * nw + b, mk(NAN, NAN));
       }
@@ -545,17 +546,29 @@ struct HeadArgs {
   const double* Bmat;      // [ncase][bmat_nn][9]
   rh_c128* Xi;
   rh_c128* F;             // non-NULL: store the wave excitation only (no solve)
-  int bmat_nn;            // node stride of Bmat: the largest nn of the call's designs
+  int bmat_nn;            // node stride of Bmat (rh_heading_response_ext's bmat_nn)
   int ndesign;            // designs[] entries: a design index outside [0, ndesign) is not read
+  const rh_c128* fext;    // [ncase][6][nw] added to the excitation (Fhydro_2nd, raft/raft_model.py:1061), or NULL
 };
 
 __global__ __launch_bounds__(kThreads, 2) void k_heading_resp(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int ic = blockIdx.y;
   const int di = a.design_idx[ic];
-  if (di < 0 || di >= a.ndesign) return;   // uniform: a bad index from the caller writes nothing
+  if (di < 0 || di >= a.ndesign || a.head[ic] < 0 || a.head[ic] >= a.designs[di].d.nhead) {
+    // uniform per block: a bad design or heading index from the caller reads no table and
+    // leaves NaN in this case's rows (never plausible-looking stale memory)
+    const int nw0 = a.designs[0].d.nw;
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nw0) {
+      const double nan = __builtin_nan("");
+      rh_c128* out = a.F ? a.F : a.Xi;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) out[((size_t)ic * 6 + c) * nw0 + b] = rh_c128{nan, nan};
+    }
+    return;
+  }
   const rh_design& d = a.designs[di].d;
-  if (a.head[ic] < 0 || a.head[ic] >= d.nhead) return;   // ... nor does a heading not tabulated
   const int nw = d.nw, nn = d.nn;
   double* bm = smem;
   double* bd = bm + 9 * nn;
@@ -574,6 +587,10 @@ __global__ __launch_bounds__(kThreads, 2) void k_heading_resp(HeadArgs a) {
   drag_exc_bin(d.node, nn, bm, Uh, nw, b, F);
 #pragma unroll
   for (int c = 0; c < 6; ++c) F[c] = add(scl(ld(Fe + c * nw + b), z), scl(F[c], z));
+  if (a.fext) {
+#pragma unroll
+    for (int c = 0; c < 6; ++c) F[c] = add(F[c], ld(a.fext + ((size_t)ic * 6 + c) * nw + b));
+  }
   if (a.F) {              // F_wave of raft/raft_model.py:1049-1061 for the system solve
 #pragma unroll
     for (int c = 0; c < 6; ++c) st(a.F + ((size_t)ic * 6 + c) * nw + b, F[c]);

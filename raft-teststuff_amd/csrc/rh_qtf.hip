@@ -917,12 +917,15 @@ __device__ __forceinline__ bool grid_cell(const double* g, int n, double x, int&
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_force2nd(int n2, const double* __restrict__ w2, const rh_c128* __restrict__ qtf,
-                                                   int nw, const double* __restrict__ w, double dw,
-                                                   const double* __restrict__ S0, double* __restrict__ fout,
-                                                   double* __restrict__ fmean) {
+// One difference-frequency index mu (0 = mean drift, 1..nw-1) of one (QTF, spectrum) pair, one
+// 256-thread block.  kCplx: f is complex [6][nw] (the fext rows of a batched solve, imaginary part
+// 0), else real [6][nw].  The same arithmetic in both forms, so the bits agree.
+template <bool kCplx>
+__device__ __forceinline__ void force2nd_block(int mu, int n2, const double* __restrict__ w2,
+                                               const rh_c128* __restrict__ qtf, int nw, const double* __restrict__ w,
+                                               double dw, const double* __restrict__ S0, double* __restrict__ fout,
+                                               double* __restrict__ fmean) {
   __shared__ double red[4][6];
-  const int mu = blockIdx.x;            // 0 = mean drift, 1..nw-1 difference frequencies
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   double acc[6] = {0, 0, 0, 0, 0, 0};
   for (int i = tid; i + mu < nw; i += 256) {
@@ -962,13 +965,46 @@ __global__ __launch_bounds__(256) void k_force2nd(int n2, const double* __restri
   __syncthreads();
   if (tid < 6) {
     const double s = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-    if (mu == 0) {
-      fmean[tid] = 2 * s * dw;
-      fout[(size_t)tid * nw + (nw - 1)] = 0.0;           // last bin has no difference frequency
+    const int bin = mu == 0 ? nw - 1 : mu - 1;            // shifted by one bin (:1809-1810)
+    const double val = mu == 0 ? 0.0 : 4 * sqrt(s) * dw;  // the last bin has no difference frequency
+    if (mu == 0) fmean[tid] = 2 * s * dw;
+    if (kCplx) {
+      fout[2 * ((size_t)tid * nw + bin)] = val;
+      fout[2 * ((size_t)tid * nw + bin) + 1] = 0.0;
     } else {
-      fout[(size_t)tid * nw + (mu - 1)] = 4 * sqrt(s) * dw;   // shifted by one bin (:1809-1810)
+      fout[(size_t)tid * nw + bin] = val;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void k_force2nd(int n2, const double* __restrict__ w2, const rh_c128* __restrict__ qtf,
+                                                   int nw, const double* __restrict__ w, double dw,
+                                                   const double* __restrict__ S0, double* __restrict__ fout,
+                                                   double* __restrict__ fmean) {
+  force2nd_block<false>(blockIdx.x, n2, w2, qtf, nw, w, dw, S0, fout, fmean);
+}
+
+// Batched form: block (mu, case); case c uses QTF qidx[c] of the stack qtf [nq][n2][n2][6] (qidx
+// NULL: QTF 0) and spectrum S0[c] [nw]; f [ncase][6][nw] complex, f_mean [ncase][6].
+__global__ __launch_bounds__(256) void k_force2nd_batch(int n2, const double* __restrict__ w2,
+                                                         const rh_c128* __restrict__ qtf, const int* __restrict__ qidx,
+                                                         int nq, int nw, const double* __restrict__ w, double dw,
+                                                         const double* __restrict__ S0, rh_c128* __restrict__ f,
+                                                         double* __restrict__ fmean) {
+  const int c = blockIdx.y;
+  const int qi = qidx ? qidx[c] : 0;
+  if (qi < 0 || qi >= nq) {               // uniform per block: a bad index gives NaN, never a stray read
+    if (threadIdx.x < 6) {
+      const double nan = __builtin_nan("");
+      const int mu = blockIdx.x;
+      const int bin = mu == 0 ? nw - 1 : mu - 1;
+      f[((size_t)c * 6 + threadIdx.x) * nw + bin] = rh_c128{nan, nan};
+      if (mu == 0) fmean[(size_t)c * 6 + threadIdx.x] = nan;
+    }
+    return;
+  }
+  force2nd_block<true>(blockIdx.x, n2, w2, qtf + (size_t)qi * n2 * n2 * 6, nw, w, dw, S0 + (size_t)c * nw,
+                       reinterpret_cast<double*>(f + (size_t)c * 6 * nw), fmean + (size_t)c * 6);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -1129,9 +1129,18 @@ __global__ __launch_bounds__(LT, LT >= 256 ? 512 / LT : 2) void k_solve_lds(Case
     }
   }
   // A case that stopped on a NaN or a singular Z has no response (the reference raises there,
-  // raft/raft_model.py:957): its Xi, PSD, RAO and std are NaN, as in k_solve_cases.  (The
+  // raft/raft_model.py:957): its Xi, F_wave, PSD, RAO and std are NaN, as in k_solve_cases.  (The
   // entries of its last iterate were stored only where they passed their test.)
   const bool failed = status == RH_CASE_NAN || status == RH_CASE_SINGULAR;   // uniform
+  if (failed && a.o.F_wave) {   // nor an excitation: an array solve of it gives NaN, not stale memory
+#pragma unroll 1
+    for (int j = 0; j < NBT; ++j) {
+      const int b = tid + LT * j;
+      if (b >= nw) continue;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) st(a.o.F_wave + ((size_t)ic * 6 + c) * nw + b, mk(NAN, NAN));
+    }
+  }
   // (kStatsC: phase C formed PSD / RAO / the RMS sums of a case that did not fail)
   double ss[6] = {0, 0, 0, 0, 0, 0};
   if (!kStatsC || failed) {

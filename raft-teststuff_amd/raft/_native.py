@@ -90,6 +90,8 @@ def lib():
                                    ctypes.POINTER(RhSolveOut), _p],
                 "rh_heading_response": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.c_int, _p, _p, _p, _p,
                                         _p, _p, _p],
+                "rh_heading_response_ext": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, ctypes.c_int, _p, _p, _p,
+                                            _p, _p, ctypes.c_int, _p, _p, _p],
                 "rh_linearize": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, _p, _p, _p, _p, _p, _p],
                 "rh_drag_excitation": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, _p, _p, _p, _p],
                 "rh_lin_partial_sums": [_p, ctypes.POINTER(RhDesign), ctypes.c_int, _p, _p, ctypes.c_int, ctypes.c_int,
@@ -121,6 +123,8 @@ def lib():
                 "rh_set_qtf_path": [_p, ctypes.c_int],
                 "rh_qtf_hankel": [_p, ctypes.c_int, _p, ctypes.c_int, _p, _p, _p],
                 "rh_force_2nd": [_p, ctypes.c_int, _p, _p, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p],
+                "rh_force_2nd_batch": [_p, ctypes.c_int, ctypes.c_int, _p, _p, ctypes.c_int, _p, ctypes.c_int, _p,
+                                       ctypes.c_double, _p, _p, _p, _p],
                 "rh_force_2nd_spectrum": [_p, ctypes.c_int, _p, _p, ctypes.c_int, _p, ctypes.c_double, _p, _p, _p, _p,
                                           _p],
                 "rh_prep_designs": [ctypes.c_int, _p, _p, ctypes.c_int, _p, _p, ctypes.c_int, ctypes.POINTER(_p)],

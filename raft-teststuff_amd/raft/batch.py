@@ -17,7 +17,8 @@ import numpy as np
 
 from .hydro_math import get_from_dict
 from .model import Model
-from .solver import CaseSet, solve_batch
+from .second_order import solve_batch_2nd
+from .solver import CaseSet
 
 
 class DesignBatch:
@@ -48,6 +49,11 @@ class DesignBatch:
         if len(statics) != len(designs):
             raise ValueError("statics: one dict for all designs or one per design")
         self._prepared = None
+        if native or specs is not None or light:
+            for d in designs:
+                if get_from_dict((d or {}).get("platform") or {}, "potSecOrder", dtype=int, default=0) > 0:
+                    raise NotImplementedError("DesignBatch: second-order loads (potSecOrder > 0) need the full design "
+                                              "models (native=False, light=False): the QTFs are built there")
         if native or specs is not None:
             self.models = self._native(designs, statics, r6, device, pool, specs, threads)
         else:
@@ -167,19 +173,22 @@ class DesignBatch:
         design's shared node and wave tables.  Such cases need the full design models
         (native=False, light=False): the rotors are built there."""
         if isinstance(cases, CaseSet):
-            return solve_batch(self.dds, cases, self.nIter, self.XiStart, tol, want=want, prepared=prepared)
+            return solve_batch_2nd(self.dds, self.fowts, cases, self.nIter, self.XiStart, tol, want=want,
+                                   prepared=prepared)
         cs = self.case_set(design_idx, cases)
         aero = self._aero_views(np.asarray(design_idx, dtype=np.int64), cases)
         if aero is None:
-            return solve_batch(self.dds, cs, self.nIter, self.XiStart, tol, want=want, prepared=prepared)
-        views, idx = aero
+            return solve_batch_2nd(self.dds, self.fowts, cs, self.nIter, self.XiStart, tol, want=want,
+                                   prepared=prepared)
+        views, idx, owners = aero
         cs = CaseSet(idx, cs.heading, cs.spectrum, cs.Hs, cs.Tp, cs.gamma)
-        return solve_batch(views, cs, self.nIter, self.XiStart, tol, want=want)
+        return solve_batch_2nd(views, owners, cs, self.nIter, self.XiStart, tol, want=want)
 
     _WAVE_KEYS = ("wave_spectrum", "wave_period", "wave_height", "wave_heading", "wave_gamma", "iCase")
 
     def _aero_views(self, design_idx, cases):
-        """(views, per-case view index) when some case has an operating rotor, else None."""
+        """(views, per-case view index, the FOWT of each view) when some case has an operating
+        rotor, else None."""
         import torch
         from .model import CaseMB
         from .prep import linear_matrices
@@ -193,6 +202,7 @@ class DesignBatch:
                                               "(native=False, light=False) to build the rotors")
             return None
         views = list(self.dds)
+        owners = list(self.fowts)
         idx = design_idx.astype(np.int32).copy()
         made = {}
         heads = np.unique([float(np.atleast_1d(c.get("wave_heading", 0))[0]) for c in cases]) * np.pi / 180.0
@@ -208,9 +218,10 @@ class DesignBatch:
                 f64 = dict(dtype=torch.float64, device=self.dds[d].device)
                 self.dds[d].ensure_headings(heads)
                 views.append(CaseMB(self.dds[d], torch.tensor(M, **f64).contiguous(), torch.tensor(B, **f64).contiguous()))
+                owners.append(fowt)
                 made[key] = len(views) - 1
             idx[i] = made[key]
-        return views, idx
+        return views, idx, owners
 
 
 def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, pool=None, chunks=4, tol=0.01,

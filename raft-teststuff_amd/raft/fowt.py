@@ -468,6 +468,11 @@ class FOWT:
         dd = self.device_design()
         beta = float(self.beta[waveHeadInd])
         self.heads_2nd = [beta]
+        if waveHeadInd not in (0, -1):
+            # the reference's qtf has one heading and is indexed with waveHeadInd
+            # (raft/raft_fowt.py:1442, 1456): every other sea state raises
+            from .second_order import qtf_index_error
+            raise qtf_index_error(waveHeadInd)
         qd = self._qtf_device(beta)
         if Xi0 is None:
             X = torch.zeros([6, self.nw], dtype=torch.complex128, device=dd.device)

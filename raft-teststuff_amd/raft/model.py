@@ -17,6 +17,7 @@ import numpy as np
 from . import _native as N
 from .fowt import FOWT, mooring_outputs
 from .hydro_math import DEG2RAD, get_from_dict, wave_numbers
+from .second_order import file_qtf_forces, qtf_index_error, solve_batch_2nd
 from .solver import CaseSet, solve_batch
 
 
@@ -496,12 +497,19 @@ class Model:
         for every extra sea state of the batch); Xi_waves [n, nW+1, 6, nw] holds them in the
         reference's layout (nW = the batch's largest sea-state count, rows of absent sea states
         and the last row zero) and psd / std sum over the sea states (getPSD / getRMS).
+        Second-order loads (raft/raft_model.py:899-1083) as solveDynamics applies them
+        (raft/second_order.py): potSecOrder=2 adds the .12d QTF's force of every sea state
+        (f2nd_mean [n,6] of sea state 0, f2nd_mean_waves [n,nW,6] with several sea states);
+        potSecOrder=1 solves twice, the QTF of each converged case's RAO between the passes
+        (iters_pair [n,2]); several sea states per case raise the reference's IndexError (Q8).
         Arrays (nFOWT > 1) go through analyzeArrayBatch: Xi [n,6N,nw], iters [n,N], ..."""
         if self.nFOWT != 1:
             return self.analyzeArrayBatch(cases, tol=tol, host=host)
         fowt = self.fowtList[0]
         seas = [self._case_sea_states(c) for c in cases]
         nws = np.array([len(s[0]) for s in seas], dtype=np.int64)
+        if fowt.potSecOrder == 1 and len(cases) and nws.max() > 1:
+            raise qtf_index_error(1)      # the slender-body QTF of sea state 1 (SURVEY.md Q8)
         hd, sp, Hs, Tp, gm = ([s[k][0] for s in seas] for k in range(5))
         multi = len(cases) > 0 and nws.max() > 1
         want_fp = tuple(want) + (("Bmat", "B_drag") if multi else ())
@@ -511,7 +519,7 @@ class Model:
         if not any(aero):
             views = [fowt.device_design()]
             cs = CaseSet(np.zeros(len(cases), dtype=np.int32), hd, sp, Hs, Tp, gm)
-            res = solve_batch(views, cs, self.nIter, self.XiStart, tol, want=want_fp)
+            res = solve_batch_2nd(views, [fowt], cs, self.nIter, self.XiStart, tol, want=want_fp)
             if multi:
                 self._extra_sea_states(res, views, cs.design_idx, seas, nws, want)
             return res.host() if host else res
@@ -531,7 +539,7 @@ class Model:
                 views.append(CaseMB(base, torch.tensor(M, **f64).contiguous(), torch.tensor(B, **f64).contiguous()))
                 idx[i] = len(views) - 1
         cs = CaseSet(idx, hd, sp, Hs, Tp, gm)
-        res = solve_batch(views, cs, self.nIter, self.XiStart, tol, want=want_fp)
+        res = solve_batch_2nd(views, [fowt] * len(views), cs, self.nIter, self.XiStart, tol, want=want_fp)
         if multi:
             self._extra_sea_states(res, views, idx, seas, nws, want)
         return res.host() if host else res
@@ -568,25 +576,36 @@ class Model:
         ext = [(i, h) for i in range(n) for h in range(1, int(nws[i]))]
         ci = np.array([i for i, _ in ext], dtype=np.int64)
         pick = lambda k: [seas[i][k][h] for i, h in ext]   # noqa: E731
-        heads = dd.ensure_headings(np.array(pick(0), dtype=float) * DEG2RAD)
+        betas = np.array(pick(0), dtype=float) * DEG2RAD
+        heads = dd.ensure_headings(betas)
         ctx, s = N.context(self.device), N.stream_handle(torch, dev)
         m = len(ext)
+        S = torch.empty([m, nw], **f64)
         zeta = torch.empty([m, nw], **f64)
         spec = torch.tensor([N.SPECTRUM_CODES[x] for x in pick(1)], **i32)
         Hs, Tp, gm = (torch.tensor(pick(k), **f64) for k in (2, 3, 4))
         N.check(N.lib().rh_sea_state(ctx, m, nw, N.ptr(dd.w), float(dd.dw), N.ptr(spec), N.ptr(Hs), N.ptr(Tp),
-                                     N.ptr(gm), None, N.ptr(zeta), s), "rh_sea_state")
+                                     N.ptr(gm), N.ptr(S), N.ptr(zeta), s), "rh_sea_state")
         sel = torch.tensor(ci, dtype=torch.long, device=dev)
         bdrag = res["B_drag"].index_select(0, sel).contiguous()
         bmat = res["Bmat"].index_select(0, sel).contiguous()
         XiE = torch.empty([m, 6, nw], dtype=torch.complex128, device=dev)
+        fext = None
+        fowt = self.fowtList[0]
+        if fowt.potSecOrder == 2:      # the .12d QTF's force of each further sea state (:1059-1061)
+            fext, fm = file_qtf_forces(dd, fowt, betas, S)
+            fw = torch.zeros([n, nwm, 6], **f64)
+            fw[:, 0] = res["f2nd_mean"]
+            fw[sel, torch.tensor([h for _, h in ext], dtype=torch.long, device=dev)] = fm
+            res["f2nd_mean_waves"] = fw
         arr = (N.RhDesign * len(views))(*[v.struct() for v in views])
         # (the index tensors are held in names: a temporary freed before the call returns would
         # hand its block to the next allocation, and the kernel would read the other array)
         didx = torch.tensor(np.asarray(idx)[ci], **i32)
         hidx = torch.tensor(heads, **i32)
-        N.check(N.lib().rh_heading_response(ctx, arr, len(views), m, N.ptr(didx), N.ptr(hidx), N.ptr(zeta),
-                                            N.ptr(bdrag), N.ptr(bmat), N.ptr(XiE), s), "rh_heading_response")
+        N.check(N.lib().rh_heading_response_ext(ctx, arr, len(views), m, N.ptr(didx), N.ptr(hidx), N.ptr(zeta),
+                                                N.ptr(bdrag), N.ptr(bmat), int(bmat.shape[1]), N.ptr(fext), N.ptr(XiE),
+                                                s), "rh_heading_response_ext")
         Xw = torch.zeros([n, nwm + 1, 6, nw], dtype=torch.complex128, device=dev)
         Xw[:, 0] = res["Xi"]
         Xw[sel, torch.tensor([h for _, h in ext], dtype=torch.long, device=dev)] = XiE
@@ -613,34 +632,46 @@ class Model:
     def prepareArrayBatch(self, cases):
         """The per-batch inputs of analyzeArrayBatch resident on the device: the (case, FOWT)
         case table with its wave tables (solver.prepare_batch), the FOWT descriptors and the
-        array stiffness.  Reusable for repeated solves of the same sea states."""
+        array stiffness.  Reusable for repeated solves of the same sea states.  Every heading of
+        every sea state is tabulated here, before any descriptor is made."""
         import torch
         nf, n = self.nFOWT, len(cases)
         dds = [f.device_design() for f in self.fowtList]   # (node counts may differ: Bmat rows padded to the largest)
         seas = [self._case_sea_states(c) for c in cases]
-        if any(len(x[0]) != 1 for x in seas):
-            raise NotImplementedError("analyzeArrayBatch: one sea state per case")
+        nws = np.array([len(x[0]) for x in seas], dtype=np.int64)
+        if any(f.potSecOrder == 1 for f in self.fowtList):
+            raise NotImplementedError("analyzeArrayBatch: potSecOrder=1 in a coupled array; the reference adds the "
+                                      "force to F_lin[i1:i2] of the whole system (raft/raft_model.py:988, SURVEY.md Q5)")
+        allh = np.unique(np.concatenate([np.asarray(x[0], dtype=float) for x in seas])) * DEG2RAD if n else []
+        for d in dds:
+            d.ensure_headings(allh)
         hd, sp, Hs, Tp, gm = ([x[k][0] for x in seas] for k in range(5))
         rep = lambda v: [x for x in v for _ in range(nf)]          # case-major, FOWT-minor
         cs = CaseSet(np.tile(np.arange(nf, dtype=np.int32), n), rep(hd), rep(sp), rep(Hs), rep(Tp), rep(gm))
         dev = dds[0].device
         from .solver import prepare_batch
         Ka = self.array_stiffness()
-        return dict(n=n, dds=dds, cs=cs, prep=prepare_batch(dds, cs), dev=dev,
+        return dict(n=n, dds=dds, cs=cs, prep=prepare_batch(dds, cs), dev=dev, seas=seas, nws=nws,
                     arr=(N.RhDesign * nf)(*[d.struct() for d in dds]),
                     K=None if Ka is None else torch.tensor(Ka, dtype=torch.float64, device=dev).contiguous())
 
     def analyzeArrayBatch(self, cases=None, tol=0.01, host=True, marks=None, prepared=None):
-        """The coupled-array response of many single-sea-state cases (raft/raft_model.py:852-1065
-        for nFOWT > 1) in two device calls instead of per-case, per-FOWT host round trips:
+        """The coupled-array response of many cases (raft/raft_model.py:852-1065 for nFOWT > 1)
+        in a few device calls instead of per-case, per-FOWT host round trips:
           1. every (case, FOWT) drag fixed point in one rh_solve_cases launch (outputs: zeta,
-             the node drag matrices and B_drag);
-          2. rh_array_response: per (case, bin) the wave excitation of each FOWT with its final
-             linearisation, its impedance rebuilt from the design's matrices and B_drag,
-             Z_sys = blockdiag(Z_i) + array mooring stiffness and Xi = Z_sys^-1 F_wave, in one
-             launch with no per-bin Z or F array in HBM;
-             and the per-FOWT motion PSD / RMS from the solution in registers
-             (rh_array_response_stats: rh_motion_stats' values, bit for bit).
+             the node drag matrices, B_drag, and each entry's wave excitation of sea state 0
+             with its final linearisation, F_wave);
+          2. rh_array_solve_stats: per (case, bin) each FOWT's impedance rebuilt from the
+             design's matrices and B_drag, Z_sys = blockdiag(Z_i) + array mooring stiffness and
+             Xi = Z_sys^-1 F_wave, and the per-FOWT motion PSD / RMS from the solution in
+             registers (rh_motion_stats' values, bit for bit);
+          3. cases with several sea states (:1049-1065): the excitation of every further
+             (sea state, FOWT) with the linearisation frozen (rh_wave_excitation) and the same
+             coupled solve for all of them in one more launch; psd / std then sum over the sea
+             states (rh_motion_stats over Xi_waves, getPSD / getRMS) and Xi_waves
+             [n, nW+1, 6N, nw] holds every response in the reference's layout.
+        FOWTs with potSecOrder=2 add their .12d QTF's force to each sea state's excitation
+        (:903-904, :1059-1061; f2nd_mean [n, N, 6]).
         Returns Xi [n, 6N, nw], iters / status [n, N], psd [n, N, 6, nw], std [n, N, 6], zeta.
         prepared: prepareArrayBatch(cases) of an earlier call (then `cases` is not needed).
         marks: optional two timing events recorded around the fixed-point launch (bench)."""
@@ -648,31 +679,98 @@ class Model:
         P = prepared if prepared is not None else self.prepareArrayBatch(cases)
         nf, n, nw = self.nFOWT, P["n"], self.nw
         dds, cs, prep, dev = P["dds"], P["cs"], P["prep"], P["dev"]
+        multi = n > 0 and int(P["nws"].max()) > 1
         # X first holds each (case, FOWT)'s F_wave, written by its fixed point with the final
         # linearisation ([n, 6 nf, nw] is the [n nf, 6, nw] layout of the fixed point's entries),
         # then the coupled response (rh_array_solve_stats)
         X = torch.empty([n, 6 * nf, nw], dtype=torch.complex128, device=dev)
         if marks:
             marks[0].record(torch.cuda.current_stream(dev))
-        res = solve_batch(dds, cs, self.nIter, self.XiStart, tol, want=("zeta", "Bmat", "B_drag", "noXi"), prepared=prep,
-                          F_wave=X.view(n * nf, 6, nw))
+        res = solve_batch_2nd(dds, self.fowtList, cs, self.nIter, self.XiStart, tol,
+                              want=("zeta", "Bmat", "B_drag", "noXi"), prepared=prep, F_wave=X.view(n * nf, 6, nw))
         if marks:
             marks[1].record(torch.cuda.current_stream(dev))
         arr = P["arr"]
         s = N.stream_handle(torch, dev)
         ctx = N.context(self.device)
         K = P["K"]
-        psd = torch.empty([n * nf, 6, nw], dtype=torch.float64, device=dev)
-        std = torch.empty([n * nf, 6], dtype=torch.float64, device=dev)
+        psd = std = None
+        if not multi:
+            psd = torch.empty([n * nf, 6, nw], dtype=torch.float64, device=dev)
+            std = torch.empty([n * nf, 6], dtype=torch.float64, device=dev)
         N.check(N.lib().rh_array_solve_stats(ctx, arr, nf, nf, n, N.ptr(prep["design"]), N.ptr(res["B_drag"]), N.ptr(K),
                                              N.ptr(X), float(self.fowtList[0].dw), N.ptr(psd), N.ptr(std), s),
                 "rh_array_solve_stats")
         out = {"Xi": X, "iters": res["iters"].view(n, nf), "status": res["status"].view(n, nf),
-               "psd": psd.view(n, nf, 6, nw), "std": std.view(n, nf, 6), "zeta": res["zeta"].view(n, nf, nw)[:, 0]}
-        out["_keep"] = (res, arr, K)
+               "zeta": res["zeta"].view(n, nf, nw)[:, 0]}
+        if "f2nd_mean" in res:
+            out["f2nd_mean"] = res["f2nd_mean"].view(n, nf, 6)
+        keep = [res, arr, K]
+        if multi:
+            psd, std = self._array_extra_sea_states(P, res, X, out, keep)
+        out["psd"], out["std"] = psd.view(n, nf, 6, nw), std.view(n, nf, 6)
+        out["_keep"] = tuple(keep)
         if host:
             return {k: v.cpu().numpy() for k, v in out.items() if k != "_keep"}
         return out
+
+    def _array_extra_sea_states(self, P, res, X, out, keep):
+        """Step 3 of analyzeArrayBatch: the further sea states of every case (one excitation and
+        one coupled-solve launch for all of them), Xi_waves and the statistics over all rows."""
+        import torch
+        nf, n, nw = self.nFOWT, P["n"], self.nw
+        dds, dev, seas, nws = P["dds"], P["dev"], P["seas"], P["nws"]
+        nwm = int(nws.max())
+        ctx, s = N.context(self.device), N.stream_handle(torch, dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        ext = [(i, h) for i in range(n) for h in range(1, int(nws[i]))]
+        m = len(ext)
+        pick = lambda k: [seas[i][k][h] for i, h in ext]   # noqa: E731
+        betas = np.array(pick(0), dtype=float) * DEG2RAD
+        from .second_order import sea_spectra
+        S, zeta = sea_spectra(dds[0], [N.SPECTRUM_CODES[x] for x in pick(1)], pick(2), pick(3), pick(4))
+        # entries (extra sea state, FOWT), sea-state-major: the [m, 6 nf, nw] layout of the solve
+        src = np.array([i * nf + f for i, _ in ext for f in range(nf)], dtype=np.int64)
+        heads = np.array([dds[f].ensure_headings([b])[0] for b in betas for f in range(nf)], dtype=np.int32)
+        didx = torch.tensor(np.tile(np.arange(nf, dtype=np.int32), m), **i32)
+        hidx = torch.tensor(heads, **i32)
+        srct = torch.tensor(src, dtype=torch.long, device=dev)
+        ze = zeta.repeat_interleave(nf, dim=0).contiguous()
+        bmat = res["Bmat"].index_select(0, srct).contiguous()
+        bdrag = res["B_drag"].index_select(0, srct).contiguous()
+        XE = torch.empty([m, 6 * nf, nw], dtype=torch.complex128, device=dev)
+        N.check(N.lib().rh_wave_excitation(ctx, P["arr"], nf, m * nf, N.ptr(didx), N.ptr(hidx), N.ptr(ze), N.ptr(bmat),
+                                           N.ptr(XE), s), "rh_wave_excitation")
+        FE = XE.view(m, nf, 6, nw)
+        if any(f.potSecOrder == 2 for f in self.fowtList):
+            fw = torch.zeros([n, nwm, nf, 6], **f64)
+            fw[:, 0] = out["f2nd_mean"]
+            hsel = torch.tensor([h for _, h in ext], dtype=torch.long, device=dev)
+            csel = torch.tensor([i for i, _ in ext], dtype=torch.long, device=dev)
+            for f, fowt in enumerate(self.fowtList):
+                if fowt.potSecOrder != 2:
+                    continue
+                fx, fm = file_qtf_forces(dds[f], fowt, betas, S)          # (:1059-1061)
+                FE[:, f] += fx
+                fw[csel, hsel, f] = fm
+            out["f2nd_mean_waves"] = fw
+        N.check(N.lib().rh_array_solve_stats(ctx, P["arr"], nf, nf, m, N.ptr(didx), N.ptr(bdrag), N.ptr(P["K"]),
+                                             N.ptr(XE), float(self.fowtList[0].dw), None, None, s),
+                "rh_array_solve_stats")
+        Xw = torch.zeros([n, nwm + 1, 6 * nf, nw], dtype=torch.complex128, device=dev)
+        Xw[:, 0] = X
+        Xw[torch.tensor([i for i, _ in ext], dtype=torch.long, device=dev),
+           torch.tensor([h for _, h in ext], dtype=torch.long, device=dev)] = XE
+        out["Xi_waves"] = Xw
+        out["nWaves"] = torch.tensor(nws, dtype=torch.int64, device=dev)
+        rows = Xw.view(n, nwm + 1, nf, 6, nw).permute(0, 2, 1, 3, 4).contiguous()      # [n, nf, nW+1, 6, nw]
+        psd = torch.empty([n * nf, 6, nw], **f64)
+        std = torch.empty([n * nf, 6], **f64)
+        N.check(N.lib().rh_motion_stats(ctx, n * nf, nwm + 1, nw, float(self.fowtList[0].dw), N.ptr(rows), N.ptr(psd),
+                                        N.ptr(std), s), "rh_motion_stats")
+        keep += [S, zeta, didx, hidx, ze, bmat, bdrag, XE, rows]
+        return psd, std
 
 
 def _load_design(input_file):

@@ -46,7 +46,7 @@ def test_host_cores_respects_affinity():
 
 
 def test_pmc_lookup_sections_and_exact_names(tmp_path, monkeypatch):
-    """pmc_traffic reads the workload's section of a sectioned summary (tools/gpu_pmc_r04.sh),
+    """pmc_traffic reads the workload's section of a sectioned summary (tools/gpu.sh pmc),
     sums exactly the named kernels (k_qtf_kay is not k_qtf_kay_sum), and returns None when a
     named kernel is absent; a flat (older) summary serves every workload."""
     import json

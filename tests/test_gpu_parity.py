@@ -344,8 +344,9 @@ def _singular_copy(dd):
 def test_failed_cases_fast_and_general_agree(tag, design, settings, ncase):
     """A batch with a NaN sea state and a case on a singular design: both solve kernels stop
     those cases with RH_CASE_NAN / RH_CASE_SINGULAR after the same iteration and report no
-    response for them (Xi, PSD, RAO and std all NaN; the reference raises there,
-    raft/raft_model.py:957), while the other cases of the batch are unaffected and agree."""
+    response for them (Xi, F_wave, PSD, RAO and std all NaN -- an array solve of them then gives
+    NaN too; the reference raises there, raft/raft_model.py:957), while the other cases of the
+    batch are unaffected and agree."""
     import torch
     from raft import _native as N
     from raft.solver import CaseSet, solve_batch
@@ -363,7 +364,11 @@ def test_failed_cases_fast_and_general_agree(tag, design, settings, ncase):
     for solver in (0, 1):
         N.check(N.lib().rh_set_solver(N.context(0), solver), "rh_set_solver")
         try:
-            out.append(solve_batch([dd, _singular_copy(dd)], cs, m.nIter, m.XiStart, 0.01, want=want).host())
+            # F_wave starts as stale finite memory: a failed case must overwrite it with NaN
+            Fw = torch.ones([ncase, 6, m.nw], dtype=torch.complex128, device=dd.device)
+            r = solve_batch([dd, _singular_copy(dd)], cs, m.nIter, m.XiStart, 0.01, want=want, F_wave=Fw).host()
+            r["F_wave"] = Fw.cpu().numpy()
+            out.append(r)
         finally:
             N.check(N.lib().rh_set_solver(N.context(0), 0), "rh_set_solver")
         torch.cuda.synchronize()
@@ -372,7 +377,7 @@ def test_failed_cases_fast_and_general_agree(tag, design, settings, ncase):
     np.testing.assert_array_equal(a["status"], b["status"])
     np.testing.assert_array_equal(a["iters"], b["iters"])
     for r in (a, b):
-        for k in ("Xi", "psd", "std", "rao"):
+        for k in ("Xi", "psd", "std", "rao", "F_wave"):
             assert np.all(np.isnan(r[k][[2, 5]])), k
             ok = np.delete(r[k], [2, 5], axis=0)
             assert np.all(np.isfinite(ok)), k

@@ -99,6 +99,33 @@ def test_qtf_full_size_400_grid(T):
 
 
 @pytest.mark.parametrize("beta_deg", [0.0, 30.0])
+def test_full_400_grid_random_pairs_vs_oracle(T, beta_deg):
+    """The full 400 x 400 device QTF against the oracle (oracle/qtf_oracle.py) on 2,080 seeded
+    random (i1 <= i2) pairs: every entry is pointwise in (w1, w2) (per-frequency tables, the RAO
+    interpolated per frequency, Kim & Yue per pair), so the oracle evaluated on a random
+    64-frequency sub-grid gives the matching principal submatrix of the full result.  1e-9
+    normwise and elementwise to 1e-9 of the largest entry, at 0 and 30 degrees (Q1)."""
+    from oracle import qtf_oracle as Q
+    from raft.hydro_math import wave_numbers
+    m, f = make(T)
+    f.calcHydroExcitation(_case(T), memberList=f.memberList)
+    w400 = np.arange(0.04, 0.35 + 0.5 * 0.04, 0.000825) * 2 * np.pi
+    k400 = wave_numbers(w400, f.depth)
+    f.w1_2nd, f.k1_2nd = w400, k400
+    f.w2_2nd, f.k2_2nd = w400.copy(), k400.copy()
+    beta = np.deg2rad(beta_deg)
+    f.beta = np.array([beta])
+    f.calcQTF_slenderBody(0, Xi0=T["out_Xi0"])
+    idx = np.sort(np.random.default_rng(2026 + int(beta_deg)).choice(len(w400), 64, replace=False))
+    ref = Q.qtf_slender(T, T["out_Xi0"], w400[idx], k400[idx], beta)
+    sub = f.qtf[np.ix_(idx, idx)]
+    iu, ju = np.triu_indices(len(idx))
+    assert len(iu) >= 2000
+    assert rel(sub[iu, ju], ref[iu, ju]) < RTOL, rel(sub[iu, ju], ref[iu, ju])
+    np.testing.assert_allclose(sub, ref, rtol=0, atol=RTOL * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("beta_deg", [0.0, 30.0])
 @pytest.mark.parametrize("grid", ["golden42", "full400"])
 def test_mfma_path_matches_per_pair_kernel(T, beta_deg, grid):
     """The default QTF path on a sorted grid (the pair sum as FP64 MFMA GEMMs, rh_qtf_mfma.hip)

@@ -432,6 +432,7 @@ def test_oc4semi_sweep_native_prep_matches_python_prep():
     import copy
     from raft.batch import DesignBatch
     base = load_design("OC4semi-RAFT_QTF")
+    base["platform"]["potSecOrder"] = 0     # first order: native / light designs carry no QTF
     designs = []
     for f in (1.0, 0.9, 1.1):
         d = copy.deepcopy(base)

@@ -1,4 +1,4 @@
-"""HBM MB per launch of each rh:: kernel from tools/gpu_ab.sh pmc passes
+"""HBM MB per launch of each rh:: kernel from tools/gpu.sh pmc passes
 (gpurun_out/<dir>/pmc_<lib>_<workload>/{WRITE_SIZE,FETCH_SIZE}); FETCH_SIZE doubled per the
 gfx950 correction (tools/pmc_summary.py)."""
 import csv
