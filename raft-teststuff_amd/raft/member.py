@@ -5,7 +5,8 @@ Per-design host preparation feeding the device node tables (SURVEY.md §8(a) row
   * pose (q, p1, p2, node r)     raft/raft_member.py:245-304
   * added mass / inertial coeffs raft/raft_member.py:877-1050
   * MacCamy-Fuchs Cm             raft/raft_member.py:1053-1088
-Statics (getInertia / getHydrostatics) are §8(f) row 1 and not part of this class yet.
+The member statics (getInertia / getHydrostatics, §8(f) row 1) are computed from these
+tables by raft/statics.py (and natively by csrc/rh_prep.h for design sweeps).
 """
 import numpy as np
 from scipy.special import hankel1

@@ -46,3 +46,4 @@ if __name__ == "__main__":
                   % (k, t[0] * 1e3, t[3] * 1e3, t[4] * 1e3, t[1] * 1e3, t[2] * 1e3), flush=True)
         del out, keep
     pool.close()
+    pool.join()          # the workers exit before the interpreter does (no SIGTERM at exit)
