@@ -7,7 +7,7 @@ at min_freq 0.0002 Hz -> nw = 1000 bins, 53 submerged strip nodes (20 circular +
 converged RAO + motion PSD in one device call.  Inputs (design tables, case parameters)
 are resident in HBM before the timed region.  Multi-GPU: one process per GPU, every rank
 solves its own 512-case shard (weak scaling, no collective inside the drag loop); each
-step's per-case outputs (std, PSD, iteration counts) are all-gathered over RCCL on a second
+step's per-case outputs (std, PSD, iteration counts) are gathered to rank 0 over RCCL on a second
 stream while the next step solves (the final response-spectrum gather of north_star), and
 the line also reports the same steps without the gather.
 
@@ -610,7 +610,7 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
     t0 = time.perf_counter()
     res, keep = solve_sweep(designs, statics, local_idx, state_idx, grid, device=device, chunks=C5_CHUNKS,
                             want=want, specs=specs, threads=threads)
-    out = gather_cases({"std": res["std"], "psd": res["psd"], "iters": res["iters"]}, n)
+    out = gather_cases({"std": res["std"], "psd": res["psd"], "iters": res["iters"]}, n, dst=0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -645,7 +645,7 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
             "iterations_mean": float(iters.mean()),
             "config": {"workload": "C5: 250 VolturnUS-S_example parametersweep variants (5 variables U(0.75,1.25)) "
                                    "x 40 sea states, nw=1000", "nw": keep[0][0].nw,
-                       "parallelism": f"case-block-sharded x{world} + all-gather (std, PSD, iterations); "
+                       "parallelism": f"case-block-sharded x{world} + gather to rank 0 (std, PSD, iterations); "
                                       f"{C5_CHUNKS} design blocks per rank, host preparation of block k+1 "
                                       "overlapped with the solve of block k",
                        "host_prep_threads_per_rank": threads,
@@ -692,9 +692,10 @@ def harness_check(args, world, rank):
             res = {"std": torch.zeros(4, 6, dtype=torch.float64), "psd": torch.zeros(4, 6, 8, dtype=torch.float64),
                    "iters": torch.full((4,), 4 + rank, dtype=torch.int32)}
             blk = pack_outputs(res)
-            out = torch.empty((world * blk.shape[0], blk.shape[1]), dtype=blk.dtype)
-            dist.all_gather_into_tensor(out, blk)
-            gathered += int((out[:, -1] >= 4).sum())
+            out = [torch.empty_like(blk) for _ in range(world)] if rank == 0 else None
+            dist.gather(blk, gather_list=out, dst=0)
+            if rank == 0:
+                gathered += int((torch.cat(out, 0)[:, -1] >= 4).sum())
     if world > 1:
         dist.barrier()
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
@@ -787,17 +788,20 @@ def main():
     comm = torch.cuda.Stream(device) if world > 1 else None
 
     def gather_async(res, e_done):
-        """All-gather of this step's packed outputs on the comm stream, after the solve
-        (event e_done), overlapping the next step's solve on the compute stream."""
+        """Gather of this step's packed outputs to rank 0 on the comm stream, after the solve
+        (event e_done), overlapping the next step's solve on the compute stream.  A gather, not
+        an all-gather: only rank 0 consumes the response spectra, and on the fully connected
+        xGMI node each rank's block then crosses one link once (DESIGN.md §6 byte budget)."""
         with torch.cuda.stream(comm):
             comm.wait_event(e_done)
             blk = pack_outputs(res)
-            out = torch.empty((world * blk.shape[0], blk.shape[1]), dtype=blk.dtype, device=blk.device)
+            out = [torch.empty_like(blk) for _ in range(world)] if rank == 0 else None
             g0 = torch.cuda.Event(enable_timing=True)
             g0.record(comm)
-            work = dist.all_gather_into_tensor(out, blk, async_op=True)
+            work = dist.gather(blk, gather_list=out, dst=0, async_op=True)
         for v in res.values():
             v.record_stream(comm)
+        blk.record_stream(comm)
         return work, out, g0
 
     # The other legs run first: the CPU baseline leaves the GPU idle for 10-20 s, and a few
@@ -856,8 +860,9 @@ def main():
                 g1.record(comm)
             torch.cuda.synchronize()
             gms = pend[-1][2].elapsed_time(g1)   # the last step's gather (nothing overlaps it)
-            out = pend[-1][1]
-            assert out.shape[0] == world * args.ncase and torch.all(out[:, -1] >= 1)
+            if rank == 0:
+                out = torch.cat(pend[-1][1], 0)
+                assert out.shape[0] == world * args.ncase and torch.all(out[:, -1] >= 1)
         return float(t.item()), (ev, end), r, gms
 
     dt_serial, (ev, end), res, _ = timed(False)
@@ -921,8 +926,9 @@ def main():
         line["gather"] = {"included_in_value": True, "value_without_gather": total_cases / dt_ng,
                           "ms_per_step_without_gather": dt_ng / args.steps * 1e3,
                           "last_gather_ms": gather_ms, "bytes_per_rank_per_step": n_out,
-                          "note": "per step: all_gather_into_tensor (RCCL) of every rank's std, PSD and iteration "
-                                  "counts on a second stream, overlapping the next step's solve"}
+                          "bytes_into_rank0_per_step": (world - 1) * n_out,
+                          "note": "per step: gather (RCCL) of every rank's std, PSD and iteration counts to rank 0 on a "
+                                  "second stream, overlapping the next step's solve (DESIGN.md §6 byte budget)"}
     line.update(legs)
     if pool is not None:
         pool.close()

@@ -96,9 +96,11 @@ def qtf_pairs_of(n2, rank, world):
     return int(len(qtf_pair_flat(n2, qtf_tiles(n2, rank, world))))
 
 
-def gather_cases(local, n_total, group=None):
+def gather_cases(local, n_total, group=None, dst=None):
     """All-gather per-case tensors ([n_local, ...]) of contiguous case blocks into
-    [n_total, ...] on every rank.  `local`: dict name -> tensor."""
+    [n_total, ...] on every rank.  `local`: dict name -> tensor.  dst: gather to that rank only
+    (the other ranks return their `local` block unchanged): each block crosses one xGMI link
+    once instead of reaching every rank (DESIGN.md §6 byte budget)."""
     import torch
     dist = _dist()
     rank, world = world_of(group)
@@ -106,13 +108,21 @@ def gather_cases(local, n_total, group=None):
         return dict(local)
     m = -(-n_total // world)
     out = {}
+    gdst = None if dst is None else (dist.get_global_rank(group, dst) if group is not None else dst)
     for k, t in local.items():
         cplx = t.is_complex()
         x = torch.view_as_real(t) if cplx else t
         pad = torch.zeros((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
         pad[:x.shape[0]] = x
-        parts = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(parts, pad, group=group)
+        if dst is not None:
+            parts = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+            dist.gather(pad, gather_list=parts, dst=gdst, group=group)
+            if rank != dst:
+                out[k] = t
+                continue
+        else:
+            parts = [torch.empty_like(pad) for _ in range(world)]
+            dist.all_gather(parts, pad, group=group)
         blocks = []
         for r in range(world):
             lo, hi = case_shard(n_total, r, world)

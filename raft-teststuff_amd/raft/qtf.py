@@ -27,36 +27,51 @@ def hank_table(kk, R):
 
 def build_tables(fowt, w2, k2, beta, host_hankel=False):
     """Static QTF tables of a FOWT for grid (w2, k2) and heading beta [rad].  The Hankel
-    table is built on the host only with host_hankel=True (the device builds it otherwise)."""
+    table is built on the host only with host_hankel=True (the device builds it otherwise).
+    Each member's submerged nodes are tabulated with whole-array operations (the per-node
+    arithmetic of raft/raft_fowt.py:1468-1502, 1532-1587 elementwise)."""
     rho, g, h = float(fowt.rho_water), float(fowt.g), float(fowt.depth)
-    ncols, mcols, kcols, hank = [], [], [], []
+    nblocks, mcols, kcols, hank = [], [], [], []
     qmstart, kstart = [0], [0]
     for mem in fowt.memberList:
         if mem.rA[2] > 0 and mem.rB[2] > 0:                     # entirely above water (:1461)
             continue
         circ = mem.shape == "circular"
         p1M, p2M, qM = mem.p1Mat, mem.p2Mat, mem.qMat
-        last_cm = last_ca = None
-        for il in range(mem.ns):
-            r = mem.r[il]
-            if r[2] >= 0:
-                continue
-            Ca_p1, Ca_p2, Ca_End = mem.coef("Ca_p1", il), mem.coef("Ca_p2", il), mem.coef("Ca_End", il)
-            ds, drs, dls = np.atleast_1d(mem.ds[il]), np.atleast_1d(mem.drs[il]), mem.dls[il]
-            v_i = 0.25 * np.pi * ds[0] ** 2 * dls if circ else ds[0] * ds[1] * dls
-            if r[2] + 0.5 * dls > 0:                             # Q12
-                v_i = v_i * (0.5 * dls - r[2]) / dls
+        sub = np.nonzero(mem.r[:, 2] < 0)[0]
+        nsub = len(sub)
+        last_cm = last_ca = np.zeros([3, 3])
+        if nsub:
+            ls = mem.ls[sub]
+            Ca_p1, Ca_p2, Ca_End = (np.interp(ls, mem.stations, getattr(mem, k)) for k in ("Ca_p1", "Ca_p2", "Ca_End"))
+            r = mem.r[sub]
+            dls = mem.dls[sub]
+            ds = np.asarray(mem.ds, dtype=float)[sub]
+            drs = np.asarray(mem.drs, dtype=float)[sub]
             if circ:
-                ve = np.pi / 12.0 * abs((ds[0] + drs[0]) ** 3 - (ds[0] - drs[0]) ** 3)
+                v_i = 0.25 * np.pi * ds ** 2 * dls
+                ve = np.pi / 12.0 * np.abs((ds + drs) ** 3 - (ds - drs) ** 3)
             else:
-                ve = np.pi / 12.0 * ((np.mean(ds + drs)) ** 3 - (np.mean(ds - drs)) ** 3)
-            CmM = (1. + Ca_p1) * p1M + (1. + Ca_p2) * p2M
-            CaM = Ca_p1 * p1M + Ca_p2 * p2M
-            last_cm, last_ca = CmM, CaM
-            ncols.append([*r, *mem.q, v_i, ve, mem.a_i[il], Ca_End, *CmM.ravel(), *CaM.ravel(),
-                          *(p1M + p2M).ravel(), *qM.ravel()])
-        nsub = len(ncols) - qmstart[-1]
-        qmstart.append(len(ncols))
+                v_i = ds[:, 0] * ds[:, 1] * dls
+                ve = np.pi / 12.0 * (np.mean(ds + drs, axis=1) ** 3 - np.mean(ds - drs, axis=1) ** 3)
+            part = r[:, 2] + 0.5 * dls > 0                        # Q12
+            v_i = np.where(part, v_i * (0.5 * dls - r[:, 2]) / np.where(part, dls, 1.0), v_i)
+            CmM = (1. + Ca_p1)[:, None] * p1M.ravel() + (1. + Ca_p2)[:, None] * p2M.ravel()
+            CaM = Ca_p1[:, None] * p1M.ravel() + Ca_p2[:, None] * p2M.ravel()
+            last_cm, last_ca = CmM[-1].reshape(3, 3), CaM[-1].reshape(3, 3)
+            blk = np.empty([nsub, QN_COUNT])
+            blk[:, 0:3] = r
+            blk[:, 3:6] = mem.q
+            blk[:, 6] = v_i
+            blk[:, 7] = ve
+            blk[:, 8] = mem.a_i[sub]
+            blk[:, 9] = Ca_End
+            blk[:, 10:19] = CmM
+            blk[:, 19:28] = CaM
+            blk[:, 28:37] = (p1M + p2M).ravel()
+            blk[:, 37:46] = qM.ravel()
+            nblocks.append(blk)
+        qmstart.append(qmstart[-1] + nsub)
         wl = mem.r[-1, 2] * mem.r[0, 2] < 0
         rint = np.zeros(3)
         awl = 0.0
@@ -72,8 +87,6 @@ def build_tables(fowt, w2, k2, beta, host_hankel=False):
                 else:
                     d1, d2 = mem.ds[i_wl, 0], mem.ds[i_wl, 1]
                 awl = d1 * d2
-        if nsub == 0:
-            last_cm = last_ca = np.zeros([3, 3])
         # Kim & Yue (raft_member.py:1111-1200)
         kay = bool(mem.MCF) and (mem.rA[2] * mem.rB[2] < 0)
         pf = np.zeros(3)
@@ -88,26 +101,23 @@ def build_tables(fowt, w2, k2, beta, host_hankel=False):
             kcols.append([R, 0.0, 0.0, *rwl])
             if host_hankel:
                 hank.append(hank_table(k2, R))
-            for il in range(mem.ns - 1):
+            ds_all = np.asarray(mem.ds, dtype=float)
+            il = np.nonzero(mem.r[:-1, 2] <= 0)[0]                 # intervals whose first node is wet
+            if len(il):
                 z1 = mem.r[il, 2]
-                if z1 > 0:
-                    continue
-                z2 = mem.r[il + 1, 2]
-                z2 = 0 if z2 > 0 else z2
-                R1 = mem.ds[il] / 2
-                if mem.dls[il] == 0:
-                    R1 = mem.ds[il]
-                R2 = mem.ds[il + 1] / 2
-                if mem.dls[il + 1] == 0:
-                    R2 = mem.ds[il]                               # Q9
+                z2 = np.where(mem.r[il + 1, 2] > 0, 0.0, mem.r[il + 1, 2])
+                R1 = np.where(mem.dls[il] == 0, ds_all[il], ds_all[il] / 2)
+                R2 = np.where(mem.dls[il + 1] == 0, ds_all[il], ds_all[il + 1] / 2)   # Q9
                 Rm = 0.5 * (R1 + R2)
-                kcols.append([Rm, z1, z2, *(0.5 * (mem.r[il] + mem.r[il + 1]))])
-                if host_hankel:
-                    hank.append(hank_table(k2, Rm))
+                mid = 0.5 * (mem.r[il] + mem.r[il + 1])
+                for j in range(len(il)):
+                    kcols.append([Rm[j], z1[j], z2[j], *mid[j]])
+                    if host_hankel:
+                        hank.append(hank_table(k2, Rm[j]))
         kstart.append(len(kcols))
         mcols.append([1.0 if wl else 0.0, *rint, awl, *last_cm.ravel(), *last_ca.ravel(), *mem.p1, *mem.p2,
                       1.0 if kay else 0.0, *pf, *rwl])
-    qnode = np.array(ncols, dtype=float).T.copy() if ncols else np.zeros([QN_COUNT, 0])
+    qnode = np.concatenate(nblocks).T.copy() if nblocks else np.zeros([QN_COUNT, 0])
     qmemb = np.array(mcols, dtype=float).T.copy() if mcols else np.zeros([QM_COUNT, 0])
     kray = np.array(kcols, dtype=float).T.copy() if kcols else np.zeros([KR_COUNT, 0])
     hk = np.array(hank, dtype=complex) if hank else None
@@ -129,20 +139,27 @@ class QtfDevice:
         f64 = dict(dtype=torch.float64, device=self.dev)
         self.n2 = len(w2)
         self.beta = float(beta)
-        self.w2 = torch.tensor(np.asarray(w2, dtype=float), **f64)
-        self.k2 = torch.tensor(np.asarray(k2, dtype=float), **f64)
         self.nq, self.nmq, self.nkr = t["qnode"].shape[1], t["qmemb"].shape[1], t["kray"].shape[1]
         pad = lambda a, rows: a if a.shape[1] else np.zeros([rows, 1])
-        self.qnode = torch.tensor(pad(t["qnode"], QN_COUNT), **f64).contiguous()
-        self.qmemb = torch.tensor(pad(t["qmemb"], QM_COUNT), **f64).contiguous()
-        self.kray = torch.tensor(pad(t["kray"], KR_COUNT), **f64).contiguous()
+        # the three tables and the grid in one upload, the two index tables in another
+        parts = [pad(t["qnode"], QN_COUNT), pad(t["qmemb"], QM_COUNT), pad(t["kray"], KR_COUNT)]
+        flat = np.concatenate([np.asarray(w2, dtype=float), np.asarray(k2, dtype=float)] + [a.ravel() for a in parts])
+        dev_flat = torch.from_numpy(flat).to(self.dev)
+        self.w2, self.k2 = dev_flat[:self.n2], dev_flat[self.n2:2 * self.n2]
+        off = 2 * self.n2
+        views = []
+        for a in parts:
+            views.append(dev_flat[off:off + a.size].view(a.shape))
+            off += a.size
+        self.qnode, self.qmemb, self.kray = views
         # Kim & Yue Hankel table [nkr][n2][12], built on the device from k2 and the radii
-        self.hank = torch.zeros([max(self.nkr, 1), self.n2, 12], dtype=torch.complex128, device=self.dev)
+        self.hank = (torch.empty if self.nkr else torch.zeros)([max(self.nkr, 1), self.n2, 12], dtype=torch.complex128,
+                                                               device=self.dev)
         if self.nkr:
             N.check(N.lib().rh_qtf_hankel(N.context(device), self.n2, N.ptr(self.k2), self.nkr, N.ptr(self.kray),
                                           N.ptr(self.hank), N.stream_handle(torch, self.dev)), "rh_qtf_hankel")
-        self.qmstart = torch.tensor(t["qmstart"], dtype=torch.int32, device=self.dev)
-        self.kstart = torch.tensor(t["kstart"], dtype=torch.int32, device=self.dev)
+        ints = torch.from_numpy(np.concatenate([t["qmstart"], t["kstart"]]).astype(np.int32)).to(self.dev)
+        self.qmstart, self.kstart = ints[:len(t["qmstart"])], ints[len(t["qmstart"]):]
         self.rho, self.g, self.h = t["rho"], t["g"], t["h"]
         # the MFMA pair path needs the upper triangle to be i2 >= i1 and nk = k2 - k1
         w2a, k2a = np.asarray(w2, dtype=float), np.asarray(k2, dtype=float)

@@ -136,6 +136,11 @@ def _gather_check(rank, world):
     got = gather_cases({"Xi": torch.tensor(full_x[lo:hi]), "iters": torch.tensor(full_i[lo:hi])}, n)
     np.testing.assert_array_equal(got["Xi"].numpy(), full_x)
     np.testing.assert_array_equal(got["iters"].numpy(), full_i)
+    # gather to one rank: the full arrays there, the rank's own block elsewhere
+    got = gather_cases({"Xi": torch.tensor(full_x[lo:hi]), "iters": torch.tensor(full_i[lo:hi])}, n, dst=1)
+    want_x, want_i = (full_x, full_i) if rank == 1 else (full_x[lo:hi], full_i[lo:hi])
+    np.testing.assert_array_equal(got["Xi"].numpy(), want_x)
+    np.testing.assert_array_equal(got["iters"].numpy(), want_i)
 
 
 def test_case_gather_world2():
