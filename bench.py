@@ -25,7 +25,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "raft-teststuff_amd"))
 
 NCASE = 512
-C5_CHUNKS = 5         # C5 design blocks: block k+1 is prepared on the host while block k solves
+C5_CHUNKS = 5         # C5 design blocks of a whole sweep: block k+1 is prepared on the host while block k solves
+
+
+def c5_chunks(world):
+    """Design blocks per rank of the C5 pipeline: C5_CHUNKS for the whole sweep, fewer for a
+    rank's share at N > 1 (each block carries a fixed host cost, profiles/r06_v1/c5_rank_pacing.txt)."""
+    return max(1, min(C5_CHUNKS, round(C5_CHUNKS / max(1, world) ** 0.5)))
 PEAK_FP64 = 78.6e12   # MI355X FP64 dense peak (vector = matrix rate), FLOP/s
 # HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950
 # correction of MI355X_MICROARCH.md + WRITE_SIZE), written by tools/pmc_summary.py
@@ -561,7 +567,7 @@ def c5_pool(world):
     from raft import Model
     from raft.batch import host_pool
     base, _ = c5_base()
-    P = max(1, min(16, len(os.sched_getaffinity(0)) // max(1, world)))
+    P = max(1, min(16, host_cores()[0] // max(1, world)))
     return host_pool(P, grids=[(Model.frequency_grid(base), float(base["site"]["water_depth"]))]), P
 
 
@@ -576,7 +582,7 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
     solve-only = the blocks' launches alone, repeated `steps` times.  Strong scaling (fixed 10k)."""
     import torch
     from raft.batch import solve_sweep, sweep_cases, sweep_shard
-    from raft.native_prep import sweep_specs
+    from raft.native_prep import SweepSpecs
     from raft.parallel import gather_cases
     from raft.sweep import sea_state_grid, sweep_multipliers
     base, C_moor = c5_base()
@@ -590,17 +596,22 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
     # member fields rewritten), so no per-variant design dict is built or parsed.
     statics = {"C_moor": C_moor}
     designs = [base] * (dhi - dlo)               # site and frequency grid only
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) // max(1, world)))
+    threads = max(1, min(16, host_cores()[0] // max(1, world)))   # (the cgroup quota, not the affinity mask)
 
-    def specs(a, b):
-        return sweep_specs(base, mult[dlo + a:dlo + b], statics=statics)
+    parsed = {}
+
+    def specs(a, b):   # the base record is parsed at the first block of a pass (SweepSpecs), inside the timing
+        if a == 0 or "ss" not in parsed:
+            parsed["ss"] = SweepSpecs(base, statics=statics)
+        return parsed["ss"].records(mult[dlo + a:dlo + b])
+    chunks = c5_chunks(world)
     local_idx = idx_all[lo:hi] - dlo
     want = ("psd", "std")
     state_idx = np.arange(lo, hi) % len(grid)          # design-major product
     # two untimed passes first (the host workers' first tasks, allocator growth), as the
     # warmup steps of the C2 leg
     for _ in range(2):
-        w_out, w_keep = solve_sweep(designs, statics, local_idx, state_idx, grid, device=device, chunks=C5_CHUNKS,
+        w_out, w_keep = solve_sweep(designs, statics, local_idx, state_idx, grid, device=device, chunks=chunks,
                                     want=want, specs=specs, threads=threads)
         torch.cuda.synchronize()
         del w_out, w_keep
@@ -608,7 +619,7 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res, keep = solve_sweep(designs, statics, local_idx, state_idx, grid, device=device, chunks=C5_CHUNKS,
+    res, keep = solve_sweep(designs, statics, local_idx, state_idx, grid, device=device, chunks=chunks,
                             want=want, specs=specs, threads=threads)
     out = gather_cases({"std": res["std"], "psd": res["psd"], "iters": res["iters"]}, n, dst=0)
     torch.cuda.synchronize()
@@ -640,17 +651,17 @@ def bench_c5(device, steps, world, rank, dist, pool=None, nproc=1):
     iters = out["iters"].cpu().numpy()
     return {"metric": "sweep cases/sec end-to-end (design prep + solve + gather)", "value": n / t_e2e,
             "unit": "cases/s", "scaling": "strong", "cases": n, "designs": C5_DESIGNS, "sea_states": len(grid),
-            "end_to_end_s": t_e2e, "host_prep_s": t_host, "blocks": C5_CHUNKS,
+            "end_to_end_s": t_e2e, "host_prep_s": t_host, "blocks": chunks,
             "solve_only_cases_per_s": n / t_solve, "solve_ms": t_solve * 1e3, "kernel_ms_rank0": kern_ms,
             "iterations_mean": float(iters.mean()),
             "config": {"workload": "C5: 250 VolturnUS-S_example parametersweep variants (5 variables U(0.75,1.25)) "
                                    "x 40 sea states, nw=1000", "nw": keep[0][0].nw,
                        "parallelism": f"case-block-sharded x{world} + gather to rank 0 (std, PSD, iterations); "
-                                      f"{C5_CHUNKS} design blocks per rank, host preparation of block k+1 "
+                                      f"{chunks} design blocks per rank, host preparation of block k+1 "
                                       "overlapped with the solve of block k",
                        "host_prep_threads_per_rank": threads,
                        "design_input": "base design + per-variant multipliers; spec records built in the timed "
-                                       "pipeline (raft/native_prep.py sweep_specs)"}}
+                                       "pipeline (raft/native_prep.py SweepSpecs)"}}
 
 
 def relaunch(nproc, argv):

@@ -103,7 +103,15 @@ class DesignBatch:
         st0 = designs[0].get("settings", {})
         nIter = get_from_dict(st0, "nIter", default=15, dtype=int)
         XiStart = get_from_dict(st0, "XiStart", default=0.1, dtype=float)
-        return [NativeDesign(P, i, d, w, k, depth, nIter, XiStart, device) for i, d in enumerate(designs)]
+        sites = {}
+        out = []
+        for i, d in enumerate(designs):
+            site = sites.get(id(d["site"]))
+            if site is None:            # the site scalars once per distinct site (a sweep shares one)
+                site = sites[id(d["site"])] = (get_from_dict(d["site"], "rho_water", default=1025.0),
+                                               get_from_dict(d["site"], "g", default=9.81))
+            out.append(NativeDesign(P, i, d, w, k, depth, nIter, XiStart, device, site=site))
+        return out
 
     def _upload(self, device):
         """Every design's device tables in one host->device copy (plus one for the member
@@ -248,6 +256,19 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
     timings: optional list that receives,
     per block, the host seconds of (design preparation, case set + tables + uploads, solve
     enqueue, DesignBatch host part, DesignBatch upload part)."""
+    import gc
+    was = gc.isenabled()
+    gc.disable()     # a full collection inside the pipeline stalled the host for 50-65 ms (profiles/r06_v1)
+    try:
+        return _solve_sweep(designs, statics, design_idx, state_idx, sea_states, device, pool, chunks, tol, want,
+                            timings, specs, threads, first, last)
+    finally:
+        if was:
+            gc.enable()
+
+
+def _solve_sweep(designs, statics, design_idx, state_idx, sea_states, device, pool, chunks, tol, want, timings,
+                 specs, threads, first, last):
     import torch
     from .solver import prepare_batch
     design_idx = np.asarray(design_idx, dtype=np.int64)
@@ -378,12 +399,13 @@ class NativeDesign(HostDesign):
     """HostDesign of a natively prepared design (rh_prep_designs): its tables are views of
     the batch's packed host array."""
 
-    def __init__(self, P, i, design, w, k, depth, nIter, XiStart, device):
-        site = design["site"]
+    def __init__(self, P, i, design, w, k, depth, nIter, XiStart, device, site=None):
         self.nw, self.w, self.k, self.dw = len(w), w, k, w[1] - w[0]
         self.depth = depth
-        self.rho_water = get_from_dict(site, "rho_water", default=1025.0)
-        self.g = get_from_dict(site, "g", default=9.81)
+        if site is None:
+            site = (get_from_dict(design["site"], "rho_water", default=1025.0),
+                    get_from_dict(design["site"], "g", default=9.81))
+        self.rho_water, self.g = site
         self.nIter, self.XiStart = nIter, XiStart
         self.device_index = device
         self._host = P.host_tables(i)

@@ -194,14 +194,20 @@ def _spec_parts(design, r6, statics, heading_adjust):
     return np.concatenate([np.asarray(hdr, dtype=float), *given]), blocks, rots
 
 
-def sweep_specs(base, mults, r6=None, statics=None):
-    """The spec records of parametersweep variants of `base` (raft/sweep.py sweep_variant with
-    each row of `mults`), without building a design dict per variant: the base record is
-    flattened once, and per variant only the fields the sweep edits -- rA, rB and d of the
-    first four platform members (raft/sweep.py variant_members) -- are rewritten in place,
-    with the same parsing (_vec / _pairs) design_spec applies.  Equal, value for value, to
-    design_spec(sweep_variant(base, m)) (tests/test_native_prep.py)."""
-    from .sweep import variant_members
+class SweepSpecs:
+    """sweep_specs with the base design parsed once: records(mults) gives the spec records of
+    those variants (the per-block call of a pipelined sweep, raft/batch.py solve_sweep)."""
+
+    def __init__(self, base, r6=None, statics=None):
+        self.base, self.r6, self.statics = base, r6, statics
+        self._parts = _sweep_base(base, r6, statics)
+
+    def records(self, mults):
+        return sweep_specs(self.base, mults, self.r6, self.statics, _parts=self._parts)
+
+
+def _sweep_base(base, r6, statics):
+    """The base record of a sweep and the slots (offsets) of the fields the sweep edits."""
     head, blocks, rots = _spec_parts(base, r6, statics, 0.0)
     spec0 = np.concatenate([head, np.asarray([x for blk in blocks for x in blk], dtype=float),
                             np.asarray(rots, dtype=float).ravel()])
@@ -216,8 +222,29 @@ def sweep_specs(base, mults, r6=None, statics=None):
         off += len(blk)
     if len(slots) < 4 or len(plat) < 4:
         raise ValueError("sweep_specs: the sweep edits four platform members")
+    return spec0, slots
+
+
+def sweep_specs(base, mults, r6=None, statics=None, _parts=None):
+    """The spec records of parametersweep variants of `base` (raft/sweep.py sweep_variant with
+    each row of `mults`), without building a design dict per variant: the base record is
+    flattened once, and per variant only the fields the sweep edits -- rA, rB and d of the
+    first four platform members (raft/sweep.py variant_members) -- are rewritten in place,
+    with the same parsing (_vec / _pairs) design_spec applies.  Equal, value for value, to
+    design_spec(sweep_variant(base, m)) (tests/test_native_prep.py)."""
+    from .sweep import variant_members
+    spec0, slots = _parts if _parts is not None else _sweep_base(base, r6, statics)
+    M = np.atleast_2d(np.asarray(mults, dtype=float))
+    fast = _variant_fields(base, M, slots)
+    if fast is not None:      # every variant at once: the assignments of variant_members on columns
+        S = np.tile(spec0, (len(M), 1))
+        for (o_r, o_d, n, circ), (rA, rB, dcols) in zip(slots, fast):
+            S[:, o_r:o_r + 3] = rA
+            S[:, o_r + 3:o_r + 6] = rB
+            S[:, o_d:o_d + dcols.shape[1]] = dcols
+        return list(S)
     out = []
-    for m in np.atleast_2d(mults):
+    for m in M:
         s = spec0.copy()
         for (o_r, o_d, n, circ), mi in zip(slots, variant_members(base, m)):
             s[o_r:o_r + 3] = [float(x) for x in mi["rA"]]
@@ -226,6 +253,49 @@ def sweep_specs(base, mults, r6=None, statics=None):
             s[o_d:o_d + len(dd)] = dd
         out.append(s)
     return out
+
+
+def _variant_fields(base, M, slots):
+    """raft/sweep.py variant_members for every row of M at once: per edited member (rA [nd, 3],
+    rB [nd, 3], the parsed d entries [nd, ...]), the same floating-point operations in the same
+    order, column-wise.  None when the base layout is not the one it restates (columns 0 and 1
+    circular with scalar d, the pontoon rectangular with a [w, h] pair, member 3's d unchanged):
+    sweep_specs then edits each variant's members one by one."""
+    from .sweep import SWEEP_VARIABLES, sweep_baseline
+    mem = base["platform"]["members"]
+    circ = [c for _, _, _, c in slots]
+    scalar_d = all(not isinstance(mem[i]["d"], (list, tuple, np.ndarray)) for i in (0, 1))
+    pair = isinstance(mem[2]["d"], (list, tuple, np.ndarray)) and len(mem[2]["d"]) == 2 and \
+        not isinstance(mem[2]["d"][0], (list, tuple, np.ndarray))
+    if not (circ[0] and circ[1] and not circ[2] and scalar_d and pair):
+        return None
+    bl = sweep_baseline(base)
+    a, b, c, dd, e = (bl[k] * M[:, i] for i, k in enumerate(SWEEP_VARIABLES))
+    nd = len(M)
+    rA = [np.tile(np.asarray([float(x) for x in mem[i]["rA"]]), (nd, 1)) for i in range(4)]
+    rB = [np.tile(np.asarray([float(x) for x in mem[i]["rB"]]), (nd, 1)) for i in range(4)]
+    pd1 = float(mem[2]["d"][1])
+    rA[2][:, 0] = rA[2][:, 0] * (a / bl["ccD"])                 # centre-column diameter
+    rA[3][:, 0] = rA[3][:, 0] * (a / bl["ccD"])
+    rB[2][:, 0] = rA[1][:, 0] - b / 2                           # outer-column diameter
+    rB[3][:, 0] = rB[1][:, 0] - b / 2
+    rA[0][:, 2] = c                                             # draft
+    rA[1][:, 2] = c
+    rA[2][:, 2] = c + pd1 / 2
+    rB[2][:, 2] = c + pd1 / 2
+    rA[1][:, 0] = dd                                            # outer-column radius
+    rB[1][:, 0] = dd
+    rB[2][:, 0] = dd - b / 2
+    rB[3][:, 0] = dd - b / 2
+    rA[2][:, 2] = rA[0][:, 2] + e / 2                           # pontoon height
+    rB[2][:, 2] = rA[1][:, 2] + e / 2
+    n = [sl[2] for sl in slots]
+    d0 = np.repeat(a[:, None], n[0], axis=1)
+    d1 = np.repeat(b[:, None], n[1], axis=1)
+    d2 = np.tile(np.stack([np.full(nd, float(mem[2]["d"][0])), e], axis=1), (1, n[2]))
+    m3 = mem[3]
+    d3 = np.tile(np.asarray(_vec(m3, "d", n[3]) if circ[3] else _pairs(m3, "d", n[3]), dtype=float), (nd, 1))
+    return list(zip(rA, rB, [d0, d1, d2, d3]))
 
 
 class PreparedDesigns:

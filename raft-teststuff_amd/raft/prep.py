@@ -19,11 +19,17 @@ from . import _native as N
 SQRT_8_PI_NOTE = "Borgman factor sqrt(8/pi) applied on the device (raft/raft_fowt.py:1223)"
 
 
+_TORCH = []
+
+
 def _torch():
+    if _TORCH:                # checked once per process (a DeviceDesign per design of a sweep block)
+        return _TORCH[0]
     import torch
     if not torch.cuda.is_available():
         raise N.NativeError("librafthip needs a visible MI355X (torch.cuda.is_available() is False); "
                             "there is no CPU fallback")
+    _TORCH.append(torch)
     return torch
 
 
@@ -152,7 +158,14 @@ class DeviceDesign:
         self.finer = None
         self.kproj = None
 
+    _TABLES = ("uhat", "kproj", "finer")
+
     def __getattr__(self, name):
+        tab = self.__dict__.get("_tab")
+        if tab is not None and name in self._TABLES:     # a view of the batch's shared tables, made on first use
+            v = self._tab_view(name)
+            self.__dict__[name] = v
+            return v
         lay = self.__dict__.get("_layout")
         if lay is None or name not in lay:
             raise AttributeError(name)
@@ -161,16 +174,37 @@ class DeviceDesign:
         self.__dict__[name] = v
         return v
 
+    def _tab_view(self, name):
+        base, off, shape = self._tab[name]
+        return base[off:off + int(np.prod(shape))].view(*shape)
+
+    def set_tables(self, tab, headings):
+        """Point the wave tables at slices of shared allocations without making the views:
+        tab[name] = (flat complex128 tensor, element offset, shape) for uhat, kproj, finer
+        (raft/prep.py tabulate_batch; the views appear on first access)."""
+        for name in self._TABLES:
+            self.__dict__.pop(name, None)
+        self._tab = tab
+        self.headings = tuple(headings)
+        self._tabver = getattr(self, "_tabver", 0) + 1
+
+    def _tab_ptr(self, name):
+        if name not in self.__dict__ and self.__dict__.get("_tab") is not None:
+            base, off, _ = self._tab[name]
+            return ctypes.c_void_p(base.data_ptr() + 16 * off)
+        return N.ptr(self.__dict__.get(name))
+
     def _addr(self, name):
         return ctypes.c_void_p(self._packed.data_ptr() + 8 * self._layout[name][0])
 
     def struct(self):
         """The rh_design descriptor of the current tables (cached until they change)."""
-        st = getattr(self, "_struct", None)
-        if st is not None and st[0] is self.kproj:
+        st = self.__dict__.get("_struct")
+        key = (self.__dict__.get("_tabver", 0), self.__dict__.get("kproj"), self.headings)
+        if st is not None and st[0][0] == key[0] and st[0][1] is key[1] and st[0][2] == key[2]:
             return st[1]
         d = self._make_struct()
-        self._struct = (self.kproj, d)
+        self._struct = (key, d)
         return d
 
     def _make_struct(self):
@@ -183,7 +217,7 @@ class DeviceDesign:
         d.w, d.k, d.node = self._addr("w"), self._addr("k"), self._addr("node")
         d.nm, d.memb, d.mstart = self.nm, self._addr("memb"), N.ptr(self.mstart)
         d.imat_mcf = N.ptr(self.imat)
-        d.uhat, d.finer, d.kproj = N.ptr(self.uhat), N.ptr(self.finer), N.ptr(self.kproj)
+        d.uhat, d.finer, d.kproj = self._tab_ptr("uhat"), self._tab_ptr("finer"), self._tab_ptr("kproj")
         d.M, d.B, d.C = self._addr("M"), self._addr("B"), self._addr("C")
         return d
 
@@ -197,10 +231,12 @@ class DeviceDesign:
             allh = have + missing
             torch = self.torch
             nh = len(allh)
+            self._tab = None
             self.uhat = torch.empty([nh, max(self.nn, 1), 3, self.nw], dtype=torch.complex128, device=self.device)
             self.finer = torch.empty([nh, 6, self.nw], dtype=torch.complex128, device=self.device)
             self.kproj = torch.empty([nh, max(self.nn, 1), 3, self.nw], dtype=torch.complex128, device=self.device)
             self.headings = tuple(allh)
+            self._tabver = getattr(self, "_tabver", 0) + 1
             beta_t = torch.tensor(allh, dtype=torch.float64, device=self.device)
             d = self.struct()
             N.check(N.lib().rh_wave_tables(N.context(self.dev_index), ctypes.byref(d), N.ptr(beta_t),
@@ -220,6 +256,40 @@ class DeviceDesign:
         s = stream if stream is not None else N.stream_handle(self.torch, self.device)
         N.check(N.lib().rh_wave_tables(N.context(self.dev_index), ctypes.byref(d), N.ptr(self._beta_keep),
                                        N.ptr(self.uhat), N.ptr(self.finer), N.ptr(self.kproj), s), "rh_wave_tables")
+
+
+def descriptor_block(designs):
+    """The rh_design descriptors of many designs as one ctypes array, filled column-wise in a
+    numpy record array of rh_design's layout (DeviceDesign._make_struct's values, without a
+    ctypes field write per field and design); each design's descriptor cache is set from it."""
+    rec = np.zeros(len(designs), dtype=np.dtype(N.RhDesign))
+    cols = {k: [] for k in rec.dtype.names}
+    for d in designs:
+        base = d._packed.data_ptr()
+        lay = d._layout
+        for k in ("w", "k", "node", "memb", "M", "B", "C"):
+            cols[k].append(base + 8 * lay[k][0])
+        for k in ("uhat", "finer", "kproj"):
+            cols[k].append(d._tab_ptr(k).value or 0)
+        cols["mstart"].append(d.mstart.data_ptr())
+        cols["imat_mcf"].append(d.imat.data_ptr() if d.imat is not None else 0)
+        cols["nw"].append(d.nw)
+        cols["nn"].append(d.nn)
+        cols["nm"].append(d.nm)
+        cols["nhead"].append(0 if d.headings is None else len(d.headings))
+        cols["mb_per_bin"].append(1 if d.per_bin else 0)
+        cols["dw"].append(d.dw)
+        cols["depth"].append(d.depth)
+        cols["rho"].append(d.rho)
+        cols["g"].append(d.g)
+    cols["pdyn_rho_g"] = [1025.0 * 9.81] * len(designs)   # getWaveKin defaults (see _make_struct)
+    for k, v in cols.items():
+        rec[k] = v
+    arr = (N.RhDesign * len(designs)).from_buffer(rec)
+    arr._rec = rec                                         # (the array's memory)
+    for j, d in enumerate(designs):
+        d._struct = ((d.__dict__.get("_tabver", 0), d.__dict__.get("kproj"), d.headings), N.RhDesign.from_buffer_copy(arr[j]))
+    return arr
 
 
 def tabulate_batch(designs, design_idx, betas, launch_stream=None):
@@ -259,15 +329,14 @@ def tabulate_batch(designs, design_idx, betas, launch_stream=None):
         k = int(k)
         hs = ub[bounds[j]:bounds[j + 1]]
         bm[j, :k] = hs
-        d.headings = tuple(float(b) for b in hs)
-        shp = [k, max(d.nn, 1), 3, nw]
-        d.uhat, d.kproj = U[ou:ou + rows[j]].view(shp), K[ou:ou + rows[j]].view(shp)
-        d.finer = Fi[of:of + k * 6 * nw].view(k, 6, nw)
+        shp = (k, max(d.nn, 1), 3, nw)
+        d.set_tables({"uhat": (U, ou, shp), "kproj": (K, ou, shp), "finer": (Fi, of, (k, 6, nw))},
+                     [float(b) for b in hs])
         ou, of = ou + rows[j], of + k * 6 * nw
     beta_t = torch.tensor(bm, dtype=torch.float64, device=dev)
     for j, d in enumerate(sel):
         d._beta_keep = beta_t[j, :int(nh[j])]
-    arr = (N.RhDesign * len(sel))(*[d.struct() for d in sel])
+    arr = descriptor_block(sel)
     if launch_stream is not None:
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dev))

@@ -153,13 +153,14 @@ def prepare_batch(designs, cases, tables_stream=None):
     else:
         order = balanced_order(cases, head)
         gstart = None
-    i32 = dict(dtype=torch.int32, device=dev)
-    f64 = dict(dtype=torch.float64, device=dev)
-    return dict(design=torch.tensor(cases.design_idx, **i32), head=torch.tensor(head, **i32),
-                spectrum=torch.tensor(cases.spectrum, **i32), Hs=torch.tensor(cases.Hs, **f64),
-                Tp=torch.tensor(cases.Tp, **f64), gamma=torch.tensor(cases.gamma, **f64),
-                order=torch.tensor(order, **i32), head_host=head,
-                group_start=None if gstart is None else torch.tensor(gstart, **i32),
+    # two uploads (the int and the float case columns), each column a view
+    n = cases.n
+    ints = torch.from_numpy(np.concatenate([cases.design_idx, np.asarray(head, dtype=np.int32), cases.spectrum,
+                                            order]).astype(np.int32, copy=False)).to(dev)
+    flts = torch.from_numpy(np.concatenate([cases.Hs, cases.Tp, cases.gamma]).astype(np.float64, copy=False)).to(dev)
+    return dict(design=ints[:n], head=ints[n:2 * n], spectrum=ints[2 * n:3 * n], order=ints[3 * n:4 * n],
+                Hs=flts[:n], Tp=flts[n:2 * n], gamma=flts[2 * n:3 * n], head_host=head,
+                group_start=None if gstart is None else torch.tensor(gstart, dtype=torch.int32, device=dev),
                 ngroup=0 if gstart is None else len(gstart) - 1)
 
 

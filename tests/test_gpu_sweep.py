@@ -454,3 +454,23 @@ def test_oc4semi_sweep_native_prep_matches_python_prep():
     for j in range(len(idx)):
         assert rel(ra["Xi"][j], rb["Xi"][j]) < 1e-11, j
         np.testing.assert_allclose(ra["std"][j], rb["std"][j], rtol=1e-11, atol=1e-11 * rb["std"][j].max())
+
+
+def test_descriptor_block_equals_per_design_descriptors():
+    """prep.descriptor_block (a sweep block's rh_design descriptors filled column-wise) writes
+    the bytes DeviceDesign._make_struct writes for every design, with the lazily viewed shared
+    wave tables (DeviceDesign.set_tables) and after the views are made."""
+    from raft.batch import DesignBatch
+    from raft.solver import prepare_batch
+    from raft.sweep import sweep_multipliers, sweep_variant
+    base = load_design("VolturnUS-S_example")
+    designs = [sweep_variant(base, m) for m in sweep_multipliers(5, seed=3)]
+    B = DesignBatch(designs, statics={"C_moor": np.diag([7e4, 7e4, 2e4, 1e7, 1e7, 1e8])}, native=True)
+    cases = [dict(wave_heading=h, wave_height=4.0, wave_period=10.0) for h in (0.0, 30.0)]
+    cs = B.case_set(np.repeat(np.arange(5), 2), cases * 5)
+    prepare_batch(B.dds, cs)
+    for d in B.dds:
+        assert "uhat" not in d.__dict__                      # not viewed yet
+        assert bytes(d.struct()) == bytes(d._make_struct())
+        assert d.uhat.shape == (2, d.nn, 3, d.nw) and d.finer.shape == (2, 6, d.nw)
+        assert bytes(d.struct()) == bytes(d._make_struct())
