@@ -253,14 +253,27 @@ def cpu_baselines(qtf_seconds=10.0):
             "calibration": "port / reference time 0.84-1.11 (mean 0.99) on the four C2 golden cases, one core, the "
                            "reference re-timed case by case beside the port (tools/calibrate_cpu.py --interleave, "
                            "profiles/r04_v2/calibrate_cpu_interleaved.txt)"}
+    ratio, cal = qtf_calibration()
     qtf = {"value": npairs / dq, "unit": "pairs/s", "cores": P, "kind": "port",
            "sample": f"{npairs} pairs (24-frequency subsets of the C3 400 grid) through oracle/qtf_oracle.py "
-                     f"(vectorised over pairs, faster per pair than the reference's 19-23 ms) on {P} cores, "
-                     f"{dq:.1f} s wall ({cores_note}); CPU {model}",
-           "calibration": "uncalibrated, faster than the reference: the port is vectorised over pairs (about 1 "
-                          "ms/pair/core against the reference's per-pair loops at 19-23 ms/pair/core, BASELINE.md), "
-                          "so this baseline overstates the reference's CPU rate about 20x"}
+                     f"(vectorised over pairs) on {P} cores, {dq:.1f} s wall ({cores_note}); CPU {model}",
+           "calibration": f"port / reference time {ratio:.3f} on the reference's 24-frequency C3 subset (300 pairs), "
+                          f"one core, the reference timed beside the port ({cal}): the port is faster than the "
+                          "reference's per-pair, per-node loops, so the reference-equivalent rate on these cores is "
+                          "value x ratio",
+           "reference_equivalent_value": npairs / dq * ratio}
     return case, qtf
+
+
+QTF_CALIBRATION = os.path.join(ROOT, "profiles", "r06_v1", "qtf_cpu_calibration.json")
+
+
+def qtf_calibration():
+    """(port / reference time ratio of the QTF CPU port, its source): tools/calibrate_cpu.py --qtf,
+    measured in the build container where the reference runs (it does not travel to the box)."""
+    with open(QTF_CALIBRATION) as fh:
+        d = json.load(fh)
+    return float(d["mean_ratio"]), "tools/calibrate_cpu.py --qtf, " + os.path.relpath(QTF_CALIBRATION, ROOT)
 
 
 CPU_BASELINE_CACHE = os.path.join("/tmp", "raft_bench_cpu_baseline.json")

@@ -4,7 +4,8 @@ golden cases (tests/golden/c2_nw1000.npz: VolturnUS-S, nw = 1000), one core each
 reference's per-case seconds were recorded while it generated the fixture (out_seconds,
 tests/golden/make_golden.py run_solve).  Prints one line per case and the mean ratio.
 --interleave: time the reference again here, case by case beside the port (tools/ref_time_c2.py in
-a child process with make_golden.py's reference environment), so both see the same machine load."""
+a child process with make_golden.py's reference environment), so both see the same machine load.
+--qtf: the same for the QTF port on the reference's 24-frequency C3 subset (tools/ref_time_qtf.py)."""
 import json
 import os
 import subprocess
@@ -31,7 +32,34 @@ def reference_seconds(ic):
     return float(r["reference_s"]), int(r["iters"])
 
 
+def calibrate_qtf(reps=3):
+    """The QTF port (oracle/qtf_oracle.py, vectorised over pairs) against the reference's
+    calcQTF_slenderBody (its per-pair, per-node loops) on the same 24-frequency C3 subset, one
+    core each, alternating, so both see the same machine load.  The bench's QTF cpu_baseline
+    reports value x mean ratio as the reference-equivalent rate."""
+    from oracle import qtf_oracle as Q
+    T = dict(np.load(os.path.join(ROOT, "tests", "golden", "c3_qtf.npz")))
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1",
+               PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "tests", "golden", "refshim"), "/root/reference",
+                                           os.path.join(ROOT, "tests", "golden")]))
+    out = []
+    for rep in range(reps):
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ref_time_qtf.py")], env=env,
+                           capture_output=True, text=True, check=True, cwd=ROOT)
+        ref = json.loads(p.stdout.strip().splitlines()[-1])
+        t0 = time.perf_counter()
+        q = Q.qtf_slender(T, T["out_Xi0"], T["sub400_w"], T["sub400_k"], 0.0)
+        dt = time.perf_counter() - t0
+        err = float(np.linalg.norm(q - T["sub400_qtf"]) / np.linalg.norm(T["sub400_qtf"]))
+        out.append(dict(port_s=dt, reference_s=ref["reference_s"], ratio=dt / ref["reference_s"], port_err=err))
+        print(f"rep {rep}: port {dt:6.2f} s  reference {ref['reference_s']:6.2f} s  ratio {dt / ref['reference_s']:6.3f}"
+              f"  (300 pairs; port vs fixture {err:.1e})", flush=True)
+    print(json.dumps({"qtf": out, "pairs": 300, "mean_ratio": float(np.mean([o["ratio"] for o in out]))}))
+
+
 def main():
+    if "--qtf" in sys.argv:
+        return calibrate_qtf()
     interleave = "--interleave" in sys.argv
     T = dict(np.load(os.path.join(ROOT, "tests", "golden", "c2_nw1000.npz")))
     out = []
