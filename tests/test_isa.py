@@ -3,10 +3,11 @@
 Compiles rh_abi.hip to assembly (hipcc cross-compiles without a GPU) and fails on
   * dynamic register indexing (s_set_gpr_idx / v_movrel) in any kernel -- the lowering that
     faulted k_qtf_hankel on the box in round 2 (DESIGN.md §4);
-  * scratch (spill) instructions inside a streaming loop of any kernel of the shipped library
-    (a reload there drains the wave-table prefetch ring every node).  Only the general case
-    solve k_solve_cases<NB> (nw > 1024) is held to a ratchet of its measured counts; the gate
-    refuses a ratchet entry for any other kernel."""
+  * scratch (spill) instructions inside a streaming loop of any kernel of the shipped library,
+    counted twice: with a vector-memory load in flight (vmcnt modelled; a reload there drains the
+    wave-table prefetch ring every node) and anywhere in the loop.  Only the general case solve
+    k_solve_cases<NB> and the single-bin small-grid k_solve_lds<1, ...> are held to ratchets of
+    their measured counts; the gate refuses a ratchet entry for any other kernel."""
 import os
 import shutil
 import subprocess
@@ -28,7 +29,11 @@ def test_isa_gate():
     assert all(k in p.stdout for k in ("k_qtf_lk", "k_qtf_gemm", "k_array_resp<2, false>", "k_array_resp<2, true>"))
     assert "k_qtf_lcoef" not in p.stdout and "k_qtf_kay(" not in p.stdout
     ratchets = [ln for ln in p.stdout.splitlines() if "ratchet" in ln]
-    assert ratchets and all("k_solve_cases<" in ln for ln in ratchets), ratchets
+    assert ratchets and all("k_solve_cases<" in ln or "k_solve_lds<1," in ln for ln in ratchets), ratchets
+    # the benched kernels (C2, C4 fixed points, the QTF and array solves) have no scratch in any loop
+    for k in ("k_solve_lds<2, 512, false, 1>", "k_solve_lds<2, 128, true, 1>", "k_qtf_gemm", "k_qtf_lk"):
+        line = next(ln for ln in p.stdout.splitlines() if k in ln)
+        assert "in_flight=  0 in_loops=  0" in line, line
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")

@@ -36,8 +36,20 @@ import __graft_entry__ as G  # noqa: E402  (the build's translation units and th
 # them.  No other kernel can get a ratchet: an entry here must name a k_solve_cases instantiation.
 # (round 5: counted only while a load of the loop is in flight, in_flight_scratch; the ratchets
 # fell from 6 / 14 / 14 / 21 to the counts below)
-ALLOW = {"k_solve_cases<1>": 6, "k_solve_cases<2>": 0, "k_solve_cases<4>": 0, "k_solve_cases<8>": 8}
+# Ratchets (measured counts; a kernel may only go down).  Round 6 re-measured them with the
+# vector-memory counter modelled (vmcnt(N) waits, scratch reloads counted as loads):
+# the general k_solve_cases<2> / <4> / <8> show 5 / 5 / 13 scratch accesses with loads in flight
+# where the round-5 walk (reset only at vmcnt(0)) saw 0 / 0 / 8 -- the kernels did not change.
+ALLOW = {"k_solve_cases<1>": 6, "k_solve_cases<2>": 5, "k_solve_cases<4>": 5, "k_solve_cases<8>": 13}
+# the older measure beside it: scratch instructions anywhere inside a streaming loop,
+# outstanding loads or not (a reload after a full drain still costs an L2 round trip).  The
+# single-bin fast kernels (grids of <= 512 bins; C1-size designs, not the benched C2 / C4
+# kernels, which have none) reload 14-20 values in their node loops, never with a load in flight.
+ALLOW_LOOP = {"k_solve_cases<1>": 12, "k_solve_cases<2>": 14, "k_solve_cases<4>": 14, "k_solve_cases<8>": 22,
+              "k_solve_lds<1, 128, true, 1>": 20, "k_solve_lds<1, 256, false, 1>": 14,
+              "k_solve_lds<1, 512, false, 1>": 14}
 assert all(k.startswith("k_solve_cases<") for k in ALLOW)
+assert all(k.startswith(("k_solve_cases<", "k_solve_lds<1,")) for k in ALLOW_LOOP)
 DYN_INDEX = re.compile(r"^\s*(s_set_gpr_idx\w*|v_movrel\w*)")
 SCRATCH = re.compile(r"^\s*(scratch_|buffer_\w+.*\boff(en)?\b.*s\[0:3\])")
 LABEL = re.compile(r"^(\.LBB\w+|\w+):")
@@ -85,26 +97,34 @@ def kernels(lines):
     return out
 
 
-VMCNT0 = re.compile(r"^\s*s_waitcnt\s+(.*\s)?vmcnt\(0\)")
+VMCNT = re.compile(r"^\s*s_waitcnt\s+(?:.*\s)?vmcnt\((\d+)\)")
+SCRATCH_LOAD = re.compile(r"^\s*(scratch_load|buffer_load\w*.*\boff(en)?\b.*s\[0:3\])")
 
 
 def in_flight_scratch(body, a, b):
     """Scratch instructions of the loop [a, b] issued while one of its vector-memory loads is
     still outstanding: the hazard (a reload waits behind the ring's loads, since they share
-    vmcnt, and drains it).  Walked in program order from the loop head; the loads still
-    outstanding at the back edge (a prefetch ring carried into the next iteration) count as
-    outstanding at the head.  A scratch access after an `s_waitcnt vmcnt(0)` and before the next
-    load -- e.g. around the LU of a bin, once its loads are consumed -- drains nothing."""
+    vmcnt, and drains it).  Walked in program order from the loop head with the vector-memory
+    counter modelled: every load (wave-table stream and scratch reload alike) adds one, and
+    `s_waitcnt vmcnt(N)` leaves at most N outstanding.  The loads still outstanding at the back
+    edge (a prefetch ring carried into the next iteration) count as outstanding at the head.
+    A scratch access once the counter is 0 -- e.g. around the LU of a bin, after its loads are
+    consumed -- drains nothing.  (Straight-line walk: a branch inside the loop is followed as if
+    both sides ran in order, which can only over-count.)"""
     def walk(carried):
         out, hits = carried, []
         for i in range(a, b + 1):
             ln = body[i]
-            if VMCNT0.match(ln):
-                out = 0
+            m = VMCNT.match(ln)
+            if m:
+                out = min(out, int(m.group(1)))
+            elif SCRATCH.match(ln):
+                if out > 0:
+                    hits.append(i)
+                if SCRATCH_LOAD.match(ln):
+                    out += 1
             elif STREAM.match(ln):
                 out += 1
-            elif SCRATCH.match(ln) and out > 0:
-                hits.append(i)
         return out, hits
     carried, _ = walk(0)
     return walk(carried)[1]
@@ -126,7 +146,9 @@ def analyse(body):
     dyn = [ln.strip() for ln in body if DYN_INDEX.match(ln)]
     scr = [i for i, ln in enumerate(body) if SCRATCH.match(ln)]
     scr_inner = [i for a, b in inner for i in in_flight_scratch(body, a, b)]
-    return {"dyn": dyn, "scratch": len(scr), "scratch_inner": len(scr_inner), "loops": len(loops), "inner": len(inner)}
+    scr_loop = [i for a, b in inner for i in range(a, b + 1) if SCRATCH.match(body[i])]
+    return {"dyn": dyn, "scratch": len(scr), "scratch_inner": len(scr_inner), "scratch_loop": len(scr_loop),
+            "loops": len(loops), "inner": len(inner)}
 
 
 def demangle(n):
@@ -153,16 +175,22 @@ def main():
         verdict = "ok"
         if r["dyn"]:
             verdict = "FAIL dynamic register indexing: " + "; ".join(sorted(set(r["dyn"])))
-        elif hot and r["scratch_inner"]:
+        elif hot and (r["scratch_inner"] or r["scratch_loop"]):
             allow = max([v for k, v in ALLOW.items() if k in dn] or [0])
+            allow_loop = max([v for k, v in ALLOW_LOOP.items() if k in dn] or [0])
             if r["scratch_inner"] > allow:
                 verdict = f"FAIL {r['scratch_inner']} scratch instructions inside streaming loops (allowed {allow})"
+            elif r["scratch_loop"] > allow_loop:
+                verdict = (f"FAIL {r['scratch_loop']} scratch instructions anywhere in streaming loops "
+                           f"(allowed {allow_loop})")
             else:
-                verdict = f"ok (ratchet: {r['scratch_inner']} <= {allow} in streaming loops, general path)"
+                verdict = (f"ok (ratchet: {r['scratch_inner']} <= {allow} with loads in flight, {r['scratch_loop']} <= "
+                           f"{allow_loop} anywhere in streaming loops, general path)")
         if verdict.startswith("FAIL"):
             fails.append(dn)
         rows.append(f"{dn:70s} hot={int(hot)} loops={r['loops']:3d} inner={r['inner']:3d} "
-                    f"scratch={r['scratch']:4d} scratch_in_streaming_loops={r['scratch_inner']:3d}  {verdict}")
+                    f"scratch={r['scratch']:4d} in_flight={r['scratch_inner']:3d} in_loops={r['scratch_loop']:3d}  "
+                    f"{verdict}")
     text = "# tools/isa_check.py: gfx950 device assembly of " + " + ".join(u for u, _ in G.UNITS) + "\n" + "\n".join(rows) + "\n"
     text += f"# {len(ks)} kernels, {len(fails)} failing\n"
     print(text)
