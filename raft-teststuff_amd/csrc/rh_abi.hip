@@ -201,7 +201,7 @@ extern "C" {
 
 const char* rh_last_error(void) { return g_err.c_str(); }
 
-int rh_version(void) { return 4; }
+int rh_version(void) { return 5; }
 
 // (rh_prof_read / rh_wgt_read of instrumented builds live in rh_solve_fast.hip, beside the counters)
 
