@@ -418,6 +418,19 @@ typedef struct {
                               runs as FP64 MFMA GEMMs (rh_qtf_mfma.hip); 0: the per-pair kernel     */
 } rh_qtf_design;
 
+/* The static tables of one FOWT for a QTF at heading beta (rad), on the host: the geometry
+ * bookkeeping of FOWT.calcQTF_slenderBody (raft/raft_fowt.py:1461-1502, 1532-1587, 1604-1625)
+ * and Member.correction_KAY (raft/raft_member.py:1111-1200) that rh_qtf_design points at.
+ * Host code only (no device, no ctx); replaces raft/qtf.py build_tables, which states the
+ * same tables in NumPy.  rec: nmemb member records back to back, rec_len doubles (format:
+ * csrc/rh_qtf_host.h; writer raft/qtf.py member_record).  out (cap doubles) receives
+ * qnode [RH_QN_COUNT][nq], qmemb [RH_QM_COUNT][nmq] and kray [RH_KR_COUNT][nkr] back to back;
+ * iout (capi ints) qmstart [nmq+1] and kstart [nmq+1]; counts = {nq, nmq, nkr}.  RH_EINVAL
+ * for a malformed record or too small a capacity (46 + 6 doubles per node and 36 per member
+ * always suffice). */
+int rh_qtf_tables(int nmemb, const double* rec, long long rec_len, double beta, double* out, long long cap, int* iout,
+                  long long capi, int* counts);
+
 /* Device workspace (bytes) rh_qtf_slender needs for a design. */
 long long rh_qtf_workspace_bytes(const rh_qtf_design* q);
 

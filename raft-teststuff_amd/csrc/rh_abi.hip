@@ -26,6 +26,7 @@
 #include "../../tools/ubench/variants_src/rh_qtf_variants.hip"  // k_qtf_gemm32, k_qtf_lcoef + k_qtf_kay (rh_set_qtf_path 2, 3)
 #endif
 #include "rh_prep.h"       // host-only: native per-design preparation (rh_prep_designs)
+#include "rh_qtf_host.h"   // host-only: the static QTF tables of a FOWT (rh_qtf_tables)
 
 // One staging slot of the design descriptor array.  A context cycles through kDescSlots of
 // them, so a launch never waits for the descriptors of the previous one: the host blocks only
@@ -201,7 +202,7 @@ extern "C" {
 
 const char* rh_last_error(void) { return g_err.c_str(); }
 
-int rh_version(void) { return 5; }
+int rh_version(void) { return 6; }
 
 // (rh_prof_read / rh_wgt_read of instrumented builds live in rh_solve_fast.hip, beside the counters)
 
@@ -1091,6 +1092,35 @@ long long rh_prep_imat(const rh_prep* p, int design, rh_c128* imat) {
   const auto& v = p->res[design].imat;
   if (imat && !v.empty()) std::memcpy(imat, v.data(), v.size() * sizeof(double));
   return (long long)(v.size() / 2);
+}
+
+// ------------------------------------------------------------------ QTF tables (host)
+int rh_qtf_tables(int nmemb, const double* rec, long long rec_len, double beta, double* out, long long cap, int* iout,
+                  long long capi, int* counts) {
+  if (nmemb < 0 || (nmemb > 0 && !rec) || rec_len < 0 || !out || !iout || !counts)
+    return fail(RH_EINVAL, "rh_qtf_tables: bad arguments (nmemb=%d)", nmemb);
+  std::vector<rhq::MemberRec> mems(nmemb);
+  long long off = 0;
+  for (int i = 0; i < nmemb; ++i) {
+    const long long n = rhq::parse(rec + off, rec_len - off, mems[i]);
+    if (n < 0) return fail(RH_EINVAL, "rh_qtf_tables: malformed member record %d", i);
+    off += n;
+  }
+  if (off != rec_len) return fail(RH_EINVAL, "rh_qtf_tables: %lld doubles after the last member record", rec_len - off);
+  long long nq, nmq, nkr;
+  rhq::count(mems, nq, nmq, nkr);
+  if (rhq::kQN * nq + rhq::kQM * nmq + rhq::kKR * nkr > cap || 2 * (nmq + 1) > capi)
+    return fail(RH_EINVAL, "rh_qtf_tables: output capacity too small (%lld doubles, %lld ints)", cap, capi);
+  const rhq::Tables T{out, out + rhq::kQN * nq, out + rhq::kQN * nq + rhq::kQM * nmq, iout, iout + nmq + 1, nq, nmq, nkr};
+  try {
+    rhq::build(mems, beta, T);
+  } catch (const std::exception& e) {
+    return fail(RH_EINVAL, "%s", e.what());
+  }
+  counts[0] = (int)nq;
+  counts[1] = (int)nmq;
+  counts[2] = (int)nkr;
+  return RH_OK;
 }
 
 void rh_prep_free(rh_prep* p) { delete p; }

@@ -130,6 +130,8 @@ def lib():
                 "rh_prep_designs": [ctypes.c_int, _p, _p, ctypes.c_int, _p, _p, ctypes.c_int, ctypes.POINTER(_p)],
                 "rh_prep_layout": [_p, _p],
                 "rh_prep_copy": [_p, _p, _p, _p],
+                "rh_qtf_tables": [ctypes.c_int, _p, ctypes.c_longlong, ctypes.c_double, _p, ctypes.c_longlong, _p,
+                                  ctypes.c_longlong, _p],
             }.items():
                 fn = getattr(L, name)
                 fn.argtypes = args

@@ -1,7 +1,10 @@
 """Device tables for the slender-body QTF.
 
 Per design, per second-order grid and heading: the static node/member/Kim-Yue tables of
-include/rafthip.h (rh_qtf_design).  The only host arithmetic is geometry bookkeeping; the
+include/rafthip.h (rh_qtf_design), built in librafthip on the host (rh_qtf_tables, from one
+record per member: member_record) -- build_tables below states the same tables in NumPy and is
+what tests/test_qtf_tables.py checks the native ones against.  The only host arithmetic is
+geometry bookkeeping; the
 Hankel-function table 0.5 (H1_{n-1}(kR) - H1_{n+1}(kR)) that the reference evaluates with
 scipy.special.hankel1 (raft/raft_member.py:1104-1107) is built on the device
 (rh_qtf_hankel), and every per-pair quantity is computed on the device by rh_qtf_slender.
@@ -126,6 +129,66 @@ def build_tables(fowt, w2, k2, beta, host_hankel=False):
                 kstart=np.array(kstart, dtype=np.int32), rho=rho, g=g, h=h)
 
 
+def member_record(mem):
+    """One member's record for rh_qtf_tables (format: csrc/rh_qtf_host.h)."""
+    return np.concatenate(((1.0 if mem.shape == "circular" else 0.0, 1.0 if mem.MCF else 0.0, len(mem.r),
+                            len(mem.stations)), mem.rA, mem.rB, mem.p1, mem.p2, mem.q, mem.p1Mat, mem.p2Mat, mem.qMat,
+                           mem.r, mem.ls, mem.dls, mem.ds, mem.drs, mem.a_i, mem.stations, mem.Ca_p1, mem.Ca_p2,
+                           mem.Ca_End), axis=None)
+
+
+def table_capacity(fowt):
+    """Doubles that native_tables may need for a FOWT's tables and index tables (an upper
+    bound: every node submerged and a Kim & Yue row per node)."""
+    mems = fowt.memberList
+    return (QN_COUNT + KR_COUNT) * sum(len(m.r) for m in mems) + QM_COUNT * len(mems) + len(mems) + 1
+
+
+def native_tables(fowt, beta, buf=None, off=0):
+    """rh_qtf_tables: the tables of build_tables (without the Hankel table), written into
+    buf[off:] (float64; allocated when None) as qnode | qmemb | kray back to back, followed by
+    qmstart | kstart as int32 bytes.  Returns (buf, end, dict of numpy views like build_tables)."""
+    mems = fowt.memberList
+    rec = np.concatenate([member_record(m) for m in mems]) if mems else np.zeros(0)
+    capi = 2 * (len(mems) + 1)
+    cap = table_capacity(fowt) - capi // 2
+    need = off + cap + capi // 2
+    if buf is None:
+        buf = np.empty(need)
+    elif buf.size < need:
+        raise ValueError("native_tables: buffer too small")
+    iout = np.empty(capi, dtype=np.int32)
+    cnt = np.zeros(3, dtype=np.int32)
+    tab = buf[off:]
+    N.check(N.lib().rh_qtf_tables(len(mems), rec.ctypes.data, rec.size, float(beta), tab.ctypes.data, cap,
+                                  iout.ctypes.data, capi, cnt.ctypes.data), "rh_qtf_tables")
+    nq, nmq, nkr = (int(x) for x in cnt)
+    o1, o2, o3 = QN_COUNT * nq, QN_COUNT * nq + QM_COUNT * nmq, QN_COUNT * nq + QM_COUNT * nmq + KR_COUNT * nkr
+    ni = 2 * (nmq + 1)
+    ints = tab[o3:o3 + (ni + 1) // 2].view(np.int32)[:ni]
+    ints[:] = iout[:ni]
+    t = dict(qnode=tab[:o1].reshape(QN_COUNT, nq), qmemb=tab[o1:o2].reshape(QM_COUNT, nmq),
+             kray=tab[o2:o3].reshape(KR_COUNT, nkr), hank=None, qmstart=ints[:nmq + 1], kstart=ints[nmq + 1:],
+             rho=float(fowt.rho_water), g=float(fowt.g), h=float(fowt.depth))
+    return buf, off + o3 + (ni + 1) // 2, t
+
+
+_STAGING = {}
+
+
+def _staging(torch, dev, n):
+    """A pinned host buffer of >= n doubles per device, reused: the tables of a new QtfDevice are
+    written there natively and go up in one asynchronous copy.  Waits for the previous copy out
+    of it first."""
+    st = _STAGING.get(dev.index)
+    if st is not None:
+        st[1].synchronize()
+    if st is None or st[0].numel() < n:
+        st = [torch.empty(max(n, 8192), dtype=torch.float64, pin_memory=True), torch.cuda.Event()]
+        _STAGING[dev.index] = st
+    return st
+
+
 class QtfDevice:
     """Device copy of the QTF tables + workspace for one (design, grid, heading)."""
 
@@ -134,32 +197,35 @@ class QtfDevice:
         self.torch = torch
         self.dev = torch.device("cuda", device)
         self.dev_index = device
-        t = build_tables(fowt, w2, k2, beta)
-        self.host = t
-        f64 = dict(dtype=torch.float64, device=self.dev)
-        self.n2 = len(w2)
+        self.n2 = n2 = len(w2)
         self.beta = float(beta)
+        # the grid, the three tables and the two index tables, written natively into one pinned
+        # buffer, in one asynchronous upload
+        stage = _staging(torch, self.dev, 2 * n2 + table_capacity(fowt))
+        host = stage[0].numpy()
+        host[:n2] = w2
+        host[n2:2 * n2] = k2
+        _, end, t = native_tables(fowt, beta, host, 2 * n2)
+        dev_flat = stage[0][:end].to(self.dev, non_blocking=True)
+        stage[1].record(torch.cuda.current_stream(self.dev))
+        self.host = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in t.items()}
         self.nq, self.nmq, self.nkr = t["qnode"].shape[1], t["qmemb"].shape[1], t["kray"].shape[1]
-        pad = lambda a, rows: a if a.shape[1] else np.zeros([rows, 1])
-        # the three tables and the grid in one upload, the two index tables in another
-        parts = [pad(t["qnode"], QN_COUNT), pad(t["qmemb"], QM_COUNT), pad(t["kray"], KR_COUNT)]
-        flat = np.concatenate([np.asarray(w2, dtype=float), np.asarray(k2, dtype=float)] + [a.ravel() for a in parts])
-        dev_flat = torch.from_numpy(flat).to(self.dev)
-        self.w2, self.k2 = dev_flat[:self.n2], dev_flat[self.n2:2 * self.n2]
-        off = 2 * self.n2
+        self.w2, self.k2 = dev_flat[:n2], dev_flat[n2:2 * n2]
+        off = 2 * n2
         views = []
-        for a in parts:
-            views.append(dev_flat[off:off + a.size].view(a.shape))
-            off += a.size
+        for rows, n in ((QN_COUNT, self.nq), (QM_COUNT, self.nmq), (KR_COUNT, self.nkr)):
+            views.append(dev_flat[off:off + rows * n].view(rows, n))
+            off += rows * n
         self.qnode, self.qmemb, self.kray = views
+        ni = 2 * (self.nmq + 1)
+        ints = dev_flat[off:off + (ni + 1) // 2].view(torch.int32)[:ni]
+        self.qmstart, self.kstart = ints[:self.nmq + 1], ints[self.nmq + 1:]
         # Kim & Yue Hankel table [nkr][n2][12], built on the device from k2 and the radii
         self.hank = (torch.empty if self.nkr else torch.zeros)([max(self.nkr, 1), self.n2, 12], dtype=torch.complex128,
                                                                device=self.dev)
         if self.nkr:
             N.check(N.lib().rh_qtf_hankel(N.context(device), self.n2, N.ptr(self.k2), self.nkr, N.ptr(self.kray),
                                           N.ptr(self.hank), N.stream_handle(torch, self.dev)), "rh_qtf_hankel")
-        ints = torch.from_numpy(np.concatenate([t["qmstart"], t["kstart"]]).astype(np.int32)).to(self.dev)
-        self.qmstart, self.kstart = ints[:len(t["qmstart"])], ints[len(t["qmstart"]):]
         self.rho, self.g, self.h = t["rho"], t["g"], t["h"]
         # the MFMA pair path needs the upper triangle to be i2 >= i1 and nk = k2 - k1
         w2a, k2a = np.asarray(w2, dtype=float), np.asarray(k2, dtype=float)

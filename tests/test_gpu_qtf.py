@@ -280,3 +280,25 @@ def test_force_spectrum_mode_matches_reference(T):
     np.testing.assert_allclose(fm, G["c3_fmean"], rtol=RTOL, atol=RTOL * np.abs(G["c3_fmean"]).max())
     with pytest.raises(ValueError):
         f.calcHydroForce_2ndOrd(f.beta[0], G["c3_S0"], interpMode="bogus")
+
+
+@pytest.mark.gpu
+def test_device_tables_are_the_numpy_tables(T):
+    """QtfDevice's tables (rh_qtf_tables on the host, one pinned asynchronous upload) on the
+    device equal raft/qtf.py build_tables bit for bit, for two QtfDevices built back to back
+    through the one staging buffer (the second must not overwrite the first's upload)."""
+    import torch
+    from raft.hydro_math import wave_numbers
+    from raft.qtf import QtfDevice, build_tables
+    m, f = make(T)
+    w2 = np.arange(0.04, 0.35 + 0.5 * 0.04, 0.000825) * 2 * np.pi
+    k2 = wave_numbers(w2, f.depth)
+    qds = [QtfDevice(f, w2, k2, b, 0) for b in (0.0, np.deg2rad(30.0))]
+    torch.cuda.synchronize()
+    for qd, b in zip(qds, (0.0, np.deg2rad(30.0))):
+        ref = build_tables(f, w2, k2, b)
+        np.testing.assert_array_equal(qd.w2.cpu().numpy(), w2)
+        np.testing.assert_array_equal(qd.k2.cpu().numpy(), k2)
+        for k in ("qnode", "qmemb", "kray", "qmstart", "kstart"):
+            np.testing.assert_array_equal(getattr(qd, k).cpu().numpy(), ref[k], err_msg=k)
+            np.testing.assert_array_equal(qd.host[k], ref[k], err_msg=k)
