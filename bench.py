@@ -364,12 +364,15 @@ def build_qtf(device):
     return T, f, dd, X, M66, w2, k2
 
 
+QTF_NEW_REPS = 9
+
+
 def bench_qtf(device, steps, warmup, world, rank, dist):
     """C3 throughput: one 400x400 QTF per step (upper triangle computed, Hermitian fill), 16 x 16
     pair tiles sharded over the ranks with one all-gather of packed pairs.  end_to_end_ms: a
-    QTF of a new (design, grid, heading) in a warm process, including its tables (host
-    geometry, device Hankel table) and their upload; first_call_ms: the same for the first QTF
-    of the process, which also loads the QTF kernels."""
+    QTF of a new (design, grid, heading) in a warm process, including its tables (native host
+    geometry, device Hankel table) and their upload, the median of QTF_NEW_REPS such QTFs;
+    first_call_ms: the first QTF of the process, which also loads the QTF kernels."""
     import torch
     from raft.qtf import QtfDevice
     T, f, dd, X, M66, w2, k2 = build_qtf(device)
@@ -383,13 +386,16 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
     torch.cuda.synchronize()
     t_first = time.perf_counter() - t0     # first QTF of the process: includes loading its kernels
     del qd, q
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()               # a new (design, grid, heading) in a warm process
-    qd = QtfDevice(f, w2, k2, 0.0, device)
-    t_tables = time.perf_counter() - t0
-    q = qd.qtf(dd.w, X, M66, group=group)
-    torch.cuda.synchronize()
-    t_e2e = time.perf_counter() - t0
+    e2e, tab = [], []
+    for _ in range(QTF_NEW_REPS):          # a new (design, grid, heading) in a warm process: median of 9
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        qd = QtfDevice(f, w2, k2, 0.0, device)
+        tab.append(time.perf_counter() - t0)
+        q = qd.qtf(dd.w, X, M66, group=group)
+        torch.cuda.synchronize()
+        e2e.append(time.perf_counter() - t0)
+    t_e2e, t_tables = float(np.median(e2e)), float(np.median(tab))
     qm = qd.host["qmemb"]
     nkay = qd.nkr - int((qm[29] != 0).sum()) if qd.nmq else 0     # KAY rows minus one waterline row per member
     nwl = int((qm[0] != 0).sum()) if qd.nmq else 0

@@ -12,6 +12,7 @@ own designs, so the host preparation scales with the rank count too); the per-ca
 outputs are all-gathered once at the end (raft/parallel.py gather_cases).
 """
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -31,7 +32,7 @@ class DesignBatch:
     """
 
     def __init__(self, designs, statics=None, r6=None, device=0, pool=None, light=False, native=False, specs=None,
-                 threads=None):
+                 threads=None, prepared=None):
         """pool: optional multiprocessing pool (see host_pool) that prepares the designs on
         the host in parallel; results are identical to the serial path.
         light: keep only what the device side needs of each design (HostDesign: its tables,
@@ -42,20 +43,24 @@ class DesignBatch:
         specs: the designs' spec records, already flattened (native_prep.sweep_specs; implies
         native); `designs` then only supplies the site and the frequency grid.
         threads: host threads of the native preparation (default: the pool's size, else
-        min(16, this process's cores))."""
+        min(16, this process's cores)).
+        prepared: the native preparation of exactly these designs, already made
+        (prepare_native, e.g. on another host thread while the previous block solves; implies
+        native)."""
         t0 = time.perf_counter()
         if isinstance(statics, dict) or statics is None:
             statics = [statics] * len(designs)
         if len(statics) != len(designs):
             raise ValueError("statics: one dict for all designs or one per design")
         self._prepared = None
-        if native or specs is not None or light:
-            for d in designs:
+        if native or specs is not None or light or prepared is not None:
+            for d in {id(d): d for d in designs}.values():     # (a sweep passes one base dict many times)
                 if get_from_dict((d or {}).get("platform") or {}, "potSecOrder", dtype=int, default=0) > 0:
                     raise NotImplementedError("DesignBatch: second-order loads (potSecOrder > 0) need the full design "
                                               "models (native=False, light=False): the QTFs are built there")
-        if native or specs is not None:
-            self.models = self._native(designs, statics, r6, device, pool, specs, threads)
+        if native or specs is not None or prepared is not None:
+            P = prepared if prepared is not None else prepare_native(designs, statics, r6, pool, specs, threads)
+            self.models = self._native(designs, P, device)
         else:
             jobs = [(d, st, r6, device, light) for d, st in zip(designs, statics)]
             if pool is not None and len(jobs) > 1:
@@ -75,31 +80,13 @@ class DesignBatch:
         self.dds = self._upload(device)
         self.upload_seconds = time.perf_counter() - t0
 
-    def _native(self, designs, statics, r6, device, pool, specs=None, threads=None):
-        """rh_prep_designs over every design (raft/native_prep.py); returns HostDesign-like
-        records holding views of the one packed host array."""
-        from .hydro_math import wave_numbers
-        from .native_prep import PreparedDesigns
-        w = Model.frequency_grid(designs[0])
-        depth = get_from_dict(designs[0]["site"], "water_depth", dtype=float)
-        for d in designs[1:]:
-            if d is designs[0]:
-                continue
-            if get_from_dict(d["site"], "water_depth", dtype=float) != depth or \
-                    not np.array_equal(Model.frequency_grid(d), w):
-                raise ValueError("all designs of a batch must share the frequency grid and the site")
-        k = wave_numbers(w, depth)
-        if specs is None:
-            jobs = [(d, None if r6 is None else np.asarray(r6, dtype=float), st) for d, st in zip(designs, statics)]
-            if pool is not None and len(jobs) > 1:
-                specs = pool.map(_spec_job, jobs, chunksize=max(1, len(jobs) // (4 * pool._processes)))
-            else:
-                specs = [_spec_job(j) for j in jobs]
-        elif len(specs) != len(designs):
-            raise ValueError("DesignBatch: one spec record per design")
-        import os
-        nt = threads or (pool._processes if pool is not None else min(16, len(os.sched_getaffinity(0))))
-        P = self._prepared = PreparedDesigns(specs, w, k, nthreads=nt)
+    def _native(self, designs, P, device):
+        """HostDesign-like records of natively prepared designs (prepare_native), holding
+        views of the one packed host array."""
+        if P.nd != len(designs):
+            raise ValueError("DesignBatch: the native preparation is not one of these designs")
+        self._prepared = P
+        w, k, depth = P.w, P.k, P.depth
         st0 = designs[0].get("settings", {})
         nIter = get_from_dict(st0, "nIter", default=15, dtype=int)
         XiStart = get_from_dict(st0, "XiStart", default=0.1, dtype=float)
@@ -122,8 +109,14 @@ class DesignBatch:
         dev = torch.device("cuda", device)
         if self._prepared is not None:     # native: already one packed host array
             P = self._prepared
-            packed = torch.from_numpy(P.packed).to(dev)
-            mst = torch.from_numpy(P.mstart).to(dev)
+            if getattr(P, "pinned", None) is not None:    # one asynchronous copy out of page-locked memory
+                flat = P.pinned.to(dev, non_blocking=True)
+                npk = P.packed.size
+                packed = flat[:npk]
+                mst = flat[npk:].view(torch.int32)[:P.mstart.size]
+            else:
+                packed = torch.from_numpy(P.packed).to(dev)
+                mst = torch.from_numpy(P.mstart).to(dev)
             dds = []
             for i, f in enumerate(self.fowts):
                 o, n, mo, nn, nm = (int(x) for x in P.info[i])
@@ -146,30 +139,12 @@ class DesignBatch:
 
     def case_set(self, design_idx, cases):
         """CaseSet of (design index, case dict) pairs; one sea state per case."""
-        hd, sp, Hs, Tp, gm = [], [], [], [], []
-
-        def one(c, k, dflt=None):
-            v = c.get(k, dflt)
-            if isinstance(v, (list, tuple, np.ndarray)):
-                if len(v) != 1:
-                    raise NotImplementedError("DesignBatch: one sea state per case")
-                return v[0]
-            return v
-        for c in cases:
-            hd.append(float(one(c, "wave_heading", 0)))
-            sp.append(str(one(c, "wave_spectrum", "JONSWAP")))
-            Hs.append(float(one(c, "wave_height")))
-            Tp.append(float(one(c, "wave_period")))
-            gm.append(float(one(c, "wave_gamma", 0)))
-        return CaseSet(np.asarray(design_idx, dtype=np.int32), hd, sp, Hs, Tp, gm)
+        return case_set_of(design_idx, cases)
 
     def case_set_grid(self, design_idx, state_idx, sea_states):
         """CaseSet of cases given as (design index, index into `sea_states`): a sweep's
         design x sea-state product without one case dict per case."""
-        cs0 = self.case_set(np.zeros(len(sea_states), dtype=np.int32), sea_states)   # each sea state parsed once
-        si = np.asarray(state_idx, dtype=np.int64)
-        return CaseSet(np.asarray(design_idx, dtype=np.int32), cs0.heading[si], cs0.spectrum[si], cs0.Hs[si],
-                       cs0.Tp[si], cs0.gamma[si])
+        return case_set_grid(design_idx, state_idx, case_set_of(np.zeros(len(sea_states), dtype=np.int32), sea_states))
 
     def solve(self, design_idx, cases, tol=0.01, want=("psd", "std", "zeta", "B_drag"), prepared=None):
         """Drag fixed point + response of every case in one device call.  Returns the
@@ -232,6 +207,33 @@ class DesignBatch:
         return views, idx, owners
 
 
+def case_set_of(design_idx, cases):
+    """CaseSet of (design index, case dict) pairs; one sea state per case."""
+    hd, sp, Hs, Tp, gm = [], [], [], [], []
+
+    def one(c, k, dflt=None):
+        v = c.get(k, dflt)
+        if isinstance(v, (list, tuple, np.ndarray)):
+            if len(v) != 1:
+                raise NotImplementedError("DesignBatch: one sea state per case")
+            return v[0]
+        return v
+    for c in cases:
+        hd.append(float(one(c, "wave_heading", 0)))
+        sp.append(str(one(c, "wave_spectrum", "JONSWAP")))
+        Hs.append(float(one(c, "wave_height")))
+        Tp.append(float(one(c, "wave_period")))
+        gm.append(float(one(c, "wave_gamma", 0)))
+    return CaseSet(np.asarray(design_idx, dtype=np.int32), hd, sp, Hs, Tp, gm)
+
+
+def case_set_grid(design_idx, state_idx, cs0):
+    """The CaseSet of cases (design index, index into the parsed sea states cs0)."""
+    si = np.asarray(state_idx, dtype=np.int64)
+    return CaseSet(np.asarray(design_idx, dtype=np.int32), cs0.heading[si], cs0.spectrum[si], cs0.Hs[si],
+                   cs0.Tp[si], cs0.gamma[si])
+
+
 def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, pool=None, chunks=4, tol=0.01,
                 want=("psd", "std"), timings=None, specs=None, threads=None, first=1.0,
                 last=1.0):
@@ -280,31 +282,43 @@ def _solve_sweep(designs, statics, design_idx, state_idx, sea_states, device, po
         raise ValueError("solve_sweep: cases must be design-major (non-decreasing design index)")
     nd = len(designs)
     cuts = sweep_cuts(nd, chunks, first, last)
+    blocks = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
     dev = torch.device("cuda", device)
     compute = torch.cuda.current_stream(dev)
     copy = _copy_stream(dev)
+    cs_all = case_set_of(np.zeros(len(sea_states), dtype=np.int32), sea_states)   # each sea state parsed once
+
+    def prep(a, b):
+        sp = None if specs is None else (specs(a, b) if callable(specs) else specs[a:b])
+        st = statics if isinstance(statics, dict) or statics is None else statics[a:b]
+        return prepare_native(designs[a:b], st, None, pool, sp, threads, pinned=True)
+
     parts, keep = [], []
-    for a, b in zip(cuts[:-1], cuts[1:]):
-        if b <= a:
-            continue
-        lo, hi = np.searchsorted(design_idx, [a, b])
-        t0 = time.perf_counter()
-        with torch.cuda.stream(copy):
-            sp = None if specs is None else (specs(a, b) if callable(specs) else specs[a:b])
-            B = DesignBatch(designs[a:b], statics=statics if isinstance(statics, dict) or statics is None
-                            else statics[a:b], device=device, pool=pool, native=True, specs=sp, threads=threads)
-            t1 = time.perf_counter()
-            cs = B.case_set_grid(design_idx[lo:hi] - a, state_idx[lo:hi], sea_states)
-            prep = prepare_batch(B.dds, cs, tables_stream=compute)
-            ready = torch.cuda.Event()
-            ready.record(copy)
-        compute.wait_event(ready)
-        t2 = time.perf_counter()
-        res = B.solve(None, cs, tol=tol, want=want, prepared=prep)   # on the solve stream
-        if timings is not None:
-            timings.append((t1 - t0, t2 - t1, time.perf_counter() - t2, B.host_seconds, B.upload_seconds))
-        parts.append(res)
-        keep.append((B, cs, prep, res))
+    # The native preparation of block k+1 runs on a worker thread (rh_prep_designs releases the
+    # GIL) while this thread uploads block k, tabulates it and enqueues its solve.
+    with ThreadPoolExecutor(1) as ex:
+        nxt = ex.submit(prep, *blocks[0]) if blocks else None
+        for j, (a, b) in enumerate(blocks):
+            lo, hi = np.searchsorted(design_idx, [a, b])
+            t0 = time.perf_counter()
+            P = nxt.result()
+            tw = time.perf_counter() - t0
+            nxt = ex.submit(prep, *blocks[j + 1]) if j + 1 < len(blocks) else None
+            with torch.cuda.stream(copy):
+                B = DesignBatch(designs[a:b], statics=statics if isinstance(statics, dict) or statics is None
+                                else statics[a:b], device=device, prepared=P)
+                t1 = time.perf_counter()
+                cs = case_set_grid(design_idx[lo:hi] - a, state_idx[lo:hi], cs_all)
+                prep_b = prepare_batch(B.dds, cs, tables_stream=compute)
+                ready = torch.cuda.Event()
+                ready.record(copy)
+            compute.wait_event(ready)
+            t2 = time.perf_counter()
+            res = B.solve(None, cs, tol=tol, want=want, prepared=prep_b)   # on the solve stream
+            if timings is not None:
+                timings.append((t1 - t0, t2 - t1, time.perf_counter() - t2, B.host_seconds, B.upload_seconds, tw))
+            parts.append(res)
+            keep.append((B, cs, prep_b, res))
     out = {k: torch.cat([r[k] for r in parts], 0) for k in parts[0]}
     # The blocks' tables were allocated on the upload stream and are read by kernels on the
     # solve stream.  The caching allocator hands a freed block back to work on the stream that
@@ -340,6 +354,39 @@ def _copy_stream(dev):
     if key not in _COPY_STREAMS:
         _COPY_STREAMS[key] = torch.cuda.Stream(dev)
     return _COPY_STREAMS[key]
+
+
+def prepare_native(designs, statics=None, r6=None, pool=None, specs=None, threads=None, pinned=False):
+    """rh_prep_designs over every design (raft/native_prep.py): the host part of
+    DesignBatch(native=True), callable on its own (a worker thread: the native call releases
+    the GIL).  Returns the PreparedDesigns with the shared grid (w, k, depth) attached.
+    pinned: its tables in page-locked memory (PreparedDesigns), uploaded asynchronously."""
+    import os
+    from .hydro_math import wave_numbers
+    from .native_prep import PreparedDesigns
+    if isinstance(statics, dict) or statics is None:
+        statics = [statics] * len(designs)
+    w = Model.frequency_grid(designs[0])
+    depth = get_from_dict(designs[0]["site"], "water_depth", dtype=float)
+    for d in designs[1:]:
+        if d is designs[0]:
+            continue
+        if get_from_dict(d["site"], "water_depth", dtype=float) != depth or \
+                not np.array_equal(Model.frequency_grid(d), w):
+            raise ValueError("all designs of a batch must share the frequency grid and the site")
+    k = wave_numbers(w, depth)
+    if specs is None:
+        jobs = [(d, None if r6 is None else np.asarray(r6, dtype=float), st) for d, st in zip(designs, statics)]
+        if pool is not None and len(jobs) > 1:
+            specs = pool.map(_spec_job, jobs, chunksize=max(1, len(jobs) // (4 * pool._processes)))
+        else:
+            specs = [_spec_job(j) for j in jobs]
+    elif len(specs) != len(designs):
+        raise ValueError("DesignBatch: one spec record per design")
+    nt = threads or (pool._processes if pool is not None else min(16, len(os.sched_getaffinity(0))))
+    P = PreparedDesigns(specs, w, k, nthreads=nt, pinned=pinned)
+    P.w, P.k, P.depth = w, k, depth
+    return P
 
 
 def prepare_design(job):

@@ -302,9 +302,13 @@ class PreparedDesigns:
     """Host tables of many designs from one rh_prep_designs call: `packed` (every design's
     real-valued tables back to back, the layout of raft/prep.py host_tables), `mstart`,
     and per design (offset, length, mstart offset, nn, nm) in `info`; `statics` [nd, 5, 6, 6]
-    = M_struc, B_struc, C_struc, C_hydro, A_hydro_morison."""
+    = M_struc, B_struc, C_struc, C_hydro, A_hydro_morison.
+    pinned: write `packed` and `mstart` into one page-locked host tensor (`pinned`, packed
+    then mstart as int32 bytes) so that they go up in one asynchronous copy
+    (raft/batch.py DesignBatch._upload); torch's pinned-memory cache recycles it only after
+    that copy has run."""
 
-    def __init__(self, specs, w, k, nthreads=0):
+    def __init__(self, specs, w, k, nthreads=0, pinned=False):
         L = N.lib()
         nd = len(specs)
         off = np.zeros(nd + 1, dtype=np.int64)
@@ -318,8 +322,17 @@ class PreparedDesigns:
         try:
             info = np.zeros(5 * nd + 2, dtype=np.int64)
             N.check(L.rh_prep_layout(h, info.ctypes.data), "rh_prep_layout")
-            self.packed = np.empty(int(info[5 * nd]), dtype=float)
-            self.mstart = np.empty(int(info[5 * nd + 1]), dtype=np.int32)
+            npk, nms = int(info[5 * nd]), int(info[5 * nd + 1])
+            self.pinned = None
+            if pinned:
+                import torch
+                self.pinned = torch.empty(npk + (nms + 1) // 2, dtype=torch.float64, pin_memory=True)
+                buf = self.pinned.numpy()
+                self.packed = buf[:npk]
+                self.mstart = buf[npk:].view(np.int32)[:nms]
+            else:
+                self.packed = np.empty(npk, dtype=float)
+                self.mstart = np.empty(nms, dtype=np.int32)
             self.statics = np.empty([nd, 5, 6, 6], dtype=float)
             N.check(L.rh_prep_copy(h, self.packed.ctypes.data, self.mstart.ctypes.data, self.statics.ctypes.data),
                     "rh_prep_copy")
@@ -335,6 +348,7 @@ class PreparedDesigns:
         finally:
             L.rh_prep_free(h)
         self.info = info[:5 * nd].reshape(nd, 5)
+        self.nd = nd
         self.nw = len(w)
         self._layouts = {}
 

@@ -7,7 +7,8 @@
 #   tests[=PATTERN]   pytest -m gpu (optionally -k PATTERN), tests.log
 #   smoke             __graft_entry__.smoke(), smoke.log
 #   bench[=ARGS]      python bench.py ARGS (commas become spaces), bench.log
-#   prof              rocprofv3 --kernel-trace --stats over the C2 + C3 + C4 bench legs, prof/
+#   prof[=ARGS]       rocprofv3 --kernel-trace --stats over the C2 + C3 + C4 bench legs (bench ARGS,
+#                     commas become spaces; default --steps 10 --warmup 2 --no-cpu-baseline --no-c5), prof/
 #   pmc[=WORKLOADS]   one rocprofv3 --pmc pass per counter group (never with tracing) over the
 #                     ubench drivers of solve,qtf,c4 (default: all three), pmc_<wl>/ and the
 #                     per-workload summary pmc_summary.json (tools/pmc_summary.py)
@@ -48,8 +49,9 @@ for step in "$@"; do
       tail -1 $OUT/bench.log | cut -c1-400;;
     prof)
       cd /tmp && export TMPDIR=/tmp
+      pargs=${arg:-"--steps,10,--warmup,2,--no-cpu-baseline,--no-c5"}
       run 300 $OUT/prof.log rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-        python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-c5
+        python3 $R/bench.py ${pargs//,/ }
       cd $R;;
     pmc)
       wls=${arg:-solve,qtf,c4}

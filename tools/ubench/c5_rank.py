@@ -78,5 +78,6 @@ if __name__ == "__main__":
           f"{dt * 1e3:.2f} ms ({n / dt:.3e} cases/s), solve only {solve * 1e3:.2f} ms ({n / solve:.3e} cases/s), "
           f"ratio {solve / dt:.2f}; host done enqueuing at {t_enq * 1e3:.2f} ms", flush=True)
     for k, t in enumerate(tm):
-        print("   block %d: DesignBatch %.2f ms (host %.2f, upload %.2f), case set + tables %.2f ms, solve enqueue %.2f ms"
-              % (k, t[0] * 1e3, t[3] * 1e3, t[4] * 1e3, t[1] * 1e3, t[2] * 1e3), flush=True)
+        print("   block %d: DesignBatch %.2f ms (waiting for the prefetched native prep %.2f, host %.2f, upload %.2f), "
+              "case set + tables %.2f ms, solve enqueue %.2f ms"
+              % (k, t[0] * 1e3, t[5] * 1e3, t[3] * 1e3, t[4] * 1e3, t[1] * 1e3, t[2] * 1e3), flush=True)

@@ -1,5 +1,8 @@
-"""Where a cold C3 QTF spends its time: host tables, uploads, device Hankel table, workspace,
-first launch.  Run on the GPU box: python tools/ubench/qtf_cold.py"""
+"""Where a QTF of a new (design, grid, heading) spends its time: the native host tables
+(raft/qtf.py native_tables), the whole QtfDevice construction (tables, one pinned upload,
+device Hankel table, workspace) and the QTF launches.  Then 50 new QTFs end to end (the
+bench's end_to_end_ms) and a cProfile of 50 QtfDevice constructions.
+Run on the GPU box: python tools/ubench/qtf_cold.py [PROFILE_OUT]"""
 import os
 import sys
 import time
@@ -21,9 +24,10 @@ def main():
     for rep in range(4):
         torch.cuda.synchronize()
         t = [time.perf_counter()]
-        tab = Q.build_tables(f, w2, k2, 0.0)
+        Q.native_tables(f, 0.0)
         t.append(time.perf_counter())
         qd = Q.QtfDevice(f, w2, k2, 0.0, 0)
+        t.append(time.perf_counter())
         torch.cuda.synchronize()
         t.append(time.perf_counter())
         q = qd.qtf(dd.w, X, M66)
@@ -33,9 +37,32 @@ def main():
         torch.cuda.synchronize()
         t.append(time.perf_counter())
         d = np.diff(t) * 1e3
-        print(f"rep {rep}: build_tables {d[0]:.3f} ms, QtfDevice {d[1]:.3f} ms, first qtf {d[2]:.3f} ms, "
-              f"warm qtf {d[3]:.3f} ms", flush=True)
-    del tab, q
+        print(f"rep {rep}: native_tables {d[0]:.3f} ms, QtfDevice {d[1]:.3f} ms (+ sync {d[2]:.3f}), first qtf "
+              f"{d[3]:.3f} ms, warm qtf {d[4]:.3f} ms", flush=True)
+    e2e, ctor = [], []
+    for rep in range(50):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        qd = Q.QtfDevice(f, w2, k2, 0.0, 0)
+        t1 = time.perf_counter()
+        q = qd.qtf(dd.w, X, M66)
+        torch.cuda.synchronize()
+        e2e.append(time.perf_counter() - t0)
+        ctor.append(t1 - t0)
+    print("50 new QTFs: end to end median %.3f ms (min %.3f), QtfDevice median %.3f ms (min %.3f)"
+          % (np.median(e2e) * 1e3, np.min(e2e) * 1e3, np.median(ctor) * 1e3, np.min(ctor) * 1e3), flush=True)
+    if len(sys.argv) > 1:
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for rep in range(50):
+            qd = Q.QtfDevice(f, w2, k2, 0.0, 0)
+        pr.disable()
+        torch.cuda.synchronize()
+        with open(sys.argv[1], "w") as fh:
+            pstats.Stats(pr, stream=fh).sort_stats("tottime").print_stats(30)
+    del q
 
 
 if __name__ == "__main__":
