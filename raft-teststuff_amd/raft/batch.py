@@ -146,7 +146,7 @@ class DesignBatch:
         design x sea-state product without one case dict per case."""
         return case_set_grid(design_idx, state_idx, case_set_of(np.zeros(len(sea_states), dtype=np.int32), sea_states))
 
-    def solve(self, design_idx, cases, tol=0.01, want=("psd", "std", "zeta", "B_drag"), prepared=None):
+    def solve(self, design_idx, cases, tol=0.01, want=("psd", "std", "zeta", "B_drag"), prepared=None, out=None):
         """Drag fixed point + response of every case in one device call.  Returns the
         BatchResult (device tensors, stream-ordered): Xi [n,6,nw], iters, status, ...
         Case dicts with wind on an operating rotor (wind_speed > 0, turbine_status
@@ -154,10 +154,11 @@ class DesignBatch:
         bin, as runRAFT gives each case of a parametersweep design (raft/parametersweep.py:91,
         raft/raft_model.py:887-889): one CaseMB view per (design, distinct wind state) on the
         design's shared node and wave tables.  Such cases need the full design models
-        (native=False, light=False): the rotors are built there."""
+        (native=False, light=False): the rotors are built there.  out: preallocated outputs of
+        a CaseSet batch (solver.solve_batch)."""
         if isinstance(cases, CaseSet):
             return solve_batch_2nd(self.dds, self.fowts, cases, self.nIter, self.XiStart, tol, want=want,
-                                   prepared=prepared)
+                                   prepared=prepared, out=out)
         cs = self.case_set(design_idx, cases)
         aero = self._aero_views(np.asarray(design_idx, dtype=np.int64), cases)
         if aero is None:
@@ -245,8 +246,8 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
     design-major order of sweep_cases) and its sea state (index into `sea_states`).  Every
     case is solved exactly as in one DesignBatch call (per-case arithmetic, so the results are
     the same bits).  The uploads of a block go through a copy stream, so the host never
-    waits behind a running solve; its sweep tables and its solve run on the current stream
-    after an event on the uploads.  Returns (result dict of device tensors in case
+    waits behind a running solve, and so do its sweep tables (they run beside the previous
+    block's solve); its solve runs on the current stream after an event on both.  Returns (result dict of device tensors in case
     order, stream-ordered on the current stream; the per-block DesignBatches, kept alive
     with their tensors until the caller synchronises).  specs: optional spec records of the
     designs (native_prep.sweep_specs), or a function (a, b) -> the records of designs [a, b),
@@ -293,6 +294,16 @@ def _solve_sweep(designs, statics, design_idx, state_idx, sea_states, device, po
         st = statics if isinstance(statics, dict) or statics is None else statics[a:b]
         return prepare_native(designs[a:b], st, None, pool, sp, threads, pinned=True)
 
+    # the sweep's outputs, allocated once: each block's solve writes its rows (no concatenation)
+    nw = len(Model.frequency_grid(designs[0]))
+    n = len(design_idx)
+    c128 = dict(dtype=torch.complex128, device=dev)
+    f64 = dict(dtype=torch.float64, device=dev)
+    shapes = {"Xi": ([n, 6, nw], c128), "iters": ([n], dict(dtype=torch.int32, device=dev)),
+              "status": ([n], dict(dtype=torch.int32, device=dev)), "zeta": ([n, nw], f64), "B_drag": ([n, 6, 6], f64),
+              "psd": ([n, 6, nw], f64), "std": ([n, 6], f64), "rao": ([n, 6, nw], c128), "margin": ([n], f64)}
+    full = {k: torch.empty(sh, **kw) for k, (sh, kw) in shapes.items()
+            if k in ("iters", "status") or k in want or (k == "Xi" and "noXi" not in want)}
     parts, keep = [], []
     # The native preparation of block k+1 runs on a worker thread (rh_prep_designs releases the
     # GIL) while this thread uploads block k, tabulates it and enqueues its solve.
@@ -309,17 +320,19 @@ def _solve_sweep(designs, statics, design_idx, state_idx, sea_states, device, po
                                 else statics[a:b], device=device, prepared=P)
                 t1 = time.perf_counter()
                 cs = case_set_grid(design_idx[lo:hi] - a, state_idx[lo:hi], cs_all)
-                prep_b = prepare_batch(B.dds, cs, tables_stream=compute)
+                prep_b = prepare_batch(B.dds, cs)    # the block's wave tables on the upload stream too:
+                # they run beside the previous block's solve (its last cases leave CUs idle)
                 ready = torch.cuda.Event()
                 ready.record(copy)
             compute.wait_event(ready)
             t2 = time.perf_counter()
-            res = B.solve(None, cs, tol=tol, want=want, prepared=prep_b)   # on the solve stream
+            res = B.solve(None, cs, tol=tol, want=want, prepared=prep_b,   # on the solve stream
+                          out={k: v[lo:hi] for k, v in full.items()})
             if timings is not None:
                 timings.append((t1 - t0, t2 - t1, time.perf_counter() - t2, B.host_seconds, B.upload_seconds, tw))
             parts.append(res)
             keep.append((B, cs, prep_b, res))
-    out = {k: torch.cat([r[k] for r in parts], 0) for k in parts[0]}
+    out = {k: full[k] if k in full else torch.cat([r[k] for r in parts], 0) for k in parts[0]}
     # The blocks' tables were allocated on the upload stream and are read by kernels on the
     # solve stream.  The caching allocator hands a freed block back to work on the stream that
     # allocated it, so order every later upload-stream operation after this sweep's kernels:

@@ -84,7 +84,7 @@ def file_qtf_forces(dd, fowt, betas, S):
     return force_batch(dd, qdev, [qt for _, qt in ops], [where[float(b)] for b in betas], S)
 
 
-def solve_batch_2nd(views, owners, cs, nIter, XiStart, tol, want, prepared=None, F_wave=None):
+def solve_batch_2nd(views, owners, cs, nIter, XiStart, tol, want, prepared=None, F_wave=None, out=None):
     """solve_batch with the second-order loads of every case whose FOWT sets potSecOrder.
     views: DeviceDesign (or CaseMB) list; owners[v]: the FOWT whose potSecOrder, QTF and
     M_struc view v uses (None: first order only).  Adds to the result:
@@ -93,16 +93,19 @@ def solve_batch_2nd(views, owners, cs, nIter, XiStart, tol, want, prepared=None,
       f2nd_mean  [n, 6]   mean drift of sea state 0 (Fhydro_2nd_mean[0])
       Fhydro_2nd [n, 6, nw] the force itself, when "Fhydro_2nd" is in want
     and iters / status / every output of the final pass.  Cases of first-order FOWTs are
-    solved exactly as solve_batch solves them."""
+    solved exactly as solve_batch solves them (out: solve_batch's preallocated outputs, first-order
+    batches only)."""
     torch = views[0].torch
     dev = views[0].device
     n, nw = cs.n, views[0].nw
     vorder = np.array([order_of(o) for o in owners], dtype=np.int64)
     if not np.any(vorder > 0):
-        return solve_batch(views, cs, nIter, XiStart, tol, want=want, prepared=prepared, F_wave=F_wave)
+        return solve_batch(views, cs, nIter, XiStart, tol, want=want, prepared=prepared, F_wave=F_wave, out=out)
     order = vorder[cs.design_idx]
     if not np.any(order > 0):
-        return solve_batch(views, cs, nIter, XiStart, tol, want=want, prepared=prepared, F_wave=F_wave)
+        return solve_batch(views, cs, nIter, XiStart, tol, want=want, prepared=prepared, F_wave=F_wave, out=out)
+    if out is not None:
+        raise ValueError("solve_batch_2nd: preallocated outputs (out=) are for first-order batches")
     if F_wave is not None and np.any(order == 1):
         raise NotImplementedError("potSecOrder=1 in a coupled array: the reference adds the force to F_lin[i1:i2] "
                                   "of the whole system (raft/raft_model.py:988, SURVEY.md Q5)")

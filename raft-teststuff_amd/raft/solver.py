@@ -50,7 +50,7 @@ class BatchResult(dict):
 
 
 def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std", "zeta", "B_drag"),
-                fext=None, stream=None, prepared=None, Xi_init=None, first_iter=0, F_wave=None):
+                fext=None, stream=None, prepared=None, Xi_init=None, first_iter=0, F_wave=None, out=None):
     """Run rh_solve_cases.  `designs`: list of DeviceDesign (same nw); `cases`: CaseSet.
     Returns a BatchResult of device tensors (stream-ordered; caller synchronises).
     want may include "Xi_prev" (the un-relaxed XiLast of the final iteration), "margin"
@@ -59,7 +59,9 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     Model.analyzeArrayBatch; then no psd / std / rao either); Xi_init /
     first_iter restart a fixed point from such a state (potSecOrder=1 second pass).  F_wave: a
     contiguous complex128 [ncase, 6, nw] tensor that receives each case's wave excitation with
-    its final linearisation (rh_solve_out.F_wave; the F of an array solve, Model.analyzeArrayBatch)."""
+    its final linearisation (rh_solve_out.F_wave; the F of an array solve, Model.analyzeArrayBatch).
+    out: optional dict of preallocated contiguous output tensors (e.g. slices of a whole sweep's
+    outputs, raft/batch.py solve_sweep) used instead of fresh ones for the keys it holds."""
     d0 = designs[0]
     torch = d0.torch
     dev = d0.device
@@ -69,33 +71,32 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
             raise ValueError("all designs in a batch must share the frequency grid")
     prep = prepared if prepared is not None else prepare_batch(designs, cases)
     ncase = cases.n
+    given = out or {}
     out = BatchResult()
     c128 = dict(dtype=torch.complex128, device=dev)
     f64 = dict(dtype=torch.float64, device=dev)
+    i32 = dict(dtype=torch.int32, device=dev)
+
+    def put(key, shape, kw):
+        t = given.get(key)
+        if t is None:
+            t = torch.empty(shape, **kw)
+        elif list(t.shape) != shape or t.dtype != kw["dtype"] or not t.is_contiguous():
+            raise ValueError(f"out[{key!r}]: expected a contiguous {kw['dtype']} tensor of shape {shape}")
+        out[key] = t
+
     if "noXi" not in want or nw > N.lib().rh_solve_noxi_max_bins():   # "noXi": the linearisation only (zeta / Bmat / B_drag);
-        out["Xi"] = torch.empty([ncase, 6, nw], **c128)   # the two-pass grids store it regardless
+        put("Xi", [ncase, 6, nw], c128)                                # the two-pass grids store it regardless
     xl = torch.empty([ncase, 6, nw], **c128)
-    out["iters"] = torch.empty([ncase], dtype=torch.int32, device=dev)
-    out["status"] = torch.empty([ncase], dtype=torch.int32, device=dev)
+    put("iters", [ncase], i32)
+    put("status", [ncase], i32)
     nnmax = max(d.nn for d in designs)
-    if "zeta" in want:
-        out["zeta"] = torch.empty([ncase, nw], **f64)
-    if "B_drag" in want:
-        out["B_drag"] = torch.empty([ncase, 6, 6], **f64)
-    if "Bmat" in want:
-        out["Bmat"] = torch.empty([ncase, nnmax, 3, 3], **f64)
-    if "psd" in want:
-        out["psd"] = torch.empty([ncase, 6, nw], **f64)
-    if "std" in want:
-        out["std"] = torch.empty([ncase, 6], **f64)
-    if "rao" in want:
-        out["rao"] = torch.empty([ncase, 6, nw], **c128)
-    if "Z" in want:
-        out["Z"] = torch.empty([ncase, nw, 6, 6], **c128)
-    if "Xi_prev" in want:
-        out["Xi_prev"] = torch.empty([ncase, 6, nw], **c128)
-    if "margin" in want:
-        out["margin"] = torch.empty([ncase], **f64)
+    for key, shape, kw in (("zeta", [ncase, nw], f64), ("B_drag", [ncase, 6, 6], f64),
+                           ("Bmat", [ncase, nnmax, 3, 3], f64), ("psd", [ncase, 6, nw], f64), ("std", [ncase, 6], f64),
+                           ("rao", [ncase, 6, nw], c128), ("Z", [ncase, nw, 6, 6], c128),
+                           ("Xi_prev", [ncase, 6, nw], c128), ("margin", [ncase], f64)):
+        if key in want:
+            put(key, shape, kw)
     for t, shape in ((fext, [ncase, 6, nw]), (Xi_init, [ncase, 6, nw]), (F_wave, [ncase, 6, nw])):
         if t is not None and (list(t.shape) != shape or t.dtype != torch.complex128 or not t.is_contiguous()):
             raise ValueError(f"expected a contiguous complex128 tensor of shape {shape}")
