@@ -246,8 +246,8 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
     design-major order of sweep_cases) and its sea state (index into `sea_states`).  Every
     case is solved exactly as in one DesignBatch call (per-case arithmetic, so the results are
     the same bits).  The uploads of a block go through a copy stream, so the host never
-    waits behind a running solve, and so do its sweep tables (they run beside the previous
-    block's solve); its solve runs on the current stream after an event on both.  Returns (result dict of device tensors in case
+    waits behind a running solve; its sweep tables and its solve run on the current stream
+    after an event on the uploads.  Returns (result dict of device tensors in case
     order, stream-ordered on the current stream; the per-block DesignBatches, kept alive
     with their tensors until the caller synchronises).  specs: optional spec records of the
     designs (native_prep.sweep_specs), or a function (a, b) -> the records of designs [a, b),
@@ -320,8 +320,9 @@ def _solve_sweep(designs, statics, design_idx, state_idx, sea_states, device, po
                                 else statics[a:b], device=device, prepared=P)
                 t1 = time.perf_counter()
                 cs = case_set_grid(design_idx[lo:hi] - a, state_idx[lo:hi], cs_all)
-                prep_b = prepare_batch(B.dds, cs)    # the block's wave tables on the upload stream too:
-                # they run beside the previous block's solve (its last cases leave CUs idle)
+                # the block's wave tables on the solve stream: beside the previous block's solve (on the
+                # upload stream) they stretched each solve by 0.5 ms (profiles/r06_v3/c5_timeline.txt)
+                prep_b = prepare_batch(B.dds, cs, tables_stream=compute)
                 ready = torch.cuda.Event()
                 ready.record(copy)
             compute.wait_event(ready)
