@@ -715,6 +715,7 @@ inline void prep_one(const double* spec, long long len, int nw, const double* w,
       for (int e = 0; e < 36; ++e) gm[b].a[e / 6][e % 6] = rd.get();
   }
   std::vector<Member> mems;
+  mems.reserve((size_t)nmemb * 4);   // (a Member is some thirty vectors: growing the array moves them all)
   for (int im = 0; im < nmemb; ++im) {
     Member b;
     b.type = (int)rd.get();
@@ -897,7 +898,7 @@ inline void prep_one(const double* spec, long long len, int nw, const double* w,
 
   // tables (raft/prep.py node_table / linear_matrices / host_tables)
   constexpr int NF = RH_NF_COUNT, MF = RH_MF_COUNT;
-  std::vector<std::vector<double>> cols;
+  std::vector<double> cols;               // node rows of NF fields, back to back
   std::vector<std::vector<double>> mcols;
   std::vector<const double*> mcf_blocks;   // per node: its [9][nw] complex block, or NULL
   out.mstart = {0};
@@ -929,18 +930,19 @@ inline void prep_one(const double* spec, long long len, int nw, const double* w,
       }
       const V3& r = m.r[il];
       const V3 rr = sub(r, rP);
-      std::vector<double> c = {r[0], r[1], r[2], rr[0], rr[1], rr[2], m.q[0], m.q[1], m.q[2], m.p1[0], m.p1[1],
-                               m.p1[2], m.p2[0], m.p2[1], m.p2[2], aq, ap1, ap2, aend, m.coef(m.cdq, il),
-                               m.coef(m.cdp1, il), m.coef(m.cdp2, il), m.coef(m.cdend, il), m.circ ? 1.0 : 0.0,
-                               m.a_i[il], m.mcf ? 1.0 : 0.0};
+      const double c[] = {r[0], r[1], r[2], rr[0], rr[1], rr[2], m.q[0], m.q[1], m.q[2], m.p1[0], m.p1[1],
+                          m.p1[2], m.p2[0], m.p2[1], m.p2[2], aq, ap1, ap2, aend, m.coef(m.cdq, il),
+                          m.coef(m.cdp1, il), m.coef(m.cdp2, il), m.coef(m.cdend, il), m.circ ? 1.0 : 0.0,
+                          m.a_i[il], m.mcf ? 1.0 : 0.0};
+      static_assert(sizeof(c) / sizeof(double) + 10 == NF, "node table fields");
       mcf_blocks.push_back(m.mcf ? m.imat_mcf.data() + (size_t)il * 9 * nw * 2 : nullptr);
+      cols.insert(cols.end(), c, c + sizeof(c) / sizeof(double));
       for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) c.push_back(m.Imat[il].a[i][j]);
-      c.push_back(m.ls[il]);
-      cols.push_back(std::move(c));
+        for (int j = 0; j < 3; ++j) cols.push_back(m.Imat[il].a[i][j]);
+      cols.push_back(m.ls[il]);
     }
   }
-  const int nn = (int)cols.size(), nm = (int)mcols.size();
+  const int nn = (int)(cols.size() / NF), nm = (int)mcols.size();
   const int nnc = nn ? nn : 1, nmc = nm ? nm : 1;
   out.nn = nn;
   out.nm = nm;
@@ -957,7 +959,7 @@ inline void prep_one(const double* spec, long long len, int nw, const double* w,
   std::copy(k, k + nw, P + nw);
   double* T = P + 2 * nw;
   for (int n = 0; n < nn; ++n)
-    for (int f = 0; f < NF; ++f) T[(size_t)f * nnc + n] = cols[n][f];
+    for (int f = 0; f < NF; ++f) T[(size_t)f * nnc + n] = cols[(size_t)n * NF + f];
   double* Mt = T + (size_t)NF * nnc;
   for (int j = 0; j < nm; ++j)
     for (int f = 0; f < MF; ++f) Mt[(size_t)f * nmc + j] = mcols[j][f];
