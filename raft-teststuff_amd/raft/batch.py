@@ -237,7 +237,7 @@ def case_set_grid(design_idx, state_idx, cs0):
 
 def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, pool=None, chunks=4, tol=0.01,
                 want=("psd", "std"), timings=None, specs=None, threads=None, first=1.0,
-                last=1.0):
+                last=1.0, block_path=True):
     """A design sweep solved in `chunks` design blocks, pipelined: while the device solves
     block k, the host prepares block k+1 (native preparation, raft/native_prep.py), so the
     host work hides behind the solve instead of preceding it.
@@ -256,6 +256,8 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
     while the first is prepared, and only the last block's solve runs after the host is done,
     so small ones shorten the pipeline's fill and drain; 1 = equal blocks, the default: on the
     C5 bench 0.25 / 0.5 measured within noise of it, 26.0-27.3 vs 25.5-27.5 ms).
+    block_path: write each block's descriptors in one array (raft/sweep_block.py) instead of a
+    DesignBatch of per-design objects (the same launches and bits; False: the per-design path).
     timings: optional list that receives,
     per block, the host seconds of (design preparation, case set + tables + uploads, solve
     enqueue, DesignBatch host part, DesignBatch upload part)."""
@@ -264,16 +266,17 @@ def solve_sweep(designs, statics, design_idx, state_idx, sea_states, device=0, p
     gc.disable()     # a full collection inside the pipeline stalled the host for 50-65 ms (profiles/r06_v1)
     try:
         return _solve_sweep(designs, statics, design_idx, state_idx, sea_states, device, pool, chunks, tol, want,
-                            timings, specs, threads, first, last)
+                            timings, specs, threads, first, last, block_path)
     finally:
         if was:
             gc.enable()
 
 
 def _solve_sweep(designs, statics, design_idx, state_idx, sea_states, device, pool, chunks, tol, want, timings,
-                 specs, threads, first, last):
+                 specs, threads, first, last, block_path=True):
     import torch
     from .solver import prepare_batch
+    from .sweep_block import prepare_block
     design_idx = np.asarray(design_idx, dtype=np.int64)
     state_idx = np.asarray(state_idx, dtype=np.int64)
     if any(get_from_dict(c, "wind_speed", shape=0, default=0.0) > 0 for c in sea_states):
@@ -316,13 +319,18 @@ def _solve_sweep(designs, statics, design_idx, state_idx, sea_states, device, po
             tw = time.perf_counter() - t0
             nxt = ex.submit(prep, *blocks[j + 1]) if j + 1 < len(blocks) else None
             with torch.cuda.stream(copy):
-                B = DesignBatch(designs[a:b], statics=statics if isinstance(statics, dict) or statics is None
-                                else statics[a:b], device=device, prepared=P)
-                t1 = time.perf_counter()
                 cs = case_set_grid(design_idx[lo:hi] - a, state_idx[lo:hi], cs_all)
                 # the block's wave tables on the solve stream: beside the previous block's solve (on the
                 # upload stream) they stretched each solve by 0.5 ms (profiles/r06_v3/c5_timeline.txt)
-                prep_b = prepare_batch(B.dds, cs, tables_stream=compute)
+                fast = prepare_block(P, designs[a:b], cs, device, compute) if block_path else None
+                if fast is not None:     # one descriptor array for the block (sweep_block.py)
+                    B, prep_b = fast
+                    t1 = time.perf_counter()
+                else:
+                    B = DesignBatch(designs[a:b], statics=statics if isinstance(statics, dict) or statics is None
+                                    else statics[a:b], device=device, prepared=P)
+                    t1 = time.perf_counter()
+                    prep_b = prepare_batch(B.dds, cs, tables_stream=compute)
                 ready = torch.cuda.Event()
                 ready.record(copy)
             compute.wait_event(ready)
@@ -330,7 +338,8 @@ def _solve_sweep(designs, statics, design_idx, state_idx, sea_states, device, po
             res = B.solve(None, cs, tol=tol, want=want, prepared=prep_b,   # on the solve stream
                           out={k: v[lo:hi] for k, v in full.items()})
             if timings is not None:
-                timings.append((t1 - t0, t2 - t1, time.perf_counter() - t2, B.host_seconds, B.upload_seconds, tw))
+                timings.append((t1 - t0, t2 - t1, time.perf_counter() - t2, getattr(B, "host_seconds", 0.0),
+                                getattr(B, "upload_seconds", 0.0), tw))
             parts.append(res)
             keep.append((B, cs, prep_b, res))
     out = {k: full[k] if k in full else torch.cat([r[k] for r in parts], 0) for k in parts[0]}

@@ -298,24 +298,10 @@ def tabulate_batch(designs, design_idx, betas, launch_stream=None):
     index of every case in its design's tables.  Tables of all designs share three device
     allocations; each DeviceDesign holds views.  launch_stream: run the launch there (after
     this stream's uploads, through an event) instead of on the current stream."""
+    from .sweep_block import table_plan
     torch = designs[0].torch
     dev = designs[0].device
-    n = len(design_idx)
-    order = np.lexsort((betas, design_idx))
-    ds, bs = design_idx[order], betas[order]
-    new = np.ones(n, dtype=bool)
-    new[1:] = (ds[1:] != ds[:-1]) | (bs[1:] != bs[:-1])
-    grp = np.cumsum(new) - 1                       # unique (design, heading) pair per sorted case
-    ud, ub = ds[new], bs[new]
-    first = np.ones(len(ud), dtype=bool)
-    first[1:] = ud[1:] != ud[:-1]
-    start = np.maximum.accumulate(np.where(first, np.arange(len(ud)), 0))
-    head = np.empty(n, dtype=np.int32)
-    head[order] = (np.arange(len(ud)) - start)[grp]
-    di = ud[first]                                 # designs involved, with their heading runs
-    bounds = np.append(np.nonzero(first)[0], len(ud))
-    nh = np.diff(bounds)
-    hstride = int(nh.max())
+    head, di, nh, hstride, bm = table_plan(design_idx, betas)
     sel = [designs[int(i)] for i in di]
     nw = sel[0].nw
     rows = [int(k) * max(d.nn, 1) * 3 * nw for d, k in zip(sel, nh)]
@@ -323,12 +309,10 @@ def tabulate_batch(designs, design_idx, betas, launch_stream=None):
     U = torch.empty([sum(rows)], **c128)
     K = torch.empty([sum(rows)], **c128)
     Fi = torch.empty([int(nh.sum()) * 6 * nw], **c128)
-    bm = np.zeros([len(sel), hstride])
     ou = of = 0
     for j, (d, k) in enumerate(zip(sel, nh)):
         k = int(k)
-        hs = ub[bounds[j]:bounds[j + 1]]
-        bm[j, :k] = hs
+        hs = bm[j, :k]
         shp = (k, max(d.nn, 1), 3, nw)
         d.set_tables({"uhat": (U, ou, shp), "kproj": (K, ou, shp), "finer": (Fi, of, (k, 6, nw))},
                      [float(b) for b in hs])

@@ -62,13 +62,17 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     its final linearisation (rh_solve_out.F_wave; the F of an array solve, Model.analyzeArrayBatch).
     out: optional dict of preallocated contiguous output tensors (e.g. slices of a whole sweep's
     outputs, raft/batch.py solve_sweep) used instead of fresh ones for the keys it holds."""
-    d0 = designs[0]
-    torch = d0.torch
-    dev = d0.device
-    nw = d0.nw
-    for d in designs:
-        if d.nw != nw:
-            raise ValueError("all designs in a batch must share the frequency grid")
+    from .sweep_block import BlockDesigns
+    if isinstance(designs, BlockDesigns):     # a sweep block: its descriptors already written (sweep_block.py)
+        if prepared is None:
+            raise ValueError("solve_batch: a BlockDesigns batch comes with its prepared case columns")
+        torch, dev, nw, dev_index = designs.torch, designs.device, designs.nw, designs.dev_index
+    else:
+        d0 = designs[0]
+        torch, dev, nw, dev_index = d0.torch, d0.device, d0.nw, d0.dev_index
+        for d in designs:
+            if d.nw != nw:
+                raise ValueError("all designs in a batch must share the frequency grid")
     prep = prepared if prepared is not None else prepare_batch(designs, cases)
     ncase = cases.n
     given = out or {}
@@ -90,7 +94,7 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     xl = torch.empty([ncase, 6, nw], **c128)
     put("iters", [ncase], i32)
     put("status", [ncase], i32)
-    nnmax = max(d.nn for d in designs)
+    nnmax = designs.nnmax if isinstance(designs, BlockDesigns) else max(d.nn for d in designs)
     for key, shape, kw in (("zeta", [ncase, nw], f64), ("B_drag", [ncase, 6, 6], f64),
                            ("Bmat", [ncase, nnmax, 3, 3], f64), ("psd", [ncase, 6, nw], f64), ("std", [ncase, 6], f64),
                            ("rao", [ncase, 6, nw], c128), ("Z", [ncase, nw, 6, 6], c128),
@@ -114,9 +118,9 @@ def solve_batch(designs, cases, nIter, XiStart=0.0, tol=0.01, want=("psd", "std"
     for k in ["zeta", "B_drag", "Bmat", "psd", "std", "rao", "Z", "Xi_prev", "margin"]:
         setattr(o, k, N.ptr(out.get(k)))
     o.F_wave = N.ptr(F_wave)
-    arr = (N.RhDesign * len(designs))(*[d.struct() for d in designs])
+    arr = designs.arr if isinstance(designs, BlockDesigns) else (N.RhDesign * len(designs))(*[d.struct() for d in designs])
     s = stream if stream is not None else N.stream_handle(torch, dev)
-    N.check(N.lib().rh_solve_cases(N.context(d0.dev_index), arr, len(designs), ctypes.byref(cs), ctypes.byref(o), s),
+    N.check(N.lib().rh_solve_cases(N.context(dev_index), arr, len(designs), ctypes.byref(cs), ctypes.byref(o), s),
             "rh_solve_cases")
     out._keep = (xl, prep, arr, fext, Xi_init, F_wave)
     return out

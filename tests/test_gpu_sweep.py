@@ -273,10 +273,18 @@ def test_pipelined_sweep_equals_one_batch():
     mult = sweep_multipliers(7, seed=13)
     out2, keep2 = solve_sweep([base] * len(designs), st, idx, sidx, grid, chunks=3, want=("std", "psd"),
                               specs=lambda a, b: sweep_specs(base, mult[a:b], statics=st), threads=4)
+    # the per-design path of the blocks (DesignBatch objects) against the block descriptor arrays
+    out3, keep3 = solve_sweep([base] * len(designs), st, idx, sidx, grid, chunks=3, want=("std", "psd"),
+                              specs=lambda a, b: sweep_specs(base, mult[a:b], statics=st), threads=4,
+                              block_path=False)
+    from raft.sweep_block import BlockDesigns
+    assert all(isinstance(k[0], BlockDesigns) for k in keep2)
+    assert not any(isinstance(k[0], BlockDesigns) for k in keep3)
     torch.cuda.synchronize()
     for k in ("Xi", "iters", "status", "std", "psd"):
         assert torch.equal(out[k], ref[k]), k
         assert torch.equal(out2[k], ref[k]), k
+        assert torch.equal(out3[k], ref[k]), k
 
 
 def test_design_batch_with_operating_rotor():
