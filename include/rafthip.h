@@ -220,7 +220,10 @@ int rh_wave_tables(rh_ctx* ctx, const rh_design* d, const double* beta,
 
 /* rh_wave_tables for many designs in ONE launch: design i tabulates designs[i].nhead headings
  * beta[i * hstride + h] (rad) into the tables its descriptor points at (uhat, finer, kproj,
- * written).  The per-design part of a design sweep (C5) as a single grid. */
+ * written).  The per-design part of a design sweep (C5) as a single grid.  A design's uhat
+ * may be NULL: its velocity table is then not stored, and only rh_solve_cases (whose fixed
+ * point reads kproj and finer) accepts the design afterwards; the entry points that read uhat
+ * return RH_EINVAL for it. */
 int rh_wave_tables_batch(rh_ctx* ctx, const rh_design* designs, int ndesign, const double* beta, int hstride,
                          rh_stream stream);
 

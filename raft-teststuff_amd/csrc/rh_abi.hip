@@ -127,13 +127,15 @@ constexpr int kThreads = 256;
 constexpr int kMaxNodes = 1024;
 constexpr size_t kMaxLds = 160 * 1024;   // LDS per workgroup on gfx950
 
-int check_design(const rh_design& d, bool need_tables) {
+// need_uhat: the entry point's kernels read the velocity table (the fixed point does not: it
+// reads kproj and finer only, so a sweep block may skip uhat, rh_wave_tables_batch)
+int check_design(const rh_design& d, bool need_tables, bool need_uhat = true) {
   if (d.nw < 2 || d.nw > 2048) return fail(RH_EINVAL, "nw=%d outside [2, 2048]", d.nw);
   if (d.nn < 0 || d.nn > kMaxNodes) return fail(RH_EINVAL, "nn=%d outside [0, %d]", d.nn, kMaxNodes);
   if (!d.w || !d.k || (d.nn > 0 && !d.node)) return fail(RH_EINVAL, "design: null w/k/node table");
   if (!d.M || !d.B || !d.C) return fail(RH_EINVAL, "design: null M/B/C");
   if (d.nn > 0 && (d.nm < 1 || !d.memb || !d.mstart)) return fail(RH_EINVAL, "design: member table missing");
-  if (need_tables && (!d.uhat || !d.finer || !d.kproj || d.nhead < 1))
+  if (need_tables && ((need_uhat && !d.uhat) || !d.finer || !d.kproj || d.nhead < 1))
     return fail(RH_EINVAL, "design: wave tables missing (call rh_wave_tables first)");
   if (!(d.dw > 0)) return fail(RH_EINVAL, "design: dw must be > 0");
   return RH_OK;
@@ -370,7 +372,7 @@ int rh_wave_tables_batch(rh_ctx* ctx, const rh_design* designs, int ndesign, con
     if (int r = check_design(d, false)) return r;
     if (d.nhead < 1 || d.nhead > hstride)
       return fail(RH_EINVAL, "rh_wave_tables_batch: design %d: nhead=%d outside [1, hstride=%d]", i, d.nhead, hstride);
-    if (!d.uhat || !d.finer || !d.kproj) return fail(RH_EINVAL, "rh_wave_tables_batch: design %d: null table", i);
+    if (!d.finer || !d.kproj) return fail(RH_EINVAL, "rh_wave_tables_batch: design %d: null table", i);
     nwmax = d.nw > nwmax ? d.nw : nwmax;
     nhmax = d.nhead > nhmax ? d.nhead : nhmax;
   }
@@ -402,7 +404,7 @@ int rh_solve_cases(rh_ctx* ctx, const rh_design* designs, int ndesign, const rh_
   const int nw = designs[0].nw;
   int nnmax = 0;
   for (int i = 0; i < ndesign; ++i) {
-    if (int r = check_design(designs[i], true)) return r;
+    if (int r = check_design(designs[i], true, false)) return r;
     if (designs[i].nw != nw) return fail(RH_EINVAL, "rh_solve_cases: all designs must share nw");
     if (designs[i].nn > nnmax) nnmax = designs[i].nn;
   }

@@ -73,7 +73,7 @@ __device__ __forceinline__ void wave_node(const rh_design& d, int h, int n, int 
   const cd u1 = scl(scl(we, c_sh), sb);
   const cd u2 = scl(iw(w, e), s_sh);
   rh_c128* U = uhat + ((size_t)(h * nn + n) * 3) * nw + b;
-  if (okb) {
+  if (okb && uhat) {                        // (uhat NULL: a sweep block's fixed point needs kproj only)
     st(U, u0);
     st(U + nw, u1);
     st(U + 2 * nw, u2);

@@ -2,7 +2,8 @@
 design: the block's natively prepared tables (native_prep.PreparedDesigns, pinned) go up in
 one copy, the rh_design descriptors of all its designs are written column-wise into one
 record array from the preparation's layout, the wave tables of every (design, heading) pair
-come from one rh_wave_tables_batch launch, and the solve takes the same array.  The
+come from one rh_wave_tables_batch launch (kproj and finer only: the fixed point reads no
+velocity table), and the solve takes the same array.  The
 descriptors, tables and launches are the ones DesignBatch + prepare_batch + solve_batch make
 for the same block (the same bits: tests/test_gpu_sweep.py); the host cost per block no
 longer grows with a per-design object, which is what paced the first block of a sweep and a
@@ -109,15 +110,15 @@ def prepare_block(P, designs, cases, device, compute):
     rg = np.array([sites[id(d["site"])] for d in designs])
     rec["rho"], rec["g"] = rg[:, 0], rg[:, 1]
     rec["pdyn_rho_g"] = 1025.0 * 9.81                      # getWaveKin defaults (prep.DeviceDesign._make_struct)
-    # the block's wave tables: three allocations, each design's slices back to back
+    # the block's wave tables: kproj and finer, each design's slices back to back; no velocity
+    # table uhat (NULL): the fixed point reads only these two, and the sweep solves nothing else
     rows = nh * nnc * 3 * nw
     c128 = dict(dtype=torch.complex128, device=dev)
-    U = torch.empty([int(rows.sum())], **c128)
     K = torch.empty([int(rows.sum())], **c128)
     Fi = torch.empty([int(nh.sum()) * 6 * nw], **c128)
     ou = np.concatenate([[0], np.cumsum(rows)[:-1]])
     of = np.concatenate([[0], np.cumsum(nh * 6 * nw)[:-1]])
-    rec["uhat"] = U.data_ptr() + 16 * ou
+    rec["uhat"] = 0
     rec["kproj"] = K.data_ptr() + 16 * ou
     rec["finer"] = Fi.data_ptr() + 16 * of
     arr = (N.RhDesign * nd).from_buffer(rec)
@@ -138,5 +139,5 @@ def prepare_block(P, designs, cases, device, compute):
                 head_host=head, group_start=None, ngroup=0)
     st0 = designs[0].get("settings", {})
     blk = BlockDesigns(torch, dev, device, arr, nd, nw, int(nn.max()), get_from_dict(st0, "nIter", default=15, dtype=int),
-                       get_from_dict(st0, "XiStart", default=0.1, dtype=float), (flat, U, K, Fi, beta_t, rec))
+                       get_from_dict(st0, "XiStart", default=0.1, dtype=float), (flat, K, Fi, beta_t, rec))
     return blk, prep

@@ -277,9 +277,20 @@ def test_pipelined_sweep_equals_one_batch():
     out3, keep3 = solve_sweep([base] * len(designs), st, idx, sidx, grid, chunks=3, want=("std", "psd"),
                               specs=lambda a, b: sweep_specs(base, mult[a:b], statics=st), threads=4,
                               block_path=False)
+    from raft import _native as N
     from raft.sweep_block import BlockDesigns
     assert all(isinstance(k[0], BlockDesigns) for k in keep2)
     assert not any(isinstance(k[0], BlockDesigns) for k in keep3)
+    # a block's designs carry no velocity table: the entry points that read it refuse them
+    blk = keep2[0][0]
+    one = torch.zeros(1, dtype=torch.int32, device="cuda")
+    z = torch.zeros([1, blk.nw], dtype=torch.float64, device="cuda")
+    bd = torch.zeros([1, 36], dtype=torch.float64, device="cuda")
+    bm = torch.zeros([1, blk.nnmax, 9], dtype=torch.float64, device="cuda")
+    xo = torch.empty([1, 6, blk.nw], dtype=torch.complex128, device="cuda")
+    rc = N.lib().rh_heading_response_ext(N.context(0), blk.arr, len(blk), 1, N.ptr(one), N.ptr(one), N.ptr(z),
+                                         N.ptr(bd), N.ptr(bm), 0, None, N.ptr(xo), N.stream_handle(torch))
+    assert rc == N.RH_EINVAL and b"wave tables missing" in N.lib().rh_last_error()
     torch.cuda.synchronize()
     for k in ("Xi", "iters", "status", "std", "psd"):
         assert torch.equal(out[k], ref[k]), k
