@@ -387,6 +387,7 @@ def prepare_native(designs, statics=None, r6=None, pool=None, specs=None, thread
     import os
     from .hydro_math import wave_numbers
     from .native_prep import PreparedDesigns
+    t0 = time.perf_counter()
     if isinstance(statics, dict) or statics is None:
         statics = [statics] * len(designs)
     w = Model.frequency_grid(designs[0])
@@ -409,6 +410,7 @@ def prepare_native(designs, statics=None, r6=None, pool=None, specs=None, thread
     nt = threads or (pool._processes if pool is not None else min(16, len(os.sched_getaffinity(0))))
     P = PreparedDesigns(specs, w, k, nthreads=nt, pinned=pinned)
     P.w, P.k, P.depth = w, k, depth
+    P.host_seconds = time.perf_counter() - t0
     return P
 
 

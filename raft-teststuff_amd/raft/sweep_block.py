@@ -24,6 +24,7 @@ class BlockDesigns:
         self.arr, self.n, self.nw, self.nnmax = arr, n, nw, nnmax
         self.nIter, self.XiStart = nIter, XiStart
         self._keep = keep
+        self.host_seconds = 0.0       # the block's native preparation (set by prepare_block)
 
     def __len__(self):
         return self.n
@@ -140,4 +141,5 @@ def prepare_block(P, designs, cases, device, compute):
     st0 = designs[0].get("settings", {})
     blk = BlockDesigns(torch, dev, device, arr, nd, nw, int(nn.max()), get_from_dict(st0, "nIter", default=15, dtype=int),
                        get_from_dict(st0, "XiStart", default=0.1, dtype=float), (flat, K, Fi, beta_t, rec))
+    blk.host_seconds = getattr(P, "host_seconds", 0.0)
     return blk, prep
