@@ -445,10 +445,26 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
         dist.barrier()
     dt = time.perf_counter() - t0
     assert all(torch.equal(o, q) for o in outs), "pipelined QTF differs"
-    t = torch.tensor([dt, t_e2e, t_tables, t_first, dt_serial], dtype=torch.float64, device=f"cuda:{device}")
+    # New RAOs on one design (the second passes of potSecOrder = 1 cases, raft/second_order.py):
+    # each QTF is a full QTF of its own RAO (two RAOs alternate), the incident-wave parts -- Kim &
+    # Yue tables and tile sums, node GEMM basis -- kept in the workspace from the first
+    # (rh_qtf_slender_ext RH_QTF_INCIDENT_CACHED; the same bits as a full call: GPU test).  One QTF
+    # at a time on one GPU, as `value`.
+    Xb = (X * 0.9).contiguous()
+    qc = QtfDevice(f, w2, k2, 0.0, device)
+    qc.qtf(dd.w, X, M66, out=outs[0])
+    for i in range(warmup):
+        qc.qtf(dd.w, Xb if i % 2 else X, M66, out=outs[0], incident_cached=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        qc.qtf(dd.w, Xb if i % 2 else X, M66, out=outs[0], incident_cached=True)
+    torch.cuda.synchronize()
+    dt_cached = time.perf_counter() - t0
+    t = torch.tensor([dt, t_e2e, t_tables, t_first, dt_serial, dt_cached], dtype=torch.float64, device=f"cuda:{device}")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt_max, e2e_max, tab_max, first_max, ser_max = (float(x) for x in t.cpu())
+    dt_max, e2e_max, tab_max, first_max, ser_max, cached_max = (float(x) for x in t.cpu())
     ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     fpp = qtf_flops_per_pair(qd.nq, nkay, nwl)
     from raft.parallel import qtf_pairs_of
@@ -465,6 +481,11 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
                        "pipeline": f"each GPU's independent QTFs rotate over {nqs} HIP streams with their own tables "
                                    "and workspace (no exchange)",
                        "full_grid_equiv_per_s": world * n2 * n2 * steps / dt_max},
+           "same_design_new_rao": {"value": npair * steps / cached_max, "unit": "pairs/s",
+                                   "ms_per_qtf": cached_max / steps * 1e3, "scaling": "per GPU",
+                                   "note": "each QTF of a new RAO (two alternate) on one design, grid and "
+                                           "heading, its incident-wave parts (Kim & Yue, node GEMM basis) "
+                                           "kept from the design's first QTF (RH_QTF_INCIDENT_CACHED)"},
            "end_to_end_ms": e2e_max * 1e3, "host_tables_ms": tab_max * 1e3,
            "first_call_ms": first_max * 1e3,
            "n_gpus": world, "n2": n2, "pairs_per_qtf": npair,

@@ -446,6 +446,17 @@ long long rh_qtf_workspace_bytes(const rh_qtf_design* q);
 int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
                    const double* M66, rh_c128* qtf, void* work, long long work_bytes, rh_stream stream);
 
+/* rh_qtf_slender with flags.  RH_QTF_INCIDENT_CACHED: `work` already holds the incident-wave
+ * parts of this QTF -- the Kim & Yue tables, their GEMM basis and pair-tile sums, the node GEMM
+ * basis and the zero K tails, none of which depends on the RAO -- from an earlier
+ * rh_qtf_slender(_ext) call with the same q and work on the MFMA path (the caller vouches for
+ * it); only the RAO-dependent tables, coefficients and GEMMs run.  The result equals a full call
+ * bit for bit.  For a design's many QTFs with different RAOs (the second passes of
+ * potSecOrder = 1 cases, raft/second_order.py).  RH_EINVAL on the per-pair path. */
+#define RH_QTF_INCIDENT_CACHED 1
+int rh_qtf_slender_ext(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
+                       const double* M66, rh_c128* qtf, void* work, long long work_bytes, int flags, rh_stream stream);
+
 /* The upper-triangle pairs (w1 <= w2) of one rank of a QTF sharded over nrank devices, no
    Hermitian fill.  The upper triangle is cut into 16 x 16 pair tiles (i1 tile T1 <= i2 tile T2,
    n2 rounded up to 16), numbered row-major; rank r owns the tiles t with t % nrank == r

@@ -204,7 +204,7 @@ extern "C" {
 
 const char* rh_last_error(void) { return g_err.c_str(); }
 
-int rh_version(void) { return 6; }
+int rh_version(void) { return 7; }
 
 // (rh_prof_read / rh_wgt_read of instrumented builds live in rh_solve_fast.hip, beside the counters)
 
@@ -831,7 +831,7 @@ static void qtf_tile_block(int n2, int rank, int nrank, int& t0, int& t1) {
 
 static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
                       const double* M66, int rank, int nrank, int mirror, rh_c128* qtf, void* work,
-                      long long work_bytes, rh_stream stream, const char* who) {
+                      long long work_bytes, rh_stream stream, const char* who, int flags = 0) {
   if (!ctx || !q || !w || !Xi0 || !M66 || !qtf || !work) return fail(RH_EINVAL, "%s: null argument", who);
   if (q->n2 < 1 || q->nq < 0 || q->nmq < 0 || q->nkr < 0 || nw < 2)
     return fail(RH_EINVAL, "%s: bad sizes n2=%d nq=%d nmq=%d nkr=%d nw=%d", who, q->n2, q->nq, q->nmq, q->nkr, nw);
@@ -846,6 +846,12 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   rh::QtfWork wk = rh::qtf_carve(*q, work);
   const bool gemm = q->order == 1 && !ctx->qtf_direct;
   if (!gemm) wk.R = nullptr;                                 // the table kernels skip the GEMM operands
+  if (flags & ~RH_QTF_INCIDENT_CACHED) return fail(RH_EINVAL, "%s: unknown flags 0x%x", who, flags);
+  // RH_QTF_INCIDENT_CACHED: the incident-wave parts (the Kim & Yue tables, basis and pair-tile
+  // sums, the node GEMM basis, the zero K tails) are already in `work` from an earlier call
+  // with this q and these tiles; only the RAO-dependent tables and coefficients are formed
+  const bool cached = (flags & RH_QTF_INCIDENT_CACHED) != 0;
+  if (cached && !gemm) return fail(RH_EINVAL, "%s: the incident-wave cache is kept by the MFMA path only", who);
   const int n2p = rh::qtf_n2p(*q);
   const int nb = (n2p + 63) / 64;
   // This call's pair tiles (MFMA path): the rank's contiguous block [t0, t0 + blocks) of the
@@ -867,7 +873,9 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   const int R0 = blocks > 0 ? row_of(t0) : 0, R1 = blocks > 0 ? row_of(t0 + blocks - 1) + 1 : 0;
   const int fb0 = gemm ? 16 * R0 / 64 : 0;   // first 64-frequency block read (the per-pair path: all)
   // the frequency row, node, waterline and KAY tables (+ GEMM basis and zero K tails): one launch
-  const int trows = 1 + q->nq + q->nmq + q->nkr + (gemm ? q->nq + rh::qtf_npad(*q) : 0);
+  // (rows in this order: frequency row, nodes, waterline members -- RAO-dependent -- then the
+  // Kim & Yue rows, node GEMM basis and zero tails, which depend on the incident wave only)
+  const int trows = 1 + q->nq + q->nmq + (cached ? 0 : q->nkr + (gemm ? q->nq + rh::qtf_npad(*q) : 0));
   if (nb > fb0) {
     hipLaunchKernelGGL(rh::k_qtf_tables, dim3(nb - fb0, trows), dim3(64), 0, s, *q, wk, nw, w, Xi0, M66, fb0);
     RH_HIP(hipGetLastError());
@@ -888,6 +896,7 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
 #if RH_ABL_LK_NOKAY    // timing ablation: no Kim & Yue tiles (wrong results)
       nkb = 0;
 #endif
+      if (cached) nkb = 0;   // their tile sums KS are in the workspace already
 #if RH_ABL_LK_NOCOEF   // timing ablation: no coefficient blocks (wrong results)
       nly = 0;
 #endif
@@ -946,6 +955,11 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
 int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0, const double* M66,
                    rh_c128* qtf, void* work, long long work_bytes, rh_stream stream) {
   return qtf_launch(ctx, q, nw, w, Xi0, M66, 0, 1, 1, qtf, work, work_bytes, stream, "rh_qtf_slender");
+}
+
+int rh_qtf_slender_ext(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,
+                       const double* M66, rh_c128* qtf, void* work, long long work_bytes, int flags, rh_stream stream) {
+  return qtf_launch(ctx, q, nw, w, Xi0, M66, 0, 1, 1, qtf, work, work_bytes, stream, "rh_qtf_slender_ext", flags);
 }
 
 int rh_qtf_slender_rows(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w, const rh_c128* Xi0,

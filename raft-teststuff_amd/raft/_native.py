@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RAFTHIP_LIB", os.path.join(os.path.dirname(_HERE), "librafthip.so"))
 
 RH_OK, RH_EINVAL, RH_ENAN, RH_ESINGULAR, RH_EHIP = 0, -1, -2, -3, -4
+RH_QTF_INCIDENT_CACHED = 1
 RH_CASE_CONVERGED, RH_CASE_NOT_CONVERGED, RH_CASE_NAN, RH_CASE_SINGULAR = 1, 0, -2, -3
 SPECTRUM_CODES = {"JONSWAP": 0, "unit": 1, "constant": 2, "none": 3, "still": 3}
 
@@ -114,6 +115,8 @@ def lib():
                                      _p, ctypes.c_int, _p, _p, _p, _p],
                 "rh_qtf_slender": [_p, ctypes.POINTER(RhQtfDesign), ctypes.c_int, _p, _p, _p, _p, _p,
                                    ctypes.c_longlong, _p],
+                "rh_qtf_slender_ext": [_p, ctypes.POINTER(RhQtfDesign), ctypes.c_int, _p, _p, _p, _p, _p,
+                                       ctypes.c_longlong, ctypes.c_int, _p],
                 "rh_qtf_slender_rows": [_p, ctypes.POINTER(RhQtfDesign), ctypes.c_int, _p, _p, _p, ctypes.c_int,
                                         ctypes.c_int, _p, _p, ctypes.c_longlong, _p],
                 "rh_qtf_hermitian_fill": [_p, ctypes.c_int, _p, _p],

@@ -245,14 +245,17 @@ class QtfDevice:
         q.order = self.order
         return q
 
-    def qtf(self, w, Xi0, M66, out=None, group=None, on_computed=None):
+    def qtf(self, w, Xi0, M66, out=None, group=None, on_computed=None, incident_cached=False):
         """Run rh_qtf_slender: w [nw] / Xi0 [6, nw] device tensors -> qtf [n2, n2, 6] device tensor.
         Sharding is opt-in: only with an explicit process `group` of world > 1 are the pairs
         row-sharded over its ranks (raft/parallel.py) -- a collective every rank of the group
         must enter with the same inputs -- and every rank returns the full matrix.  group=None
         (what FOWT.calcQTF_slenderBody passes) never communicates, so ranks that each solve
         their own cases or designs can call it independently.  on_computed: optional callback
-        run after this rank's pair kernels are enqueued, before any exchange (bench timing)."""
+        run after this rank's pair kernels are enqueued, before any exchange (bench timing).
+        incident_cached: this QtfDevice's workspace holds the incident-wave parts of an earlier
+        whole-QTF call on the default (MFMA) path (rh_qtf_slender_ext RH_QTF_INCIDENT_CACHED):
+        only the RAO-dependent parts run; the same bits as a full call."""
         torch = self.torch
         from .parallel import assemble_qtf, world_of
         if group is not None and world_of(group)[1] > 1:
@@ -260,10 +263,12 @@ class QtfDevice:
                                 device=self.dev, group=group, on_computed=on_computed)
         if out is None:
             out = torch.empty([self.n2, self.n2, 6], dtype=torch.complex128, device=self.dev)
-        N.check(N.lib().rh_qtf_slender(N.context(self.dev_index), ctypes.byref(self.struct_), int(w.numel()), N.ptr(w),
-                                       N.ptr(Xi0), N.ptr(M66), N.ptr(out), N.ptr(self.work),
-                                       ctypes.c_longlong(self.work_bytes), N.stream_handle(torch, self.dev)),
-                "rh_qtf_slender")
+        N.check(N.lib().rh_qtf_slender_ext(N.context(self.dev_index), ctypes.byref(self.struct_), int(w.numel()),
+                                           N.ptr(w), N.ptr(Xi0), N.ptr(M66), N.ptr(out), N.ptr(self.work),
+                                           ctypes.c_longlong(self.work_bytes),
+                                           N.RH_QTF_INCIDENT_CACHED if incident_cached else 0,
+                                           N.stream_handle(torch, self.dev)),
+                "rh_qtf_slender_ext")
         if on_computed is not None:
             on_computed()
         return out

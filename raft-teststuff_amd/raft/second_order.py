@@ -155,14 +155,16 @@ def _second_pass(views, owners, cs, sel, res, S, fext, fmean, nIter, XiStart, to
     dev = views[0].device
     f64 = dict(dtype=torch.float64, device=dev)
     mass = {}
-    for c in sel:
+    warm = set()     # QtfDevices whose incident-wave parts this pass has formed (the same design,
+    for c in sel:    # grid and heading: later cases' QTFs form only their RAO's parts, the same bits)
         v = int(cs.design_idx[c])
         fowt, dd = owners[v], views[v]
         beta = float(cs.heading[c]) * DEG2RAD
         qd = fowt._qtf_device(beta)
         if id(fowt) not in mass:
             mass[id(fowt)] = torch.tensor(np.asarray(fowt.M_struc, dtype=float), **f64).contiguous()
-        q = qd.qtf(dd.w, res["rao"][c].contiguous(), mass[id(fowt)])
+        q = qd.qtf(dd.w, res["rao"][c].contiguous(), mass[id(fowt)], incident_cached=id(qd) in warm)
+        warm.add(id(qd))
         f, fm = force_batch(dd, qd, [q], [0], S[c:c + 1])
         fext[c] = f[0]
         fmean[c] = fm[0]

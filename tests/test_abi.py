@@ -44,7 +44,7 @@ def test_library_exports_every_declared_symbol(libpath):
 def test_library_loads_and_binds(libpath):
     from raft import _native as N
     L = N.lib()
-    assert L.rh_version() == 6
+    assert L.rh_version() == 7
     assert L.rh_group_cases() >= 1
     # the tuning knobs live on a context (no mutable process globals);
     # without a GPU there is no context, and a null one is rejected

@@ -302,3 +302,41 @@ def test_device_tables_are_the_numpy_tables(T):
         for k in ("qnode", "qmemb", "kray", "qmstart", "kstart"):
             np.testing.assert_array_equal(getattr(qd, k).cpu().numpy(), ref[k], err_msg=k)
             np.testing.assert_array_equal(qd.host[k], ref[k], err_msg=k)
+
+
+@pytest.mark.gpu
+def test_incident_cached_qtf_equals_full_qtf(T):
+    """rh_qtf_slender_ext with RH_QTF_INCIDENT_CACHED (the Kim & Yue tables and tile sums, the
+    node GEMM basis: the parts that do not depend on the RAO, kept in the workspace from an
+    earlier call) gives a new RAO's QTF bit for bit as a full call on a fresh workspace; the
+    per-pair path refuses the flag."""
+    import torch
+    from raft import _native as N
+    from raft.hydro_math import wave_numbers
+    from raft.qtf import QtfDevice
+    m, f = make(T)
+    dd = f.device_design()
+    M66 = torch.tensor(f.M_struc, dtype=torch.float64, device=dd.device).contiguous()
+    w2 = np.arange(0.04, 0.35 + 0.5 * 0.04, 0.000825) * 2 * np.pi
+    k2 = wave_numbers(w2, f.depth)
+    X1 = torch.tensor(T["out_Xi0"], dtype=torch.complex128, device=dd.device)
+    rng = np.random.default_rng(5)
+    X2 = X1 * torch.tensor(rng.uniform(0.5, 1.5, X1.shape) * np.exp(1j * rng.uniform(-0.3, 0.3, X1.shape)),
+                           dtype=torch.complex128, device=dd.device)
+    for beta in (0.0, np.deg2rad(30.0)):
+        qd = QtfDevice(f, w2, k2, beta, 0)
+        a1 = qd.qtf(dd.w, X1, M66).clone()
+        a2 = qd.qtf(dd.w, X2, M66, incident_cached=True).clone()
+        a1b = qd.qtf(dd.w, X1, M66, incident_cached=True).clone()
+        ref2 = QtfDevice(f, w2, k2, beta, 0).qtf(dd.w, X2, M66)
+        torch.cuda.synchronize()
+        assert torch.equal(a2, ref2)
+        assert torch.equal(a1b, a1)
+        assert not torch.equal(a1, a2)
+    ctx = N.context(0)
+    N.check(N.lib().rh_set_qtf_path(ctx, 1), "rh_set_qtf_path")
+    try:
+        with pytest.raises(ValueError, match="MFMA path"):
+            qd.qtf(dd.w, X2, M66, incident_cached=True)
+    finally:
+        N.check(N.lib().rh_set_qtf_path(ctx, 0), "rh_set_qtf_path")
