@@ -406,6 +406,18 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    # value: K QTFs one after another, no timing marks between them (as the C2 leg's value);
+    # then the same K with HIP events around each one's kernels, for kernel_ms and the roofline
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        q = qd.qtf(dd.w, X, M66, group=group)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt_serial = time.perf_counter() - t0   # one GPU: a QTF at a time; N GPUs: each QTF tile-sharded
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -416,8 +428,7 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    dt_serial = dt                         # one GPU: a QTF at a time; N GPUs: each QTF tile-sharded
+    ms_marked = (time.perf_counter() - t0) / steps * 1e3
     # The QTF stream pipelined over RAFT_BENCH_QTF_STREAMS HIP streams (default 3: with the
     # 4-wave GEMM, 3 streams 1.13e9 against 1.05e9 pairs/s for 2), each with its own tables and
     # workspace (QtfDevice): one QTF's short table and coefficient launches run beside the
@@ -475,7 +486,7 @@ def bench_qtf(device, steps, warmup, world, rank, dist):
     # own pipelined stream of independent QTFs (weak scaling), beside it (round 5 had made that the
     # value; ADVICE r05: the metric must not change meaning).
     out = {"metric": "QTF pairs/sec", "value": npair * steps / ser_max, "unit": "pairs/s", "steps": steps,
-           "ms_per_qtf": ser_max / steps * 1e3, "scaling": "strong",
+           "ms_per_qtf": ser_max / steps * 1e3, "ms_per_qtf_with_event_marks": ms_marked, "scaling": "strong",
            "streams": {"value": world * npair * steps / dt_max, "unit": "pairs/s", "ms_per_qtf": dt_max / steps * 1e3,
                        "scaling": "weak",
                        "pipeline": f"each GPU's independent QTFs rotate over {nqs} HIP streams with their own tables "
