@@ -557,6 +557,8 @@ def bench_c4(device, steps, world, rank, dist, ncase=512):
     # two events per step, around the fixed-point launch; the step's device time runs from one
     # step's first mark to the next one's (`end` closes the last step).  Every timing event is a
     # barrier packet: 4 per step cost 19 us of a 0.55 ms step (tools/ubench/event_cost.py)
+    # value: the K steps with no timing marks (as the C2 and QTF legs); then the same K with the
+    # marks, for the fixed point's kernel time and the device time per step
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
     end = torch.cuda.Event(enable_timing=True)
     stream = torch.cuda.current_stream()
@@ -565,12 +567,18 @@ def bench_c4(device, steps, world, rank, dist, ncase=512):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
-        r = m.analyzeArrayBatch(prepared=P, host=False, marks=(ev[i][0], ev[i][1]))
-    end.record(stream)
+        r = m.analyzeArrayBatch(prepared=P, host=False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=f"cuda:{device}")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    for i in range(steps):
+        r = m.analyzeArrayBatch(prepared=P, host=False, marks=(ev[i][0], ev[i][1]))
+    end.record(stream)
+    torch.cuda.synchronize()
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
