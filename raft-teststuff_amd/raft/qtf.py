@@ -261,6 +261,8 @@ class QtfDevice:
         if group is not None and world_of(group)[1] > 1:
             return assemble_qtf(lambda o, r, n: self.qtf_rows(w, Xi0, M66, o, r, n), self.hermitian_fill, self.n2,
                                 device=self.dev, group=group, on_computed=on_computed)
+        if incident_cached and not getattr(self, "_incident_ready", False):
+            raise ValueError("QtfDevice.qtf: incident_cached needs an earlier whole-QTF call on this device")
         if out is None:
             out = torch.empty([self.n2, self.n2, 6], dtype=torch.complex128, device=self.dev)
         N.check(N.lib().rh_qtf_slender_ext(N.context(self.dev_index), ctypes.byref(self.struct_), int(w.numel()),
@@ -269,6 +271,7 @@ class QtfDevice:
                                            N.RH_QTF_INCIDENT_CACHED if incident_cached else 0,
                                            N.stream_handle(torch, self.dev)),
                 "rh_qtf_slender_ext")
+        self._incident_ready = True
         if on_computed is not None:
             on_computed()
         return out

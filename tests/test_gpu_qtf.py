@@ -325,6 +325,8 @@ def test_incident_cached_qtf_equals_full_qtf(T):
                            dtype=torch.complex128, device=dd.device)
     for beta in (0.0, np.deg2rad(30.0)):
         qd = QtfDevice(f, w2, k2, beta, 0)
+        with pytest.raises(ValueError, match="earlier whole-QTF call"):
+            qd.qtf(dd.w, X1, M66, incident_cached=True)
         a1 = qd.qtf(dd.w, X1, M66).clone()
         a2 = qd.qtf(dd.w, X2, M66, incident_cached=True).clone()
         a1b = qd.qtf(dd.w, X1, M66, incident_cached=True).clone()
