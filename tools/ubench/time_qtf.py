@@ -40,6 +40,14 @@ def main(tag):
     if tag == "ranks":
         time_ranks(qd, dd, X, M66, int(sys.argv[2]) if len(sys.argv) > 2 else 8)
         return
+    if tag == "pmc_cached":     # one whole QTF, then 20 of new RAOs with the incident parts kept
+        q = qd.qtf(dd.w, X, M66)
+        Xb = (X * 0.9).contiguous()
+        for i in range(20):
+            q = qd.qtf(dd.w, Xb if i % 2 else X, M66, incident_cached=True)
+        torch.cuda.synchronize()
+        print("pmc_cached: 1 + 20 QTFs", flush=True)
+        return
     ref = None
     # PMC passes: the default path only (MFMA GEMMs on this sorted grid); otherwise the
     # per-pair kernel at 1, 2 and 4 waves per tile
