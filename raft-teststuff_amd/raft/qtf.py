@@ -254,8 +254,9 @@ class QtfDevice:
         their own cases or designs can call it independently.  on_computed: optional callback
         run after this rank's pair kernels are enqueued, before any exchange (bench timing).
         incident_cached: this QtfDevice's workspace holds the incident-wave parts of an earlier
-        whole-QTF call on the default (MFMA) path (rh_qtf_slender_ext RH_QTF_INCIDENT_CACHED):
-        only the RAO-dependent parts run; the same bits as a full call."""
+        whole-QTF call on the default (MFMA) path, on this stream or one synchronised with it
+        (rh_qtf_slender_ext RH_QTF_INCIDENT_CACHED): only the RAO-dependent parts run; the same
+        bits as a full call."""
         torch = self.torch
         from .parallel import assemble_qtf, world_of
         if group is not None and world_of(group)[1] > 1:

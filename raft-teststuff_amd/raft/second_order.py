@@ -51,10 +51,13 @@ def sea_spectra(dd, cs_spectrum, Hs, Tp, gamma):
     return S, zeta
 
 
+QTF_CHUNK = 32     # QTFs of one stack in the potSecOrder = 1 second pass (15 MB each on the C3 grid)
+
+
 def force_batch(dd, qdev, qtfs, qidx, S):
     """rh_force_2nd_batch: the 'qtf'-mode force of n sea states (calcHydroForce_2ndOrd,
     raft/raft_fowt.py:1788-1810).  qtfs: list of [n2, n2, 6] device QTFs on qdev's grid; qidx:
-    per sea state, which one; S [n, nw].  Returns (f [n, 6, nw] complex, f_mean [n, 6])."""
+    per sea state, which one (or one [m, n2, n2, 6] tensor); S [n, nw].  Returns (f [n, 6, nw] complex, f_mean [n, 6])."""
     torch = dd.torch
     dev = dd.device
     n, nw = S.shape[0], dd.nw
@@ -62,8 +65,11 @@ def force_batch(dd, qdev, qtfs, qidx, S):
     fm = torch.empty([n, 6], dtype=torch.float64, device=dev)
     if n == 0:
         return f, fm
-    stack = qtfs[0][None] if len(qtfs) == 1 else torch.stack(qtfs)
-    stack = stack.contiguous()
+    if torch.is_tensor(qtfs) and qtfs.dim() == 4:     # already one stack [m, n2, n2, 6]
+        stack = qtfs.contiguous()
+    else:
+        stack = qtfs[0][None] if len(qtfs) == 1 else torch.stack(qtfs)
+        stack = stack.contiguous()
     qi = torch.tensor(np.asarray(qidx, dtype=np.int32), dtype=torch.int32, device=dev)
     S = S.contiguous()
     N.check(N.lib().rh_force_2nd_batch(N.context(dd.dev_index), n, qdev.n2, N.ptr(qdev.w2), N.ptr(stack),
@@ -155,19 +161,28 @@ def _second_pass(views, owners, cs, sel, res, S, fext, fmean, nIter, XiStart, to
     dev = views[0].device
     f64 = dict(dtype=torch.float64, device=dev)
     mass = {}
-    warm = set()     # QtfDevices whose incident-wave parts this pass has formed (the same design,
-    for c in sel:    # grid and heading: later cases' QTFs form only their RAO's parts, the same bits)
+    # the converged cases grouped by QTF (design view, heading): each group's QTFs go into one
+    # stack (chunks of QTF_CHUNK) and its forces come from one rh_force_2nd_batch launch; after
+    # a QtfDevice's first QTF the incident-wave parts are kept (rh_qtf_slender_ext, the same bits)
+    groups = {}
+    for c in sel:
         v = int(cs.design_idx[c])
+        groups.setdefault((v, float(cs.heading[c])), []).append(c)
+    for (v, hdg), cases in groups.items():
         fowt, dd = owners[v], views[v]
-        beta = float(cs.heading[c]) * DEG2RAD
-        qd = fowt._qtf_device(beta)
+        qd = fowt._qtf_device(hdg * DEG2RAD)
         if id(fowt) not in mass:
             mass[id(fowt)] = torch.tensor(np.asarray(fowt.M_struc, dtype=float), **f64).contiguous()
-        q = qd.qtf(dd.w, res["rao"][c].contiguous(), mass[id(fowt)], incident_cached=id(qd) in warm)
-        warm.add(id(qd))
-        f, fm = force_batch(dd, qd, [q], [0], S[c:c + 1])
-        fext[c] = f[0]
-        fmean[c] = fm[0]
+        for lo in range(0, len(cases), QTF_CHUNK):
+            cc = cases[lo:lo + QTF_CHUNK]
+            stack = torch.empty([len(cc), qd.n2, qd.n2, 6], dtype=torch.complex128, device=dev)
+            for j, c in enumerate(cc):
+                qd.qtf(dd.w, res["rao"][c].contiguous(), mass[id(fowt)], out=stack[j],
+                       incident_cached=getattr(qd, "_incident_ready", False))
+            idx = torch.tensor(cc, dtype=torch.long, device=dev)
+            f, fm = force_batch(dd, qd, stack, np.arange(len(cc)), S.index_select(0, idx))
+            fext.index_copy_(0, idx, f)
+            fmean.index_copy_(0, idx, fm)   # (the stack is freed in stream order)
     st = torch.tensor(sel, dtype=torch.long, device=dev)
     sub = CaseSet(cs.design_idx[sel], cs.heading[sel], cs.spectrum[sel], cs.Hs[sel], cs.Tp[sel], cs.gamma[sel])
     fx = fext.index_select(0, st).contiguous()
