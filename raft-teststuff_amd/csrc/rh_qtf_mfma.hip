@@ -524,46 +524,14 @@ __device__ __forceinline__ void dlin_unit(int j, double x, double y, double z, d
     case 2: o[2] = 1; break;
     case 3: o[1] = -z; o[2] = y; break;
     case 4: o[0] = z; o[2] = -x; break;
-    default: o[0] = -y; o[1] = x; break;
+    case 5: o[0] = -y; o[1] = x; break;
+    default: break;
   }
 }
 
 // global probe g (0..17) of node n: X_j -> conj(dr2); w X_j -> conj(v2) = -i conj(w dr2)
-// (its projection vp and the axial part va) and conj(om2) = -i conj(w X[3:]); w^2 X: none
-__device__ __forceinline__ void node_probe_glob(const rh_qtf_design& q, int n, int g, const NodeW1& a, cd* Q) {
-  NodeZ z;
-  const double x = qn(q, RH_QN_RX, n), y = qn(q, RH_QN_RY, n), zz = qn(q, RH_QN_RZ, n);
-  double D[3];
-  if (g < 6) {
-    dlin_unit(g, x, y, zz, D);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) z.dr[i] = mk(D[i], 0);
-    node_force_z<ZDR>(q, n, a, z, Q);
-  } else if (g < 12) {
-    const int j = g - 6;
-    dlin_unit(j, x, y, zz, D);
-    const double qv[3] = {qn(q, RH_QN_QX, n), qn(q, RH_QN_QY, n), qn(q, RH_QN_QZ, n)};
-    cd v[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) v[i] = mk(0, -D[i]);
-    const cd vq = add(add(scl(v[0], qv[0]), scl(v[1], qv[1])), scl(v[2], qv[2]));
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      z.vp[i] = sub(v[i], scl(vq, qv[i]));
-      z.om[i] = mk(0, 0);
-    }
-    z.va = scl(vq, -1.0);                      // conj(va2) = (conj u2 - conj v2) . q with conj u2 = 0
-    if (j >= 3) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) z.om[i] = mk(0, i == j - 3 ? -1.0 : 0.0);   // no dynamic register index
-      node_force_z<ZVP | ZVA | ZOM>(q, n, a, z, Q);
-    } else {
-      node_force_z<ZVP | ZVA>(q, n, a, z, Q);
-    }
-  }
-}
-
-// node_probe_glob for one kind of probe: K = 0 (g < 6: X_j), 1 (6 <= g < 9: w X_j translation),
+// (its projection vp and the axial part va) and conj(om2) = -i conj(w X[3:]); w^2 X: none.
+// One kind of probe per instantiation: K = 0 (g < 6: X_j), 1 (6 <= g < 9: w X_j translation),
 // 2 (9 <= g < 12: w X_j rotation): the same arithmetic, one node_force_z instantiation per kind
 template <int K>
 __device__ __forceinline__ void node_probe_glob_k(const rh_qtf_design& q, int n, int g, const NodeW1& a, cd* Q) {
@@ -590,8 +558,13 @@ __device__ __forceinline__ void node_probe_glob_k(const rh_qtf_design& q, int n,
     }
     z.va = scl(vq, -1.0);
     if constexpr (K == 2) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) z.om[i] = mk(0, i == j - 3 ? -1.0 : 0.0);
+      // Written out per component, as are dlin_unit's cases: the loop form
+      // (z.om[i] = i == j - 3 ? -i : 0, with dlin_unit's yaw row as `default`) came out of the
+      // compiler with a wrong yaw column (g = 11) while g = 9, 10 were right
+      // (tools/ubench/qtf_lcol_diag.py); the per-pair path had it right
+      z.om[0] = mk(0, j == 3 ? -1.0 : 0.0);
+      z.om[1] = mk(0, j == 4 ? -1.0 : 0.0);
+      z.om[2] = mk(0, j == 5 ? -1.0 : 0.0);
       node_force_z<ZVP | ZVA | ZOM>(q, n, a, z, Q);
     } else {
       node_force_z<ZVP | ZVA>(q, n, a, z, Q);
@@ -688,15 +661,16 @@ __device__ __forceinline__ void pinkster_probe(const rh_qtf_design& q, const Qtf
 #pragma unroll
   for (int i = 0; i < 6; ++i) F2c[i] = mk(0, 0);
   if (g >= 3 && g < 6) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) th2c[i] = mk(i == g - 3 ? 1.0 : 0.0, 0);
+    th2c[0] = mk(g == 3 ? 1.0 : 0.0, 0);
+    th2c[1] = mk(g == 4 ? 1.0 : 0.0, 0);
+    th2c[2] = mk(g == 5 ? 1.0 : 0.0, 0);
   } else if (g >= 12) {
     const int j = g - 12;
+    F2c[0] = mk(j == 0 ? -M66[0] : 0.0, 0);
+    F2c[1] = mk(j == 1 ? -M66[0] : 0.0, 0);
+    F2c[2] = mk(j == 2 ? -M66[0] : 0.0, 0);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      F2c[i] = mk(i == j ? -M66[0] : 0.0, 0);
-      F2c[3 + i] = mk(j >= 3 ? -M66[6 * (3 + i) + j] : 0.0, 0);
-    }
+    for (int i = 0; i < 3; ++i) F2c[3 + i] = mk(j >= 3 ? -M66[6 * (3 + i) + j] : 0.0, 0);
   } else {
     return;
   }

@@ -132,7 +132,8 @@ def test_mfma_path_matches_per_pair_kernel(T, beta_deg, grid):
     against the per-pair kernel k_qtf_pairs (rh_set_qtf_path(ctx, 1)): the same arithmetic
     reassociated, so they agree far inside the 1e-9 parity bar (1e-12 normwise, elementwise
     to 1e-12 of the largest entry), with the moving body and fixed, at 0 and 30 degrees (Q1).
-    In a variant library (tools/build_variants.sh, RAFTHIP_LIB) the 32 x 32 GEMM tiles
+    The RAOs: the reference's (no sway, roll or yaw at 0 degrees), none, and a seeded random
+    one in all six DOFs.  In a variant library (tools/build_variants.sh, RAFTHIP_LIB) the 32 x 32 GEMM tiles
     (rh_set_qtf_path(ctx, 2)) and the GEMM coefficients and Kim & Yue sums as two launches
     (rh_set_qtf_path(ctx, 3), one merged launch by default) give the default's bits; the shipped
     library refuses those paths."""
@@ -153,7 +154,9 @@ def test_mfma_path_matches_per_pair_kernel(T, beta_deg, grid):
     ctx = N.context(0)
     variants = N.lib().rh_set_qtf_path(ctx, 2) == N.RH_OK
     N.check(N.lib().rh_set_qtf_path(ctx, 0), "rh_set_qtf_path")
-    for X0 in (T["out_Xi0"], np.zeros_like(T["out_Xi0"])):
+    rng = np.random.default_rng(11)
+    Xr = (rng.normal(size=T["out_Xi0"].shape) + 1j * rng.normal(size=T["out_Xi0"].shape)) * np.abs(T["out_Xi0"]).max()
+    for X0 in (T["out_Xi0"], np.zeros_like(T["out_Xi0"]), Xr):   # Xr: every DOF moving, yaw included
         X = torch.tensor(X0, dtype=torch.complex128, device=dd.device)
         out = []
         try:
@@ -201,6 +204,25 @@ def test_device_hankel_table_matches_scipy(T):
     ref = hank_table(x, 1.0)
     err = np.abs(out[0].cpu().numpy() - ref) / np.abs(ref)
     assert err.max() < 1e-13, err.max()
+
+
+@pytest.mark.parametrize("beta_deg", [0.0, 30.0])
+def test_all_dof_rao_qtf_matches_oracle(T, beta_deg):
+    """A seeded random RAO moving in all six DOFs (the reference's golden RAO has no sway, roll
+    or yaw) through the default (MFMA) path against the oracle on the golden 42-frequency grid,
+    1e-9 normwise and elementwise to 1e-9 of the largest entry.  The yaw column of the GEMM
+    coefficients was once wrong while every golden-RAO test passed."""
+    from oracle import qtf_oracle as Q
+    m, f = make(T)
+    f.calcHydroExcitation(_case(T), memberList=f.memberList)
+    f.beta = np.array([np.deg2rad(beta_deg)])
+    rng = np.random.default_rng(12 + int(beta_deg))
+    X0 = T["out_Xi0"]
+    X = (rng.normal(size=X0.shape) + 1j * rng.normal(size=X0.shape)) * np.abs(X0).max()
+    f.calcQTF_slenderBody(0, Xi0=X)
+    ref = Q.qtf_slender(T, X, T["w1_2nd"], T["k1_2nd"], np.deg2rad(beta_deg))
+    assert rel(f.qtf, ref) < RTOL, rel(f.qtf, ref)
+    np.testing.assert_allclose(f.qtf, ref, rtol=0, atol=RTOL * np.abs(ref).max())
 
 
 def test_fixed_body_qtf_matches_oracle(T):
@@ -342,3 +364,48 @@ def test_incident_cached_qtf_equals_full_qtf(T):
             qd.qtf(dd.w, X2, M66, incident_cached=True)
     finally:
         N.check(N.lib().rh_set_qtf_path(ctx, 0), "rh_set_qtf_path")
+
+
+@pytest.mark.gpu
+def test_qtf_of_a_design_without_kim_yue_rows_cached_and_oracle():
+    """VolturnUS-S (no MacCamy-Fuchs members: no Kim & Yue rows, nkr = 0; rectangular pontoons)
+    on a 24-frequency grid: the native tables equal build_tables, the MFMA QTF agrees with the
+    per-pair kernel (1e-12), and a further RAO with the incident parts kept equals a whole QTF
+    bit for bit.  (No reference run of this design's QTF exists: the QTF itself is pinned on
+    OC4semi above; here the nkr = 0 paths are.)"""
+    import torch
+    import raft
+    from raft import _native as N
+    from raft.hydro_math import wave_numbers
+    from raft.qtf import QtfDevice, build_tables
+    d = load_design("VolturnUS-S_example")
+    m = raft.Model(d)
+    f = m.fowtList[0]
+    f.setPosition(np.zeros(6))
+    f.calcStatics()
+    f.calcHydroConstants()
+    dd = f.device_design()
+    w2 = np.linspace(0.3, 1.8, 24)
+    k2 = wave_numbers(w2, f.depth)
+    qd = QtfDevice(f, w2, k2, np.deg2rad(20.0), 0)
+    assert qd.nkr == 0 and qd.order == 1
+    ref_t = build_tables(f, w2, k2, np.deg2rad(20.0))
+    for k in ("qnode", "qmemb", "kray", "qmstart", "kstart"):
+        np.testing.assert_array_equal(qd.host[k], ref_t[k], err_msg=k)
+    rng = np.random.default_rng(9)
+    M66 = torch.tensor(f.M_struc, dtype=torch.float64, device=dd.device).contiguous()
+    X1 = (rng.normal(size=(6, f.nw)) + 1j * rng.normal(size=(6, f.nw))) * 0.5
+    X2 = X1 * 1.3 + 0.1j
+    T1 = torch.tensor(X1, dtype=torch.complex128, device=dd.device)
+    T2 = torch.tensor(X2, dtype=torch.complex128, device=dd.device)
+    a1 = qd.qtf(dd.w, T1, M66).cpu().numpy()
+    a2 = qd.qtf(dd.w, T2, M66, incident_cached=True).cpu().numpy()
+    ref2 = QtfDevice(f, w2, k2, np.deg2rad(20.0), 0).qtf(dd.w, T2, M66).cpu().numpy()
+    np.testing.assert_array_equal(a2, ref2)
+    ctx = N.context(0)
+    N.check(N.lib().rh_set_qtf_path(ctx, 1), "rh_set_qtf_path")
+    try:
+        p1 = QtfDevice(f, w2, k2, np.deg2rad(20.0), 0).qtf(dd.w, T1, M66).cpu().numpy()
+    finally:
+        N.check(N.lib().rh_set_qtf_path(ctx, 0), "rh_set_qtf_path")
+    assert np.abs(a1).max() > 0 and rel(a1, p1) < 1e-12, rel(a1, p1)
