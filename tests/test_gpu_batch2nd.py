@@ -79,6 +79,23 @@ def test_slender_body_qtf_design_through_the_batch():
                              wave_spectrum=["JONSWAP", "JONSWAP"], wave_gamma=[0.0, 0.0]))
 
 
+def test_slender_body_batch_off_axis_headings_match_oracle():
+    """potSecOrder=1 at 30 and 60 degrees, where the first-pass RAO has sway, roll and yaw (the
+    reference run is at 0 degrees, and solveDynamics shares the batch's QTF kernels): the batch
+    against the oracle's whole potSecOrder=1 solve (oracle/raft_oracle.py solve_dynamics with
+    its qtf_slender), 1e-9 and the same iteration pair."""
+    T = load_golden("c3_qtf")
+    m, f = _qtf_model(T)
+    cases = _seeded(np.random.default_rng(67), 4, headings=(30.0, 60.0))
+    r = m.analyzeCasesBatch(cases)
+    for j, c in enumerate(cases):
+        o = O.solve_dynamics(T, dict(c), int(T["nIter"]), float(T["XiStart"]),
+                             second_order=dict(w1_2nd=T["w1_2nd"], k1_2nd=T["k1_2nd"]))
+        assert list(r["iters_pair"][j]) == list(o["iters_pair"]), (j, r["iters_pair"][j], o["iters_pair"])
+        assert np.abs(o["Xi"][0, 5]).max() > 1e-3 * np.abs(o["Xi"][0]).max()      # the RAO yaws
+        assert rel(r["Xi"][j], o["Xi"][0]) < RTOL, (j, rel(r["Xi"][j], o["Xi"][0]))
+
+
 def test_slender_body_unconverged_first_pass_keeps_first_order():
     """tol = 1e-13: no case converges in the first pass, so no QTF is formed (the reference
     reaches :966 only on convergence) and the batch equals solveDynamics with first order only."""
