@@ -524,7 +524,7 @@ __device__ __forceinline__ void dlin_unit(int j, double x, double y, double z, d
     case 2: o[2] = 1; break;
     case 3: o[1] = -z; o[2] = y; break;
     case 4: o[0] = z; o[2] = -x; break;
-    case 5: o[0] = -y; o[1] = x; break;
+    case 5: o[0] = -y; o[1] = x; break;   // not `default`: see node_probe_glob_k
     default: break;
   }
 }
@@ -558,10 +558,10 @@ __device__ __forceinline__ void node_probe_glob_k(const rh_qtf_design& q, int n,
     }
     z.va = scl(vq, -1.0);
     if constexpr (K == 2) {
-      // Written out per component, as are dlin_unit's cases: the loop form
-      // (z.om[i] = i == j - 3 ? -i : 0, with dlin_unit's yaw row as `default`) came out of the
-      // compiler with a wrong yaw column (g = 11) while g = 9, 10 were right
-      // (tools/ubench/qtf_lcol_diag.py); the per-pair path had it right
+      // Written out per component.  dlin_unit's yaw row must stay an explicit `case 5`: as the
+      // switch's `default` it came out of the compiler with a wrong yaw column here (g = 11;
+      // g = 9, 10 right; the loop form of these three lines alone was fine), DESIGN.md §5,
+      // tools/ubench/qtf_lcol_diag.py, profiles/r06_v6/yaw_variants.txt
       z.om[0] = mk(0, j == 3 ? -1.0 : 0.0);
       z.om[1] = mk(0, j == 4 ? -1.0 : 0.0);
       z.om[2] = mk(0, j == 5 ? -1.0 : 0.0);
