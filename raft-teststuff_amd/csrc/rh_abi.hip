@@ -4,8 +4,13 @@
 // the design descriptors, kernel configuration and error translation.  No numerics here.
 #include <cstdarg>
 #include <cstdio>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <mutex>
+#include <thread>
+
+#include <unistd.h>
 #include <string>
 #include <vector>
 
@@ -1026,6 +1031,67 @@ int rh_force_2nd_spectrum(rh_ctx* ctx, int n2, const double* w2, const rh_c128* 
 
 
 // ---------------------------------------------------------------- native design preparation
+namespace {
+// Worker threads kept across rh_prep_designs calls.  Spawning and joining 16 threads per call
+// cost 0.3-0.7 ms of host time, paid by every design block of a sweep and in full by its first
+// block, which nothing overlaps.  One job at a time (callers queue on call_mx); the caller runs the
+// job too.  A forked child gets a new pool: the parent's threads do not exist there, so the old
+// pool is left alone (never destroyed, as is the process-lifetime pool itself).
+struct PrepPool {
+  explicit PrepPool(pid_t p) : pid(p) {}
+  const pid_t pid;
+  std::mutex call_mx, mx;
+  std::condition_variable cv_start, cv_done;
+  std::vector<std::thread> th;
+  const std::function<void()>* job = nullptr;
+  unsigned long gen = 0;
+  int want = 0, pending = 0;
+
+  void worker(int idx) {
+    unsigned long seen = 0;
+    std::unique_lock<std::mutex> lk(mx);
+    for (;;) {
+      cv_start.wait(lk, [&] { return gen != seen; });
+      seen = gen;
+      if (idx >= want) continue;
+      const std::function<void()>* f = job;
+      lk.unlock();
+      (*f)();
+      lk.lock();
+      if (--pending == 0) cv_done.notify_all();
+    }
+  }
+  // fn on nt threads (the caller and nt - 1 workers), back when every one has returned
+  void run(int nt, const std::function<void()>& fn) {
+    std::lock_guard<std::mutex> call(call_mx);
+    const int helpers = nt - 1;
+    {
+      std::lock_guard<std::mutex> lk(mx);
+      while ((int)th.size() < helpers) {
+        const int idx = (int)th.size();
+        th.emplace_back([this, idx] { worker(idx); });
+      }
+      job = &fn;
+      want = helpers;
+      pending = helpers;
+      ++gen;
+    }
+    cv_start.notify_all();
+    fn();
+    std::unique_lock<std::mutex> lk(mx);
+    cv_done.wait(lk, [&] { return pending == 0; });
+    job = nullptr;
+  }
+  static PrepPool& get() {   // this process's pool
+    static std::mutex m;
+    static PrepPool* pool = nullptr;
+    std::lock_guard<std::mutex> lk(m);
+    if (!pool || pool->pid != getpid()) pool = new PrepPool(getpid());
+    return *pool;
+  }
+};
+}  // namespace
+
 int rh_prep_designs(int ndesign, const double* spec, const long long* spec_off, int nw, const double* w,
                     const double* k, int nthreads, rh_prep** out) {
   if (!out) return fail(RH_EINVAL, "rh_prep_designs: null out");
@@ -1053,9 +1119,8 @@ int rh_prep_designs(int ndesign, const double* spec, const long long* spec_off, 
   if (nt == 1) {
     work();
   } else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t) th.emplace_back(work);
-    for (auto& t : th) t.join();
+    const std::function<void()> job(work);
+    PrepPool::get().run(nt, job);
   }
   for (int i = 0; i < ndesign; ++i)
     if (!p->res[i].ok) {

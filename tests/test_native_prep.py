@@ -144,3 +144,52 @@ def test_native_bad_specs():
         PreparedDesigns([bad], w, w)
     assert N.lib().rh_prep_layout(None, None) == N.RH_EINVAL
     assert N.lib().rh_prep_imat(None, 0, None) == N.RH_EINVAL
+
+
+def _pool_specs(n):
+    from raft.hydro_math import wave_numbers
+    from raft.model import Model
+    from raft.native_prep import design_spec
+    from raft.sweep import sweep_multipliers, sweep_variant
+    base = load_design("VolturnUS-S_example")
+    designs = [sweep_variant(base, m) for m in sweep_multipliers(n, seed=7)]
+    w = Model.frequency_grid(base)
+    k = wave_numbers(w, float(base["site"]["water_depth"]))
+    return [design_spec(d, statics={"C_moor": C_MOOR}) for d in designs], w, k
+
+
+def _pool_child(q, specs, w, k):
+    from raft.native_prep import PreparedDesigns
+    q.put(PreparedDesigns(specs, w, k, nthreads=3).packed.tobytes())
+
+
+def test_prep_worker_pool_threads_callers_and_fork():
+    """rh_prep_designs runs on worker threads kept across calls (csrc/rh_abi.hip PrepPool):
+    every thread count gives the single-thread tables bit for bit, calls from several Python
+    threads at once (queued on the pool) too, and a forked child, which has none of its
+    parent's workers, gets a pool of its own."""
+    import multiprocessing as mp
+    import threading
+    from raft.native_prep import PreparedDesigns
+    specs, w, k = _pool_specs(12)
+    ref = PreparedDesigns(specs, w, k, nthreads=1).packed.copy()
+    for nt in (2, 5, 16, 3, 16):
+        np.testing.assert_array_equal(PreparedDesigns(specs, w, k, nthreads=nt).packed, ref)
+    out = [None] * 4
+    def call(i):
+        out[i] = PreparedDesigns(specs, w, k, nthreads=2 + 3 * i).packed.copy()
+    th = [threading.Thread(target=call, args=(i,)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    for o in out:
+        np.testing.assert_array_equal(o, ref)
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    p = ctx.Process(target=_pool_child, args=(q, specs, w, k))
+    p.start()
+    got = q.get(timeout=120)
+    p.join(60)
+    assert p.exitcode == 0
+    assert got == ref.tobytes()
