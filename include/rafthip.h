@@ -507,7 +507,10 @@ int rh_force_2nd_spectrum(rh_ctx* ctx, int n2, const double* w2, const rh_c128* 
  * here in C++ (raft-teststuff_amd/csrc/rh_prep.h) so that a design sweep (C5) pays no
  * interpreter time per design.  spec: one float64 record per design, design i at
  * spec[spec_off[i] .. spec_off[i+1]) (format: rh_prep.h; writer: raft/native_prep.py).
- * w, k [nw]: the shared frequency grid and wave numbers.  nthreads <= 0: all host cores.
+ * w, k [nw]: the shared frequency grid and wave numbers.  nthreads <= 0: all host cores (at
+ * most 64).  The calling thread works too; the other nthreads - 1 are kept by the library
+ * across calls (created on first need, one call at a time: concurrent callers queue; a forked
+ * child makes its own).
  * MacCamy-Fuchs members (raft/raft_member.py:1053-1088) get their frequency-dependent inertial
  * excitation matrices, one [9][nw] block per node: rh_prep_imat. */
 typedef struct rh_prep rh_prep;
