@@ -30,6 +30,9 @@
 #include "../../tools/ubench/variants_src/rh_a0.hip"            // k_a0_sums (rh_set_a0)
 #include "../../tools/ubench/variants_src/rh_qtf_variants.hip"  // k_qtf_gemm32, k_qtf_lcoef + k_qtf_kay (rh_set_qtf_path 2, 3)
 #endif
+#ifndef RH_KAY_SPLIT_MAX_TILES
+#define RH_KAY_SPLIT_MAX_TILES(ncu) (ncu)   // k_qtf_lk: one wave per part of a member's rows up to this many tiles
+#endif
 #include "rh_prep.h"       // host-only: native per-design preparation (rh_prep_designs)
 #include "rh_qtf_host.h"   // host-only: the static QTF tables of a FOWT (rh_qtf_tables)
 
@@ -896,8 +899,13 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
     constexpr bool sep = false, t32 = false;
 #endif
     if (blocks > 0 && !sep) {
-      // the Kim & Yue tiles (two per workgroup) and the GEMM coefficient blocks in one launch
-      int nkb = (blocks + rh::kLkTiles - 1) / rh::kLkTiles, nly = 18 + q->nq + q->nmq;
+      // the Kim & Yue tiles and the GEMM coefficient blocks in one launch.  A call with few
+      // tiles (a rank's share of a sharded QTF) gives each tile a workgroup and each part of a
+      // member's rows a wave (S = kKayP); a whole QTF two tiles per workgroup (S = 1).  The same
+      // bits either way (kay_tile), so a sharded QTF still equals the single-device one.
+      const bool split = blocks <= RH_KAY_SPLIT_MAX_TILES(ctx->ncu);
+      const int per = split ? rh::lk_tiles<rh::kKayP>() : rh::lk_tiles<1>();
+      int nkb = (blocks + per - 1) / per, nly = 18 + q->nq + q->nmq;
 #if RH_ABL_LK_NOKAY    // timing ablation: no Kim & Yue tiles (wrong results)
       nkb = 0;
 #endif
@@ -905,8 +913,12 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
 #if RH_ABL_LK_NOCOEF   // timing ablation: no coefficient blocks (wrong results)
       nly = 0;
 #endif
-      hipLaunchKernelGGL(rh::k_qtf_lk, dim3(nkb + nbx * nly), dim3(rh::kLkThreads), 0, s, *q, wk, M66, t0, blocks,
-                         nkb, bx0, nbx);
+      if (split)
+        hipLaunchKernelGGL(rh::k_qtf_lk<rh::kKayP>, dim3(nkb + nbx * nly), dim3(rh::kLkThreads), 0, s, *q, wk, M66, t0,
+                           blocks, nkb, bx0, nbx);
+      else
+        hipLaunchKernelGGL(rh::k_qtf_lk<1>, dim3(nkb + nbx * nly), dim3(rh::kLkThreads), 0, s, *q, wk, M66, t0, blocks,
+                           nkb, bx0, nbx);
       RH_HIP(hipGetLastError());
     } else {
 #ifdef RH_VARIANTS

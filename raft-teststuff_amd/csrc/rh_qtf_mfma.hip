@@ -1161,27 +1161,37 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(RH_QT
 // order.  The next row's operands are loaded while the current row is reduced.
 
 #ifndef RH_KAY_SPLIT
-#define RH_KAY_SPLIT 1   // 2 and 4 measured slower
+#define RH_KAY_SPLIT 1   // waves per member of the variants' k_qtf_kay (k_qtf_lk picks per call)
 #endif
 constexpr int kKayM = 4;                   // Kim & Yue members per round
-constexpr int kKayS = RH_KAY_SPLIT;        // waves per member: each takes a contiguous part of its rows
-constexpr int kKayW = kKayM * kKayS;
-constexpr int kKayThreads = 64 * kKayW;
+// A member's rows are summed in kKayP contiguous parts, and the parts' sums added in part order,
+// whether one wave takes all the parts one after the other (S = 1) or each part has a wave of
+// its own (S = kKayP): the same bits either way, so the launch can pick S per call (a rank's few
+// tiles of a sharded QTF: S = kKayP, more waves per tile; a whole QTF: S = 1, two tiles per block)
+constexpr int kKayP = 2;
+static_assert(kKayP == 2, "kay_tile: the part sums are added as P0 + P1");
+template <int S>
+constexpr int kay_threads() { return 64 * kKayM * S; }
+constexpr int kKayS = RH_KAY_SPLIT;
+constexpr int kKayThreads = kay_threads<kKayS>();
 // One pair tile's Kim & Yue sums by a group of kKayW waves (tid 0 .. kKayThreads - 1 of the
 // group) into acc[12][256]; live = false: the group has no tile and only joins the block's
 // barriers (every group of a block runs the same member rounds).  Every __syncthreads here is
 // a whole-block barrier: the caller's block is made of such groups only.  A member's rows are
 // split into kKayS contiguous parts, one per wave; the parts' row sums meet in part order
 // (psg, LDS) before the member's phase is applied.
+template <int S>
 __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& wk, int T1, int T2, bool live, int tid,
                                          double (*acc)[256], double* psg) {
+  static_assert(S == 1 || S == kKayP, "kay_tile: one wave per member or one per part");
+  constexpr int kThreads = kay_threads<S>();
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int slot = wv / kKayS, part = wv % kKayS;
+  const int slot = wv / S, part = wv % S;
   const int n2 = q.n2, n2p = qtf_n2p(q), nt = n2p / 16, nkr = q.nkr;
   const int mr = lane & 15, kr = lane >> 4;
   const int i1b = 16 * T1, i2b = 16 * T2;
-  for (int e = tid; e < 12 * 256; e += kKayThreads) (&acc[0][0])[e] = 0.0;
+  for (int e = tid; e < 12 * 256; e += kThreads) (&acc[0][0])[e] = 0.0;
   const double rho = q.rho, g = q.g, h = q.depth;
   const double cbr = cos(q.beta), sbr = sin(q.beta);
   const int i2s = min(i2b + mr, n2 - 1);
@@ -1211,7 +1221,6 @@ __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& 
       for (int r = 0; r < 4; ++r) sg[c][r] = 0.0;
     if (mine >= 0) {
       const int r0 = ldsi(q.kstart + mine), r1m = min(ldsi(q.kstart + mine + 1), nkr);
-      const int ra = r0 + (r1m - r0) * part / kKayS, r1 = r0 + (r1m - r0) * (part + 1) / kKayS;
       double va[6], vb[6], vr[6];
       auto load_row = [&](int ir, double* A, double* B, double* Rr) {
         const size_t o1 = ((size_t)ir * kKayK + kr) * n2p + i1b + mr, o2 = ((size_t)ir * kKayK + kr) * n2p + i2b + mr;
@@ -1235,8 +1244,22 @@ __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& 
         k1v[r] = q.k2[i1];
         w1v[r] = q.w2[i1];
       }
+      // S = 1: all the member's rows in order, part 0's sums parked in this lane's psg slot when
+      // part 1 begins (r1m > r0: a member in the scan has rows, so that happens once)
+      const int rmid = r0 + (r1m - r0) / kKayP;
+      const int ra = S == 1 ? r0 : r0 + (r1m - r0) * part / kKayP;
+      const int r1 = S == 1 ? r1m : r0 + (r1m - r0) * (part + 1) / kKayP;
 #pragma unroll 1
       for (int ir = ra; ir < r1; ++ir) {
+        if (S == 1 && ir == rmid) {   // wave-uniform
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              psg[(slot * 16 + 4 * c + r) * 64 + lane] = sg[c][r];
+              sg[c][r] = 0.0;
+            }
+        }
         load_row(ir, va, vb, vr);
         double t1[4][6], t2[6];
         {
@@ -1298,21 +1321,26 @@ __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& 
           sg[3][r] += sre * pz;
         }
       }
+      if (S == 1) {   // P0 + P1: part 0's sums (parked) plus part 1's
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sg[c][r] = psg[(slot * 16 + 4 * c + r) * 64 + lane] + sg[c][r];
+      }
     }
-    if (kKayS > 1) {   // the later parts' row sums to the first part's wave, added in part order
+    if (S > 1) {   // part 1's row sums to part 0's wave: P0 + P1
       if (part > 0 && mine >= 0) {
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) psg[((slot * (kKayS - 1) + part - 1) * 16 + 4 * c + r) * 64 + lane] = sg[c][r];
+          for (int r = 0; r < 4; ++r) psg[(slot * 16 + 4 * c + r) * 64 + lane] = sg[c][r];
       }
       __syncthreads();
       if (part == 0 && mine >= 0) {
-        for (int pp = 1; pp < kKayS; ++pp)
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < 4; ++c)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) sg[c][r] += psg[((slot * (kKayS - 1) + pp - 1) * 16 + 4 * c + r) * 64 + lane];
+          for (int r = 0; r < 4; ++r) sg[c][r] += psg[(slot * 16 + 4 * c + r) * 64 + lane];
       }
     }
     // this round's members reach the tile sum in member order (deterministic): at its turn a
@@ -1346,7 +1374,7 @@ __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& 
   // the tile's Kim & Yue sums to the workspace; the GEMM epilogue adds them to the pair sums
   if (live) {
     double* ks = wk.KS + (size_t)qtf_tile_id(T1, T2, nt) * 12 * 256;
-    for (int e = tid; e < 12 * 256; e += kKayThreads) ks[e] = (&acc[0][0])[e];
+    for (int e = tid; e < 12 * 256; e += kThreads) ks[e] = (&acc[0][0])[e];
   }
 }
 
@@ -1355,29 +1383,34 @@ __device__ __forceinline__ void kay_tile(const rh_qtf_design& q, const QtfWork& 
 #define RH_KAY_WPE 2
 #endif
 // k_qtf_lcoef and k_qtf_kay in ONE launch (both read only the tables of k_qtf_tables): the
-// first nkb workgroups take two Kim & Yue pair tiles each (two kay_tile groups of kKayThreads),
-// the rest are k_qtf_lcoef's (x, y) blocks, so the coefficient blocks fill the CUs the Kim & Yue
-// tiles leave idle instead of running before them.  Per tile and per block the arithmetic is
-// that of the two kernels: the same bits.
-constexpr int kLkTiles = 512 / kKayThreads;   // Kim & Yue tiles per k_qtf_lk block (2, or 1 when split)
-constexpr int kLkThreads = kLkTiles * kKayThreads;
+// first nkb workgroups take the Kim & Yue pair tiles (S = 1: two tiles per workgroup, one wave
+// per member; S = kKayP: one tile, one wave per part of a member's rows), the rest are
+// k_qtf_lcoef's (x, y) blocks, so the coefficient blocks fill the CUs the Kim & Yue tiles leave
+// idle instead of running before them.  Per tile and per block the arithmetic is that of the
+// two kernels, and either S gives the same bits.
+template <int S>
+constexpr int lk_tiles() { return 512 / kay_threads<S>(); }   // Kim & Yue tiles per k_qtf_lk block
+constexpr int kLkThreads = 512;
+constexpr int kPsg = kKayM * (kKayP - 1) * 16 * 64;          // one group's parked / handed part sums
 
 static_assert(kLkThreads == 512, "k_qtf_lk: lcoef_block is a 512-thread block");
+template <int S>
 __global__ __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(RH_KAY_WPE))) void k_qtf_lk(
     rh_qtf_design q, QtfWork wk, const double* __restrict__ M66, int t0, int ntile, int nkb, int bx0, int nbx) {
+  constexpr int kTiles = lk_tiles<S>(), kThreads = kay_threads<S>();
   constexpr int kAcc = 12 * 256, kRed = 8 * 12 * 64;
   constexpr int kSm = 2 * kAcc > kRed ? 2 * kAcc : kRed;
-  __shared__ double sm[kSm];                 // kLkTiles Kim & Yue tile sums, or lcoef_block's wave sums
-  __shared__ double psg[kKayS > 1 ? kLkTiles * kKayM * (kKayS - 1) * 16 * 64 : 1];
+  __shared__ double sm[kSm];                 // kTiles Kim & Yue tile sums, or lcoef_block's wave sums
+  __shared__ double psg[kTiles * kPsg];
   const int tid = (int)threadIdx.x;
   if ((int)blockIdx.x < nkb) {               // block-uniform
-    const int grp = __builtin_amdgcn_readfirstlane(tid / kKayThreads);   // wave-uniform: the tile indices stay scalar
-    const int t = kLkTiles * xcd_remap((int)blockIdx.x, nkb) + grp;   // this group's tile of the rank's order
+    const int grp = __builtin_amdgcn_readfirstlane(tid / kThreads);   // wave-uniform: the tile indices stay scalar
+    const int t = kTiles * xcd_remap((int)blockIdx.x, nkb) + grp;   // this group's tile of the rank's order
     const bool live = t < ntile;
     int T1 = 0, T2 = 0;
     if (live) qtf_tile_of(t0 + t, qtf_n2p(q) / 16, T1, T2);
-    kay_tile(q, wk, T1, T2, live, tid - grp * kKayThreads, reinterpret_cast<double(*)[256]>(sm + grp * kAcc),
-             psg + (kKayS > 1 ? grp * kKayM * (kKayS - 1) * 16 * 64 : 0));
+    kay_tile<S>(q, wk, T1, T2, live, tid - grp * kThreads, reinterpret_cast<double(*)[256]>(sm + grp * kAcc),
+                psg + grp * kPsg);
   } else {
     // (k_qtf_lcoef's block order; frequency-block-major runs per XCD cut the launch's HBM reads
     // from 52 to 31 MB but cost 3.5 us per QTF); the w1 blocks bx0 .. bx0 + nbx - 1

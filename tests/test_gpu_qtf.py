@@ -289,6 +289,36 @@ def test_tile_sharded_qtf_equals_single_device(T):
         np.testing.assert_array_equal(acc.cpu().numpy(), f.qtf[:, :, 0, :])
 
 
+def test_tile_sharded_full_grid_equals_single_device(T):
+    """The 400-frequency grid over 2 and 8 simulated ranks: a rank's 163 or 40-odd pair tiles
+    (at most one per CU) run the Kim & Yue sums with one wave per part of a member's rows
+    (k_qtf_lk<kKayP>), the whole QTF's 325 tiles with one wave per member (k_qtf_lk<1>); the
+    parts' sums are added in the same order, so the sharded QTF equals the single-device one
+    bit for bit."""
+    import torch
+    from raft.hydro_math import wave_numbers
+    from raft.qtf import QtfDevice
+    m, f = make(T)
+    dd = f.device_design()
+    w2 = np.arange(0.04, 0.35 + 0.5 * 0.04, 0.000825) * 2 * np.pi
+    k2 = wave_numbers(w2, f.depth)
+    qd = QtfDevice(f, w2, k2, np.deg2rad(30.0), 0)
+    rng = np.random.default_rng(21)
+    X0 = T["out_Xi0"]
+    X = torch.tensor((rng.normal(size=X0.shape) + 1j * rng.normal(size=X0.shape)) * np.abs(X0).max(),
+                     dtype=torch.complex128, device=dd.device)
+    M66 = torch.tensor(f.M_struc, dtype=torch.float64, device=dd.device).contiguous()
+    whole = qd.qtf(dd.w, X, M66).cpu().numpy()
+    for world in (2, 8):
+        acc = torch.zeros([qd.n2, qd.n2, 6], dtype=torch.complex128, device=dd.device)
+        for r in range(world):
+            part = torch.zeros_like(acc)
+            qd.qtf_rows(dd.w, X, M66, part, r, world)
+            acc += part
+        qd.hermitian_fill(acc)
+        np.testing.assert_array_equal(acc.cpu().numpy(), whole)
+
+
 def test_force_spectrum_mode_matches_reference(T):
     """calcHydroForce_2ndOrd(interpMode='spectrum') on the device (rh_force_2nd_spectrum)
     against the reference method on the same QTF and spectrum (f2nd_spectrum.npz)."""

@@ -157,10 +157,10 @@ __global__ __launch_bounds__(512) void k_qtf_lcoef(rh_qtf_design q, QtfWork wk, 
 __global__ __launch_bounds__(kKayThreads) __attribute__((amdgpu_waves_per_eu(RH_KAY_WPE))) void k_qtf_kay(
     rh_qtf_design q, QtfWork wk, int t0) {
   __shared__ double acc[12][256];
-  __shared__ double psg[kKayS > 1 ? kKayM * (kKayS - 1) * 16 * 64 : 1];   // the parts' row sums
+  __shared__ double psg[kPsg];   // the parts' row sums
   int T1, T2;
   qtf_tile_of(t0 + xcd_remap((int)blockIdx.x, (int)gridDim.x), qtf_n2p(q) / 16, T1, T2);
-  kay_tile(q, wk, T1, T2, true, (int)threadIdx.x, acc, psg);
+  kay_tile<kKayS>(q, wk, T1, T2, true, (int)threadIdx.x, acc, psg);
 }
 
 }  // namespace rh
