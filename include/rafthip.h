@@ -447,8 +447,9 @@ int rh_qtf_slender(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double* w,
                    const double* M66, rh_c128* qtf, void* work, long long work_bytes, rh_stream stream);
 
 /* rh_qtf_slender with flags.  RH_QTF_INCIDENT_CACHED: `work` already holds the incident-wave
- * parts of this QTF -- the Kim & Yue tables, their GEMM basis and pair-tile sums, the node GEMM
- * basis and the zero K tails, none of which depends on the RAO -- from an earlier
+ * parts of this QTF -- the nodes' grad u / grad p / dw/dz tables, the Kim & Yue tables, their
+ * GEMM basis and pair-tile sums, the node GEMM basis and the zero K tails, none of which depends
+ * on the RAO -- from an earlier
  * rh_qtf_slender(_ext) call with the same q and work on the MFMA path (the caller vouches for
  * it); only the RAO-dependent tables, coefficients and GEMMs run.  The result equals a full call
  * bit for bit.  For a design's many QTFs with different RAOs (the second passes of

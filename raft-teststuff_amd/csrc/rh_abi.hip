@@ -855,8 +855,9 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   const bool gemm = q->order == 1 && !ctx->qtf_direct;
   if (!gemm) wk.R = nullptr;                                 // the table kernels skip the GEMM operands
   if (flags & ~RH_QTF_INCIDENT_CACHED) return fail(RH_EINVAL, "%s: unknown flags 0x%x", who, flags);
-  // RH_QTF_INCIDENT_CACHED: the incident-wave parts (the Kim & Yue tables, basis and pair-tile
-  // sums, the node GEMM basis, the zero K tails) are already in `work` from an earlier call
+  // RH_QTF_INCIDENT_CACHED: the incident-wave parts (the nodes' grad u / grad p / dw/dz tables,
+  // the Kim & Yue tables, basis and pair-tile sums, the node GEMM basis, the zero K tails) are
+  // already in `work` from an earlier call
   // with this q and these tiles; only the RAO-dependent tables and coefficients are formed
   const bool cached = (flags & RH_QTF_INCIDENT_CACHED) != 0;
   if (cached && !gemm) return fail(RH_EINVAL, "%s: the incident-wave cache is kept by the MFMA path only", who);
@@ -883,7 +884,7 @@ static int qtf_launch(rh_ctx* ctx, const rh_qtf_design* q, int nw, const double*
   // the frequency row, node, waterline and KAY tables (+ GEMM basis and zero K tails): one launch
   // (rows in this order: frequency row, nodes, waterline members -- RAO-dependent -- then the
   // Kim & Yue rows, node GEMM basis and zero tails, which depend on the incident wave only)
-  const int trows = 1 + q->nq + q->nmq + (cached ? 0 : q->nkr + (gemm ? q->nq + rh::qtf_npad(*q) : 0));
+  const int trows = 1 + q->nq + q->nmq + (cached ? 0 : q->nq + q->nkr + (gemm ? q->nq + rh::qtf_npad(*q) : 0));
   if (nb > fb0) {
     hipLaunchKernelGGL(rh::k_qtf_tables, dim3(nb - fb0, trows), dim3(64), 0, s, *q, wk, nw, w, Xi0, M66, fb0);
     RH_HIP(hipGetLastError());

@@ -4,8 +4,10 @@
 //   qtf_freq_at  : per second-order frequency: RAO resampled from the first-order grid
 //                  (np.interp, left=right=0, raft/raft_fowt.py:1415-1417), first-order force
 //                  F1st = M a (:1437-1439), rotation generator i w theta (:1556-1557)
-//   qtf_nodes_at : per (node, frequency): incident velocity u, node displacement/velocity,
-//                  grad u (raft/helpers.py:157-195), grad p (:202-225), axial projections
+//   qtf_nodes_motion_at : per (node, frequency): incident velocity u, node displacement/velocity
+//                  and their axial projections (RAO-dependent)
+//   qtf_nodes_grad_at : per (node, frequency): grad u (raft/helpers.py:157-195), grad p
+//                  (:202-225), dw/dz along the axis (incident wave only)
 //   qtf_wl_at    : per (member, frequency): waterline kinematics (raft/raft_fowt.py:1486-1502)
 //   k_qtf_pairs  : per (w1 <= w2) pair: Pinkster IV + every node term + waterline term +
 //                  Kim & Yue correction, then the Hermitian fill (:1449-1640, raft_member.py:1090-1205)
@@ -244,7 +246,7 @@ __device__ __forceinline__ void airy_u(double w, double k, double beta, double h
   if (eta_out) *eta_out = scl(e, c_ch);   // pDyn with rho = g = 1 (raft/raft_fowt.py:1493)
 }
 
-__device__ __forceinline__ void qtf_nodes_at(const rh_qtf_design& q, const QtfWork& wk, int f, int n, const cd (&X)[6]) {
+__device__ __forceinline__ void qtf_nodes_motion_at(const rh_qtf_design& q, const QtfWork& wk, int f, int n, const cd (&X)[6]) {
   const int n2 = q.n2;
   if (f >= n2) return;
   const double w = q.w2[f], k = q.k2[f], h = q.depth, beta = q.beta;
@@ -265,6 +267,24 @@ __device__ __forceinline__ void qtf_nodes_at(const rh_qtf_design& q, const QtfWo
   cd vp[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) vp[i] = sub(v[i], scl(vq, qv[i]));
+  rh_c128* T = wk.node + (size_t)n * QT_COUNT * n2 + f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    st(T + (size_t)(QT_U + i) * n2, u[i]);
+    st(T + (size_t)(QT_VP + i) * n2, vp[i]);
+    st(T + (size_t)(QT_DR + i) * n2, dr[i]);
+  }
+  st(T + (size_t)QT_VA * n2, va);
+}
+
+// the incident-wave fields of a node's table (grad u, grad p, dw/dz along the axis): no RAO in
+// them, so a further RAO on the same rh_qtf_design keeps them (RH_QTF_INCIDENT_CACHED)
+__device__ __forceinline__ void qtf_nodes_grad_at(const rh_qtf_design& q, const QtfWork& wk, int f, int n) {
+  const int n2 = q.n2;
+  if (f >= n2) return;
+  const double w = q.w2[f], k = q.k2[f], h = q.depth, beta = q.beta;
+  const double x = qn(q, RH_QN_RX, n), y = qn(q, RH_QN_RY, n), z = qn(q, RH_QN_RZ, n);
+  const double qv[3] = {qn(q, RH_QN_QX, n), qn(q, RH_QN_QY, n), qn(q, RH_QN_QZ, n)};
   // grad u (raft/helpers.py:157-195) with the degree-converted direction cosines (Q1), Q2
   cd G[9];
 #pragma unroll
@@ -320,13 +340,7 @@ __device__ __forceinline__ void qtf_nodes_at(const rh_qtf_design& q, const QtfWo
   const cd dwdz = add(add(scl(Gq[0], qv[0]), scl(Gq[1], qv[1])), scl(Gq[2], qv[2]));
   rh_c128* T = wk.node + (size_t)n * QT_COUNT * n2 + f;
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    st(T + (size_t)(QT_U + i) * n2, u[i]);
-    st(T + (size_t)(QT_VP + i) * n2, vp[i]);
-    st(T + (size_t)(QT_DR + i) * n2, dr[i]);
-    st(T + (size_t)(QT_GP + i) * n2, gp[i]);
-  }
-  st(T + (size_t)QT_VA * n2, va);
+  for (int i = 0; i < 3; ++i) st(T + (size_t)(QT_GP + i) * n2, gp[i]);
 #pragma unroll
   for (int i = 0; i < 9; ++i) st(T + (size_t)(QT_GU + i) * n2, G[i]);
   st(T + (size_t)QT_DWDZ * n2, dwdz);
@@ -425,9 +439,10 @@ __global__ __launch_bounds__(64) void k_qtf_hankel(int n2, const double* __restr
 __global__ __launch_bounds__(64) void k_qtf_tables(rh_qtf_design q, QtfWork wk, int nw, const double* __restrict__ w,
                                                     const rh_c128* __restrict__ Xi0, const double* __restrict__ M66,
                                                     int fb0) {
-  // blockIdx.y: the frequency row (k_qtf_freq before round 4), node tables, waterline tables,
-  // KAY tables; on the MFMA path also the node GEMM basis and the zero K-tail rows, as rows of
-  // their own (more waves in flight).  Frequencies from 64 fb0: a call that computes only the
+  // blockIdx.y: the frequency row (k_qtf_freq before round 4), the nodes' motion tables,
+  // waterline tables, then the nodes' incident-wave gradients (grad u, grad p, dw/dz) and KAY
+  // tables; on the MFMA path also the node GEMM basis and the zero K-tail rows, as rows of their
+  // own (more waves in flight).  Frequencies from 64 fb0: a call that computes only the
   // pair tiles of rows i1 >= 64 fb0 reads no table entry below (i2 >= i1 on every tile).
   const int f = (fb0 + blockIdx.x) * 64 + threadIdx.x;
   const bool basis = wk.R != nullptr && f < qtf_n2p(q);   // MFMA path operands (zero padded to n2p)
@@ -441,7 +456,7 @@ __global__ __launch_bounds__(64) void k_qtf_tables(rh_qtf_design q, QtfWork wk, 
     if (f < q.n2) {
       cd X[6];
       qtf_resample(q, nw, w, Xi0, f, X);
-      qtf_nodes_at(q, wk, f, y, X);
+      qtf_nodes_motion_at(q, wk, f, y, X);
     }
     return;
   }
@@ -456,6 +471,12 @@ __global__ __launch_bounds__(64) void k_qtf_tables(rh_qtf_design q, QtfWork wk, 
     return;
   }
   y -= q.nmq;
+  // the rows from here on depend on the incident wave only (kept by RH_QTF_INCIDENT_CACHED calls)
+  if (y < q.nq) {
+    qtf_nodes_grad_at(q, wk, f, y);
+    return;
+  }
+  y -= q.nq;
   if (y < q.nkr) {
     qtf_kay_at(q, wk, f, y);
     if (basis) qtf_kay_basis(q, wk, f, y);
