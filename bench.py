@@ -35,7 +35,7 @@ def c5_chunks(world):
 PEAK_FP64 = 78.6e12   # MI355X FP64 dense peak (vector = matrix rate), FLOP/s
 # HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950
 # correction of MI355X_MICROARCH.md + WRITE_SIZE), written by tools/pmc_summary.py
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06_v2", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06_v9", "pmc_summary.json")
 
 
 def pmc_section(workload):
